@@ -1,0 +1,240 @@
+/*
+ * oaxaca_boot.h -- C ABI of the MI355X bootstrap-inference engine for Oaxaca-Blinder.
+ *
+ * Drop-in boundary for the bootstrap driver of `OaxacaBuilder::run()` in
+ * dot-comma-hyphen/oaxaca-blinder-rs (paths below are relative to oaxaca_blinder/src/).
+ * Plain C types only: no torch, no HIP types (a hipStream_t is passed as void*).
+ * INTEGRATION.md shows the Rust `extern "C"` block and the edited run() a maintainer adds.
+ *
+ * Layering:
+ *   1. hot path   ob_panel_* / ob_point_estimate / ob_boot_run*   replaces builder.rs:808-847
+ *   2. inference  ob_bootstrap_stats / ob_rif                      inference.rs:4-34, math/rif.rs:14-88
+ *   3. builder    ob_builder_* / ob_prepared_* / ob_results_*      OaxacaBuilder (builder.rs:37-983)
+ *                 for hosts without a Rust toolchain (the Python front end binds these).
+ *
+ * All calls are blocking unless named *_device. One ob_ctx per thread, or external locking.
+ * Errors: return code (OB_OK = 0) + thread-local message from ob_last_error().
+ */
+#ifndef OAXACA_BOOT_H
+#define OAXACA_BOOT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- errors: one code per OaxacaError variant (error.rs:6-19) plus engine codes ---------- */
+#define OB_OK 0
+#define OB_E_POLARS 1        /* OaxacaError::PolarsError: dtype / frame errors */
+#define OB_E_COLUMN 2        /* OaxacaError::ColumnNotFound */
+#define OB_E_GROUP 3         /* OaxacaError::InvalidGroupVariable (also negative weights, ols.rs:60-66) */
+#define OB_E_LINALG 4        /* OaxacaError::NalgebraError (Cholesky failure, ols.rs:107-111) */
+#define OB_E_DIAG 5          /* OaxacaError::DiagnosticError */
+#define OB_E_INSUFFICIENT 6  /* OaxacaError::InsufficientData (n <= k, ols.rs:98-105) */
+#define OB_E_HIP 7           /* HIP runtime failure / no GPU: the engine never falls back to the CPU */
+#define OB_E_INVALID 8       /* bad argument */
+#define OB_E_UNSUPPORTED 9   /* outside the engine's scope (Heckman selection, sizes over limits) */
+#define OB_E_OVERFLOW 10     /* a resample count exceeded 255 in one row (probability < 1e-500) */
+
+const char* ob_last_error(void);
+const char* ob_version(void);
+
+/* ---- ReferenceCoefficients (decomposition.rs:5-20) ---------------------------------------- */
+#define OB_REF_GROUP_A 0
+#define OB_REF_GROUP_B 1
+#define OB_REF_POOLED 2   /* == Neumark */
+#define OB_REF_WEIGHTED 3 /* == Cotton  */
+#define OB_REF_COTTON 4
+#define OB_REF_NEUMARK 5
+
+/* ---- per-replicate row layout (Kd = K + n_base, K = p + 1 incl. the intercept) ------------ */
+#define OB_ROW_EXPLAINED 0
+#define OB_ROW_UNEXPLAINED 1
+#define OB_ROW_ENDOWMENTS 2
+#define OB_ROW_COEFFICIENTS 3
+#define OB_ROW_INTERACTION 4
+#define OB_ROW_TOTAL_GAP 5
+#define OB_ROW_DETAILED 6 /* [6, 6+Kd) explained, [6+Kd, 6+2Kd) unexplained, then
+                             beta_a[K], beta_b[K], xa_mean[K], xb_mean[K], beta_star[K] */
+
+/* ---- device context ---------------------------------------------------------------------- */
+typedef struct ob_ctx ob_ctx;
+int ob_device_count(int* n);
+int ob_ctx_create(int device, ob_ctx** out);
+void ob_ctx_destroy(ob_ctx* ctx);
+
+/* ---- hot path: the two groups' design, resident in HBM -------------------------------------
+ * Replaces the per-replicate polars resample + prepare_data + OlsEstimator of builder.rs:816-839.
+ * The caller builds X as in prepare_data (builder.rs:294-378) WITHOUT the intercept column:
+ * column-major n x p, predictors then dummy columns (builder.rs:325-327). */
+typedef struct {
+  int64_t n;       /* rows (df_a.height() / df_b.height()) */
+  const double* x; /* column-major, ldx >= n */
+  int64_t ldx;
+  const double* y; /* outcome */
+  const double* w; /* weights or NULL */
+} ob_group_desc;
+
+typedef struct {
+  int32_t p;        /* predictor columns (numeric + dummies); K = p + 1 */
+  int32_t n_num;    /* numeric predictors: the pooled group indicator is inserted at 1 + n_num
+                       (builder.rs:560-564 -> prepare_data extra_predictors) */
+  int32_t weighted; /* 1 if .weights() was set */
+  ob_group_desc a;  /* advantaged group A */
+  ob_group_desc b;  /* reference group B */
+  /* categorical normalization (estimation.rs:76-91, normalization.rs:5-51, builder.rs:634-674);
+     n_norm = 0 disables it. Column indices count the intercept as column 0. */
+  int32_t n_norm;
+  const int32_t* norm_start;   /* n_norm + 1 offsets into norm_idx */
+  const int32_t* norm_idx;     /* columns named "{var}_*" (normalization.rs:11-16) */
+  const int32_t* norm_m;       /* category_counts[var] or matches + 1 */
+  const int32_t* pooled_start; /* the same on the pooled predictor list (indicator inserted) */
+  const int32_t* pooled_idx;
+  const int32_t* has_base;     /* 1 if var has a base category (adds a detailed term) */
+} ob_panel_desc;
+
+typedef struct ob_panel ob_panel;
+
+/* Copies the design into HBM (the caller keeps ownership of its buffers). Fails with
+   OB_E_GROUP on negative weights (ols.rs:60-66) and OB_E_HIP without a GPU. */
+int ob_panel_create(ob_ctx* ctx, const ob_panel_desc* desc, ob_panel** out);
+void ob_panel_destroy(ob_panel* panel);
+int ob_panel_row_len(const ob_panel* panel);
+int ob_panel_k(const ob_panel* panel);
+int ob_panel_n_base(const ob_panel* panel);
+
+/* Point estimate: run_single_pass on the unresampled data (builder.rs:810-811).
+   resid_b (n_b entries, may be NULL) receives y_B - X_B beta_B (OaxacaResults::residuals). */
+int ob_point_estimate(ob_panel* panel, int ref_mode, double* row, double* resid_b);
+
+/* Bootstrap replicates [first_rep, first_rep + n_reps) of the OBRS-1 stream keyed by seed.
+   rows: n_reps x ob_panel_row_len(); ok[r] = 0 marks a replicate the reference would drop
+   (filter_map + .ok(), builder.rs:816-839): Cholesky failure or zero total weight. Results are
+   a pure function of (seed, replicate id): identical on 1 or 8 GPUs. */
+int ob_boot_run(ob_panel* panel, uint64_t seed, uint64_t first_rep, uint64_t n_reps, int ref_mode,
+                double* rows, uint8_t* ok);
+/* Same, rows/ok in device memory, enqueued on hip_stream (hipStream_t; NULL = engine stream).
+   Returns after enqueueing; synchronize the stream before reading. */
+int ob_boot_run_device(ob_panel* panel, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
+                       int ref_mode, double* d_rows, uint8_t* d_ok, void* hip_stream);
+
+/* HIP-event timings of the last boot run (ms summed over its launches; 0 if not run). */
+typedef struct {
+  double level1_ms; /* level-1 tile counts */
+  double gram_ms;   /* resample + X^T diag(c w) X MFMA kernel (the dominant kernel) */
+  double reduce_ms;
+  double solve_ms;  /* Cholesky solves + OB algebra */
+  int32_t gram_launches;
+  int32_t chunks;
+  int32_t blocks;
+} ob_timing;
+int ob_panel_last_timing(const ob_panel* panel, ob_timing* out);
+/* Synchronize the stream used by the last *_device call and collect its timings. */
+int ob_panel_sync(ob_panel* panel);
+
+/* ---- inference (host) --------------------------------------------------------------------- */
+/* inference.rs:4-34: out = {std_err, p_value, ci_lower, ci_upper}; n = 0 gives NaNs. */
+int ob_bootstrap_stats(const double* estimates, int64_t n, double point_estimate, double out[4]);
+/* math/rif.rs:14-88 (R type-7 quantile, Silverman bandwidth, Gaussian KDE). */
+int ob_rif(const double* y, int64_t n, double tau, double* out);
+
+/* ---- builder: OaxacaBuilder over a column frame ------------------------------------------- */
+#define OB_COL_F64 0
+#define OB_COL_I64 1
+#define OB_COL_STR 2
+
+typedef struct {
+  const char* name;
+  int32_t kind;
+  const double* f64;       /* OB_COL_F64 */
+  const int64_t* i64;      /* OB_COL_I64 */
+  const char* const* str;  /* OB_COL_STR; a NULL entry is a null */
+  const uint8_t* valid;    /* numeric kinds: 1 = valid, 0 = null; NULL = all valid */
+} ob_column;
+
+typedef struct {
+  const char* outcome;
+  const char* group;
+  const char* reference_group;
+  const char* const* predictors;
+  int32_t n_predictors;
+  const char* const* categorical;
+  int32_t n_categorical;
+  const char* const* normalize;
+  int32_t n_normalize;
+  const char* weights;           /* NULL: unweighted */
+  const char* selection_outcome; /* Heckman: not supported (OB_E_UNSUPPORTED) */
+  uint64_t bootstrap_reps;       /* builder default 20 (builder.rs:122) */
+  int32_t reference_coeffs;      /* builder default OB_REF_GROUP_A (builder.rs:123) */
+  int32_t has_seed;              /* 0: fresh entropy per run, like the unseeded reference */
+  uint64_t seed;
+} ob_builder_config;
+
+typedef struct ob_prepared ob_prepared;
+typedef struct ob_results ob_results;
+typedef struct ob_matrices ob_matrices;
+
+/* clean_dataframe -> dummies -> split_groups -> prepare_data -> HBM upload -> point estimate
+   (builder.rs:787-814). */
+int ob_builder_prepare(ob_ctx* ctx, const ob_column* cols, int32_t n_cols, int64_t n_rows,
+                       const ob_builder_config* cfg, ob_prepared** out);
+int ob_prepared_row_len(const ob_prepared* prep);
+uint64_t ob_prepared_seed(const ob_prepared* prep);
+ob_panel* ob_prepared_panel(ob_prepared* prep);
+int ob_prepared_boot(ob_prepared* prep, uint64_t first_rep, uint64_t n_reps, double* rows, uint8_t* ok);
+int ob_prepared_boot_device(ob_prepared* prep, uint64_t first_rep, uint64_t n_reps, double* d_rows,
+                            uint8_t* d_ok, void* hip_stream);
+/* Aggregation of builder.rs:841-950 over the successful rows (ok != 0), in replicate order. */
+int ob_prepared_finish(ob_prepared* prep, const double* rows, const uint8_t* ok, uint64_t n_reps,
+                       ob_results** out);
+void ob_prepared_destroy(ob_prepared* prep);
+
+/* prepare + all replicates + finish: OaxacaBuilder::run() (builder.rs:787). */
+int ob_builder_run(ob_ctx* ctx, const ob_column* cols, int32_t n_cols, int64_t n_rows,
+                   const ob_builder_config* cfg, ob_results** out);
+/* OaxacaBuilder::decompose_quantile (builder.rs:711-757). */
+int ob_builder_decompose_quantile(ob_ctx* ctx, const ob_column* cols, int32_t n_cols, int64_t n_rows,
+                                  const ob_builder_config* cfg, double quantile, ob_results** out);
+/* OaxacaBuilder::get_data_matrices (builder.rs:252-291). Host only: needs no GPU. */
+int ob_builder_data_matrices(const ob_column* cols, int32_t n_cols, int64_t n_rows,
+                             const ob_builder_config* cfg, ob_matrices** out);
+
+/* ---- results (types.rs:8-47,160-180) ------------------------------------------------------ */
+#define OB_TABLE_TWO_FOLD 0            /* two_fold.aggregate: explained, unexplained */
+#define OB_TABLE_DETAILED_EXPLAINED 1
+#define OB_TABLE_DETAILED_UNEXPLAINED 2
+#define OB_TABLE_DETAILED_SELECTION 3  /* always empty (Heckman only) */
+#define OB_TABLE_THREE_FOLD 4          /* endowments, coefficients, interaction */
+
+typedef struct {
+  const char* name; /* valid until ob_results_free */
+  double estimate, std_err, t_stat, p_value, ci_lower, ci_upper;
+} ob_component;
+
+#define OB_VEC_RESIDUALS 0 /* point-estimate residuals of group B */
+#define OB_VEC_XA_MEAN 1
+#define OB_VEC_XB_MEAN 2
+#define OB_VEC_BETA_STAR 3
+
+double ob_results_total_gap(const ob_results* r);
+int64_t ob_results_n_a(const ob_results* r);
+int64_t ob_results_n_b(const ob_results* r);
+int64_t ob_results_n_failed(const ob_results* r); /* dropped replicates (builder.rs:841-847) */
+int ob_results_count(const ob_results* r, int32_t table);
+int ob_results_component(const ob_results* r, int32_t table, int32_t i, ob_component* out);
+int ob_results_vector(const ob_results* r, int32_t which, const double** data, int64_t* len);
+void ob_results_free(ob_results* r);
+
+/* get_data_matrices: X column-major n x K including the intercept column. */
+int ob_matrices_dims(const ob_matrices* m, int64_t* n_a, int64_t* n_b, int32_t* k);
+int ob_matrices_get(const ob_matrices* m, const double** x_a, const double** y_a, const double** x_b,
+                    const double** y_b);
+const char* ob_matrices_name(const ob_matrices* m, int32_t i);
+void ob_matrices_free(ob_matrices* m);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OAXACA_BOOT_H */

@@ -1,0 +1,18 @@
+"""MI355X-native bootstrap-inference engine for Oaxaca-Blinder decomposition.
+
+Drop-in for the bootstrap driver of ``OaxacaBuilder::run()`` in dot-comma-hyphen/oaxaca-blinder-rs.
+Import with ``importlib.import_module("oaxaca-blinder-rs_amd")`` (the directory name carries a
+hyphen). See DESIGN.md for the kernels and INTEGRATION.md for the Rust/C binding.
+"""
+from . import _native
+from ._native import OaxacaError
+from .api import (BudgetAdjustment, ComponentResult, DecompositionDetail, OaxacaBlinder, OaxacaBuilder,
+                  OaxacaResults, PreparedRun, ReferenceCoefficients, TwoFoldResults, parse_formula)
+from .engine import Panel, bootstrap_stats, rif, row_layout
+from .frame import Frame
+
+__all__ = [
+    "OaxacaBuilder", "OaxacaBlinder", "OaxacaResults", "TwoFoldResults", "DecompositionDetail",
+    "ComponentResult", "BudgetAdjustment", "ReferenceCoefficients", "OaxacaError", "PreparedRun",
+    "Panel", "Frame", "bootstrap_stats", "rif", "row_layout", "parse_formula",
+]

@@ -1,0 +1,748 @@
+// ob_builder.cpp -- native host runtime mirroring `OaxacaBuilder` (oaxaca_blinder/src/builder.rs)
+// over a column frame, with the bootstrap driver delegated to the MI355X engine.
+//
+//   clean_dataframe        builder.rs:760-784
+//   create_dummies_manual  builder.rs:380-418
+//   split_groups           builder.rs:61-102
+//   prepare_data           builder.rs:294-378
+//   run                    builder.rs:787-951 (point estimate, bootstrap, aggregation)
+//   process_component      builder.rs:849-865, process_detailed_components builder.rs:953-983
+//   decompose_quantile     builder.rs:711-757
+//   get_data_matrices      builder.rs:252-291
+// Polars semantics that matter here are kept: rows with a null in any used column are dropped,
+// categorical levels are the sorted unique strings (byte order), group A is the first sorted
+// level that is not the reference, a third level is ignored, outcome/weights must be Float64.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <random>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "ob_common.hpp"
+#include "ob_engine.hpp"
+#include "ob_host.hpp"
+#include "ob_spec.h"
+
+namespace ob {
+
+struct Col {
+  std::string name;
+  int kind = OB_COL_F64;
+  std::vector<double> f;       // OB_COL_F64 values (OB_COL_I64 values cast on use)
+  std::vector<int64_t> i;      // OB_COL_I64
+  std::vector<std::string> s;  // OB_COL_STR
+  std::vector<uint8_t> valid;  // 1 = non-null
+};
+
+struct Frame {
+  int64_t nrows = 0;
+  std::vector<Col> cols;
+  int find(const std::string& n) const {
+    for (size_t c = 0; c < cols.size(); ++c)
+      if (cols[c].name == n) return (int)c;
+    return -1;
+  }
+};
+
+struct Config {
+  std::string outcome, group, reference_group;
+  std::vector<std::string> predictors, categorical, normalize;
+  bool has_weights = false;
+  std::string weights;
+  bool has_selection = false;
+  std::string selection;
+  uint64_t reps = 20;
+  int ref = OB_REF_GROUP_A;
+  bool has_seed = false;
+  uint64_t seed = 0;
+};
+
+static const char* dtype_name(int kind) {
+  switch (kind) {
+    case OB_COL_F64: return "f64";
+    case OB_COL_I64: return "i64";
+    default: return "str";
+  }
+}
+
+static int load_frame(const ob_column* cols, int n_cols, int64_t n_rows, Frame& out) {
+  if (n_cols < 0 || n_rows < 0 || (n_cols > 0 && !cols)) return fail(OB_E_INVALID, "bad frame arguments");
+  out.nrows = n_rows;
+  out.cols.clear();
+  for (int c = 0; c < n_cols; ++c) {
+    const ob_column& src = cols[c];
+    if (!src.name) return fail(OB_E_INVALID, "column %d has no name", c);
+    if (out.find(src.name) >= 0)
+      return fail(OB_E_POLARS, "%sduplicate: column with name '%s' has more than one occurrence",
+                  error_prefix(OB_E_POLARS), src.name);
+    Col col;
+    col.name = src.name;
+    col.kind = src.kind;
+    col.valid.assign(n_rows, 1);
+    if (src.kind == OB_COL_F64) {
+      if (n_rows && !src.f64) return fail(OB_E_INVALID, "column '%s' has no f64 data", src.name);
+      col.f.assign(src.f64, src.f64 + n_rows);
+      if (src.valid) col.valid.assign(src.valid, src.valid + n_rows);
+    } else if (src.kind == OB_COL_I64) {
+      if (n_rows && !src.i64) return fail(OB_E_INVALID, "column '%s' has no i64 data", src.name);
+      col.i.assign(src.i64, src.i64 + n_rows);
+      if (src.valid) col.valid.assign(src.valid, src.valid + n_rows);
+    } else if (src.kind == OB_COL_STR) {
+      if (n_rows && !src.str) return fail(OB_E_INVALID, "column '%s' has no string data", src.name);
+      col.s.resize(n_rows);
+      for (int64_t r = 0; r < n_rows; ++r) {
+        if (src.str[r]) {
+          col.s[r] = src.str[r];
+        } else {
+          col.valid[r] = 0;
+        }
+      }
+    } else {
+      return fail(OB_E_INVALID, "column '%s' has unknown kind %d", src.name, src.kind);
+    }
+    for (auto& v : col.valid) v = v ? 1 : 0;
+    out.cols.push_back(std::move(col));
+  }
+  return OB_OK;
+}
+
+static Col take_col(const Col& c, const std::vector<int64_t>& rows) {
+  Col o;
+  o.name = c.name;
+  o.kind = c.kind;
+  o.valid.resize(rows.size());
+  if (c.kind == OB_COL_F64) o.f.resize(rows.size());
+  if (c.kind == OB_COL_I64) o.i.resize(rows.size());
+  if (c.kind == OB_COL_STR) o.s.resize(rows.size());
+  for (size_t r = 0; r < rows.size(); ++r) {
+    const int64_t src = rows[r];
+    o.valid[r] = c.valid[src];
+    if (c.kind == OB_COL_F64) o.f[r] = c.f[src];
+    if (c.kind == OB_COL_I64) o.i[r] = c.i[src];
+    if (c.kind == OB_COL_STR) o.s[r] = c.s[src];
+  }
+  return o;
+}
+
+static Frame take(const Frame& f, const std::vector<int64_t>& rows) {
+  Frame o;
+  o.nrows = (int64_t)rows.size();
+  for (const Col& c : f.cols) o.cols.push_back(take_col(c, rows));
+  return o;
+}
+
+static int config_from(const ob_builder_config* c, Config& out) {
+  if (!c || !c->outcome || !c->group || !c->reference_group) return fail(OB_E_INVALID, "incomplete builder config");
+  out.outcome = c->outcome;
+  out.group = c->group;
+  out.reference_group = c->reference_group;
+  auto names = [](const char* const* v, int n, std::vector<std::string>& o) -> int {
+    o.clear();
+    if (n < 0 || (n > 0 && !v)) return fail(OB_E_INVALID, "bad name list");
+    for (int i = 0; i < n; ++i) {
+      if (!v[i]) return fail(OB_E_INVALID, "null name");
+      o.emplace_back(v[i]);
+    }
+    return OB_OK;
+  };
+  OB_TRY(names(c->predictors, c->n_predictors, out.predictors));
+  OB_TRY(names(c->categorical, c->n_categorical, out.categorical));
+  OB_TRY(names(c->normalize, c->n_normalize, out.normalize));
+  out.has_weights = c->weights != nullptr;
+  if (c->weights) out.weights = c->weights;
+  out.has_selection = c->selection_outcome != nullptr;
+  if (c->selection_outcome) out.selection = c->selection_outcome;
+  out.reps = c->bootstrap_reps;
+  out.ref = c->reference_coeffs;
+  if (out.ref < OB_REF_GROUP_A || out.ref > OB_REF_NEUMARK)
+    return fail(OB_E_INVALID, "unknown reference coefficients %d", out.ref);
+  out.has_seed = c->has_seed != 0;
+  out.seed = c->seed;
+  return OB_OK;
+}
+
+// builder.rs:760-784
+static int clean_dataframe(const Frame& f, const Config& c, Frame& out) {
+  std::vector<std::string> cols = {c.outcome, c.group};
+  cols.insert(cols.end(), c.predictors.begin(), c.predictors.end());
+  cols.insert(cols.end(), c.categorical.begin(), c.categorical.end());
+  if (c.has_weights) cols.push_back(c.weights);
+  if (c.has_selection) cols.push_back(c.selection);
+  std::vector<int> idx;
+  for (const auto& name : cols) {
+    const int i = f.find(name);
+    if (i < 0) return fail(OB_E_COLUMN, "%s%s", error_prefix(OB_E_COLUMN), name.c_str());
+    idx.push_back(i);
+  }
+  std::vector<int64_t> keep;
+  keep.reserve(f.nrows);
+  for (int64_t r = 0; r < f.nrows; ++r) {
+    bool ok = true;
+    for (int i : idx) ok = ok && f.cols[i].valid[r];
+    if (ok) keep.push_back(r);
+  }
+  out = take(f, keep);
+  return OB_OK;
+}
+
+static int expect_str(const Col& c) {
+  if (c.kind != OB_COL_STR)
+    return fail(OB_E_POLARS, "%sinvalid series dtype: expected `String`, got `%s` for `%s`", error_prefix(OB_E_POLARS),
+                dtype_name(c.kind), c.name.c_str());
+  return OB_OK;
+}
+
+static std::vector<std::string> sorted_levels(const Col& c) {
+  std::vector<std::string> lv;
+  for (size_t r = 0; r < c.s.size(); ++r)
+    if (c.valid[r]) lv.push_back(c.s[r]);
+  std::sort(lv.begin(), lv.end());
+  lv.erase(std::unique(lv.begin(), lv.end()), lv.end());
+  return lv;
+}
+
+struct Dummies {
+  std::vector<Col> cols;
+  size_t m = 0;
+  std::string base_name;
+};
+
+// builder.rs:380-418: base = first sorted level, one f64 0/1 column "{col}_{level}" per other level
+static int create_dummies(const Col& series, Dummies& out) {
+  OB_TRY(expect_str(series));
+  const auto levels = sorted_levels(series);
+  out.m = levels.size();
+  if (levels.empty())
+    return fail(OB_E_GROUP, "%sCould not get reference category for %s", error_prefix(OB_E_GROUP), series.name.c_str());
+  out.base_name = series.name + "_" + levels[0];
+  for (size_t l = 1; l < levels.size(); ++l) {
+    Col d;
+    d.name = series.name + "_" + levels[l];
+    d.kind = OB_COL_F64;
+    d.f.resize(series.s.size());
+    d.valid.assign(series.s.size(), 1);
+    for (size_t r = 0; r < series.s.size(); ++r) d.f[r] = (series.valid[r] && series.s[r] == levels[l]) ? 1.0 : 0.0;
+    out.cols.push_back(std::move(d));
+  }
+  return OB_OK;
+}
+
+struct Split {
+  std::vector<int64_t> a, b;
+  std::string name_a;
+};
+
+// builder.rs:61-102
+static int split_groups(const Frame& f, const Config& c, Split& out) {
+  const int gi = f.find(c.group);
+  if (gi < 0) return fail(OB_E_COLUMN, "%s%s", error_prefix(OB_E_COLUMN), c.group.c_str());
+  const Col& g = f.cols[gi];
+  OB_TRY(expect_str(g));
+  const auto levels = sorted_levels(g);
+  if (levels.size() < 2) return fail(OB_E_GROUP, "%sNot enough groups for comparison", error_prefix(OB_E_GROUP));
+  const std::string& b = c.reference_group;
+  out.name_a = levels[0] == b ? levels[1] : levels[0];
+  out.a.clear();
+  out.b.clear();
+  for (int64_t r = 0; r < f.nrows; ++r) {
+    if (!g.valid[r]) continue;
+    if (g.s[r] == out.name_a) out.a.push_back(r);
+    if (g.s[r] == b) out.b.push_back(r);
+  }
+  return OB_OK;
+}
+
+struct Design {
+  int64_t n = 0;
+  std::vector<double> x;  // column-major n x p (no intercept)
+  std::vector<double> y, w;
+};
+
+static int numeric_value(const Col& c, int64_t r, double& v) {
+  if (c.kind == OB_COL_F64) {
+    v = c.f[r];
+  } else if (c.kind == OB_COL_I64) {
+    v = (double)c.i[r];
+  } else {
+    return fail(OB_E_POLARS, "%scannot cast column `%s` of dtype `str` to `f64`", error_prefix(OB_E_POLARS),
+                c.name.c_str());
+  }
+  return OB_OK;
+}
+
+// builder.rs:294-378 for the rows of one group. X columns = predictors then dummies.
+static int prepare_data(const Frame& f, const std::vector<int64_t>& rows, const Config& c,
+                        const std::vector<std::string>& dummy_names, bool want_w, Design& d) {
+  const int yi = f.find(c.outcome);
+  if (yi < 0) return fail(OB_E_COLUMN, "%s%s", error_prefix(OB_E_COLUMN), c.outcome.c_str());
+  if (f.cols[yi].kind != OB_COL_F64)  // `.f64()?` (builder.rs:308)
+    return fail(OB_E_POLARS, "%sinvalid series dtype: expected `Float64`, got `%s` for `%s`", error_prefix(OB_E_POLARS),
+                dtype_name(f.cols[yi].kind), c.outcome.c_str());
+  const int64_t n = (int64_t)rows.size();
+  const size_t p = c.predictors.size() + dummy_names.size();
+  d.n = n;
+  d.x.assign((size_t)n * p, 0.0);
+  d.y.resize(n);
+  for (int64_t r = 0; r < n; ++r) d.y[r] = f.cols[yi].f[rows[r]];
+  size_t col = 0;
+  for (const auto& name : c.predictors) {
+    const int ci = f.find(name);
+    if (ci < 0) return fail(OB_E_COLUMN, "%s%s", error_prefix(OB_E_COLUMN), name.c_str());
+    for (int64_t r = 0; r < n; ++r) OB_TRY(numeric_value(f.cols[ci], rows[r], d.x[col * n + r]));
+    ++col;
+  }
+  for (const auto& name : dummy_names) {  // missing dummy -> zero column (builder.rs:340-343)
+    const int ci = f.find(name);
+    if (ci >= 0)
+      for (int64_t r = 0; r < n; ++r) OB_TRY(numeric_value(f.cols[ci], rows[r], d.x[col * n + r]));
+    ++col;
+  }
+  d.w.clear();
+  if (want_w && c.has_weights) {
+    const int wi = f.find(c.weights);
+    if (wi < 0) return fail(OB_E_COLUMN, "%s%s", error_prefix(OB_E_COLUMN), c.weights.c_str());
+    if (f.cols[wi].kind != OB_COL_F64)
+      return fail(OB_E_POLARS, "%sinvalid series dtype: expected `Float64`, got `%s` for `%s`",
+                  error_prefix(OB_E_POLARS), dtype_name(f.cols[wi].kind), c.weights.c_str());
+    d.w.resize(n);
+    for (int64_t r = 0; r < n; ++r) d.w[r] = f.cols[wi].f[rows[r]];
+  }
+  return OB_OK;
+}
+
+// clean -> dummies -> split (builder.rs:787-808), shared by run/get_data_matrices.
+struct Staged {
+  Frame df;
+  std::vector<std::string> dummy_names;
+  std::unordered_map<std::string, size_t> category_counts;
+  std::unordered_map<std::string, std::string> base_categories;
+  Split split;
+};
+
+static int stage(const Frame& input, const Config& c, Staged& st) {
+  OB_TRY(clean_dataframe(input, c, st.df));
+  for (const auto& cat : c.categorical) {
+    const int ci = st.df.find(cat);
+    Dummies dm;
+    OB_TRY(create_dummies(st.df.cols[ci], dm));
+    st.category_counts[cat] = dm.m;
+    st.base_categories[cat] = dm.base_name;
+    for (auto& col : dm.cols) {
+      if (st.df.find(col.name) >= 0)
+        return fail(OB_E_POLARS, "%sduplicate: column with name '%s' has more than one occurrence",
+                    error_prefix(OB_E_POLARS), col.name.c_str());
+      st.dummy_names.push_back(col.name);
+      st.df.cols.push_back(std::move(col));
+    }
+  }
+  OB_TRY(split_groups(st.df, c, st.split));
+  return OB_OK;
+}
+
+static bool starts_with(const std::string& s, const std::string& pre) {
+  return s.size() >= pre.size() && std::equal(pre.begin(), pre.end(), s.begin());
+}
+
+}  // namespace ob
+
+// ---------------------------------------------------------------------------------------------
+// prepared run: panel in HBM + point estimate; boot ranges; aggregation
+// ---------------------------------------------------------------------------------------------
+struct ob_results {
+  double total_gap = 0.0;
+  int64_t n_a = 0, n_b = 0, n_failed = 0;
+  struct Comp {
+    std::string name;
+    double estimate, std_err, t_stat, p_value, ci_lower, ci_upper;
+  };
+  std::vector<Comp> tables[5];
+  std::vector<double> residuals, xa_mean, xb_mean, beta_star;
+};
+
+struct ob_prepared {
+  ob_ctx* ctx = nullptr;
+  ob_panel* panel = nullptr;
+  ob::Config cfg;
+  int ref = OB_REF_GROUP_A;
+  uint64_t seed = 0;
+  int k = 0, n_base = 0, row_len = 0;
+  std::vector<std::string> names;         // K final predictor names
+  std::vector<std::string> detail_names;  // K + n_base (base categories appended)
+  std::vector<double> point_row, resid_b;
+  int64_t n_a = 0, n_b = 0;
+};
+
+struct ob_matrices {
+  int64_t n_a = 0, n_b = 0;
+  int32_t k = 0;
+  std::vector<double> xa, ya, xb, yb;
+  std::vector<std::string> names;
+};
+
+namespace ob {
+
+static uint64_t fresh_seed() {
+  std::random_device rd;
+  return ((uint64_t)rd() << 32) ^ (uint64_t)rd();
+}
+
+static int prepare(ob_ctx* ctx, const Frame& input, const Config& c, ob_prepared** out) {
+  if (c.has_selection)
+    return fail(OB_E_UNSUPPORTED,
+                "Heckman selection (heckman_selection) is outside the MI355X bootstrap engine's scope");
+  Staged st;
+  OB_TRY(stage(input, c, st));
+  if (st.split.a.empty() || st.split.b.empty())  // builder.rs:431-435
+    return fail(OB_E_GROUP, "%sOne group has no data", error_prefix(OB_E_GROUP));
+  Design da, db;
+  OB_TRY(prepare_data(st.df, st.split.a, c, st.dummy_names, true, da));
+  OB_TRY(prepare_data(st.df, st.split.b, c, st.dummy_names, true, db));
+  const int p = (int)(c.predictors.size() + st.dummy_names.size());
+  const int k = p + 1;
+  // ols() check order for A then B (ols.rs:60-66 negative weights, ols.rs:98-105 n <= k)
+  for (const Design* d : {&da, &db}) {
+    if (c.has_weights)
+      for (double w : d->w)
+        if (w < 0.0) return fail(OB_E_GROUP, "%sWeights cannot be negative", error_prefix(OB_E_GROUP));
+    if ((double)d->n <= (double)k)
+      return fail(OB_E_INSUFFICIENT,
+                  "%sInsufficient data for OLS calculation: n_obs (%lld) must be strictly greater than k (%d)",
+                  error_prefix(OB_E_INSUFFICIENT), (long long)d->n, k);
+  }
+  // names: [intercept, predictors, dummies] and the pooled list with the indicator
+  std::vector<std::string> names = {"__ob_intercept__"};
+  names.insert(names.end(), c.predictors.begin(), c.predictors.end());
+  names.insert(names.end(), st.dummy_names.begin(), st.dummy_names.end());
+  std::vector<std::string> pooled = {"__ob_intercept__"};
+  pooled.insert(pooled.end(), c.predictors.begin(), c.predictors.end());
+  pooled.push_back("__ob_group_indicator__");
+  pooled.insert(pooled.end(), st.dummy_names.begin(), st.dummy_names.end());
+  std::vector<int32_t> nstart = {0}, nidx, nm, pstart = {0}, pidx, has;
+  std::vector<std::string> base_names;
+  for (const auto& var : c.normalize) {
+    const std::string pre = var + "_";
+    for (int i = 0; i < (int)names.size(); ++i)
+      if (starts_with(names[i], pre)) nidx.push_back(i);
+    for (int i = 0; i < (int)pooled.size(); ++i)
+      if (starts_with(pooled[i], pre)) pidx.push_back(i);
+    nstart.push_back((int32_t)nidx.size());
+    pstart.push_back((int32_t)pidx.size());
+    auto cc = st.category_counts.find(var);
+    nm.push_back(cc == st.category_counts.end() ? -1 : (int32_t)cc->second);
+    auto bc = st.base_categories.find(var);
+    has.push_back(bc != st.base_categories.end() ? 1 : 0);
+    if (bc != st.base_categories.end()) base_names.push_back(bc->second);
+  }
+  ob_panel_desc pd{};
+  pd.p = p;
+  pd.n_num = (int32_t)c.predictors.size();
+  pd.weighted = c.has_weights ? 1 : 0;
+  pd.a = {da.n, da.x.data(), da.n, da.y.data(), c.has_weights ? da.w.data() : nullptr};
+  pd.b = {db.n, db.x.data(), db.n, db.y.data(), c.has_weights ? db.w.data() : nullptr};
+  pd.n_norm = (int32_t)c.normalize.size();
+  pd.norm_start = nstart.data();
+  pd.norm_idx = nidx.data();
+  pd.norm_m = nm.data();
+  pd.pooled_start = pstart.data();
+  pd.pooled_idx = pidx.data();
+  pd.has_base = has.data();
+  ob_prepared* pr = new ob_prepared();
+  pr->ctx = ctx;
+  pr->cfg = c;
+  pr->ref = c.ref;
+  pr->seed = c.has_seed ? c.seed : fresh_seed();
+  int rc = ob_panel_create(ctx, &pd, &pr->panel);
+  if (rc != OB_OK) {
+    delete pr;
+    return rc;
+  }
+  pr->k = k;
+  pr->n_base = ob_panel_n_base(pr->panel);
+  pr->row_len = ob_panel_row_len(pr->panel);
+  pr->names = names;
+  pr->detail_names = names;
+  pr->detail_names.insert(pr->detail_names.end(), base_names.begin(), base_names.end());
+  pr->n_a = da.n;
+  pr->n_b = db.n;
+  pr->point_row.assign(pr->row_len, 0.0);
+  pr->resid_b.assign(db.n, 0.0);
+  rc = ob_point_estimate(pr->panel, pr->ref, pr->point_row.data(), pr->resid_b.data());
+  if (rc != OB_OK) {
+    ob_panel_destroy(pr->panel);
+    delete pr;
+    return rc;
+  }
+  *out = pr;
+  return OB_OK;
+}
+
+// builder.rs:841-950 over successful rows in replicate order.
+static int finish(const ob_prepared* pr, const double* rows, const uint8_t* ok, uint64_t n_reps, ob_results** out) {
+  const int k = pr->k, kd = k + pr->n_base, rl = pr->row_len;
+  std::vector<uint64_t> good;
+  for (uint64_t r = 0; r < n_reps; ++r)
+    if (ok[r]) good.push_back(r);
+  const uint64_t ng = good.size();
+  if (ng < n_reps)
+    fprintf(stderr,
+            "Warning: %llu out of %llu bootstrap replications failed and were discarded. The analysis is based on "
+            "%llu successful replications.\n",
+            (unsigned long long)(n_reps - ng), (unsigned long long)n_reps, (unsigned long long)ng);
+  ob_results* res = new ob_results();
+  res->total_gap = pr->point_row[OB_ROW_TOTAL_GAP];
+  res->n_a = pr->n_a;
+  res->n_b = pr->n_b;
+  res->n_failed = (int64_t)(n_reps - ng);
+  res->residuals = pr->resid_b;
+  const double* tail = pr->point_row.data() + 6 + 2 * kd;
+  res->xa_mean.assign(tail + 2 * k, tail + 3 * k);
+  res->xb_mean.assign(tail + 3 * k, tail + 4 * k);
+  res->beta_star.assign(tail + 4 * k, tail + 5 * k);
+
+  struct Job {
+    int table;
+    std::string name;
+    double point;
+    std::vector<int> cols;  // row offsets whose values feed this component, in order
+  };
+  std::vector<Job> jobs;
+  const char* two[2] = {"explained", "unexplained"};
+  const char* three[3] = {"endowments", "coefficients", "interaction"};
+  for (int i = 0; i < 2; ++i) jobs.push_back({OB_TABLE_TWO_FOLD, two[i], pr->point_row[i], {i}});
+  for (int i = 0; i < 3; ++i) jobs.push_back({OB_TABLE_THREE_FOLD, three[i], pr->point_row[2 + i], {2 + i}});
+  // process_detailed_components: estimates merged by variable name (builder.rs:963-971)
+  for (int t = 0; t < 2; ++t) {
+    const int base = 6 + t * kd;
+    for (int i = 0; i < kd; ++i) {
+      Job j{t == 0 ? OB_TABLE_DETAILED_EXPLAINED : OB_TABLE_DETAILED_UNEXPLAINED, pr->detail_names[i],
+            pr->point_row[base + i], {}};
+      for (int q = 0; q < kd; ++q)
+        if (pr->detail_names[q] == pr->detail_names[i]) j.cols.push_back(base + q);
+      jobs.push_back(std::move(j));
+    }
+  }
+  std::vector<ob_results::Comp> comps(jobs.size());
+  auto work = [&](size_t lo, size_t hi) {
+    std::vector<double> v;
+    for (size_t ji = lo; ji < hi; ++ji) {
+      const Job& j = jobs[ji];
+      v.clear();
+      v.reserve(ng * j.cols.size());
+      for (uint64_t r : good)
+        for (int c : j.cols) v.push_back(rows[r * rl + c]);
+      double st[4];
+      bootstrap_stats(v.data(), (int64_t)v.size(), st);
+      const double t = std::fabs(st[0]) > 1e-9 ? j.point / st[0] : 0.0;  // builder.rs:851-855
+      comps[ji] = {j.name, j.point, st[0], t, st[1], st[2], st[3]};
+    }
+  };
+  const size_t nth = std::min<size_t>({jobs.size(), 16, std::max(1u, std::thread::hardware_concurrency())});
+  if (nth <= 1 || ng < 4096) {
+    work(0, jobs.size());
+  } else {
+    std::vector<std::thread> th;
+    const size_t per = (jobs.size() + nth - 1) / nth;
+    for (size_t t = 0; t < nth; ++t) {
+      const size_t lo = t * per, hi = std::min(jobs.size(), lo + per);
+      if (lo < hi) th.emplace_back(work, lo, hi);
+    }
+    for (auto& t : th) t.join();
+  }
+  for (size_t ji = 0; ji < jobs.size(); ++ji) res->tables[jobs[ji].table].push_back(comps[ji]);
+  *out = res;
+  return OB_OK;
+}
+
+static int run_all(ob_ctx* ctx, const Frame& f, const Config& c, ob_results** out) {
+  ob_prepared* pr = nullptr;
+  OB_TRY(prepare(ctx, f, c, &pr));
+  std::vector<double> rows((size_t)c.reps * pr->row_len);
+  std::vector<uint8_t> ok(c.reps, 0);
+  int rc = OB_OK;
+  if (c.reps > 0) rc = ob_boot_run(pr->panel, pr->seed, 0, c.reps, pr->ref, rows.data(), ok.data());
+  if (rc == OB_OK) rc = finish(pr, rows.data(), ok.data(), c.reps, out);
+  ob_panel_destroy(pr->panel);
+  delete pr;
+  return rc;
+}
+
+}  // namespace ob
+
+extern "C" {
+
+int ob_builder_prepare(ob_ctx* ctx, const ob_column* cols, int32_t n_cols, int64_t n_rows,
+                       const ob_builder_config* cfg, ob_prepared** out) {
+  if (!ctx || !out) return ob::fail(OB_E_INVALID, "null pointer");
+  *out = nullptr;
+  ob::Frame f;
+  ob::Config c;
+  OB_TRY(ob::config_from(cfg, c));
+  OB_TRY(ob::load_frame(cols, n_cols, n_rows, f));
+  return ob::prepare(ctx, f, c, out);
+}
+
+int ob_prepared_row_len(const ob_prepared* p) { return p ? p->row_len : 0; }
+uint64_t ob_prepared_seed(const ob_prepared* p) { return p ? p->seed : 0; }
+ob_panel* ob_prepared_panel(ob_prepared* p) { return p ? p->panel : nullptr; }
+
+int ob_prepared_boot(ob_prepared* p, uint64_t first_rep, uint64_t n_reps, double* rows, uint8_t* ok) {
+  if (!p) return ob::fail(OB_E_INVALID, "null pointer");
+  return ob_boot_run(p->panel, p->seed, first_rep, n_reps, p->ref, rows, ok);
+}
+
+int ob_prepared_boot_device(ob_prepared* p, uint64_t first_rep, uint64_t n_reps, double* d_rows, uint8_t* d_ok,
+                            void* hip_stream) {
+  if (!p) return ob::fail(OB_E_INVALID, "null pointer");
+  return ob_boot_run_device(p->panel, p->seed, first_rep, n_reps, p->ref, d_rows, d_ok, hip_stream);
+}
+
+int ob_prepared_finish(ob_prepared* p, const double* rows, const uint8_t* ok, uint64_t n_reps, ob_results** out) {
+  if (!p || !out || (n_reps && (!rows || !ok))) return ob::fail(OB_E_INVALID, "null pointer");
+  *out = nullptr;
+  return ob::finish(p, rows, ok, n_reps, out);
+}
+
+void ob_prepared_destroy(ob_prepared* p) {
+  if (!p) return;
+  ob_panel_destroy(p->panel);
+  delete p;
+}
+
+int ob_builder_run(ob_ctx* ctx, const ob_column* cols, int32_t n_cols, int64_t n_rows, const ob_builder_config* cfg,
+                   ob_results** out) {
+  if (!ctx || !out) return ob::fail(OB_E_INVALID, "null pointer");
+  *out = nullptr;
+  ob::Frame f;
+  ob::Config c;
+  OB_TRY(ob::config_from(cfg, c));
+  OB_TRY(ob::load_frame(cols, n_cols, n_rows, f));
+  return ob::run_all(ctx, f, c, out);
+}
+
+// builder.rs:711-757: RIF of each group's outcome on the cleaned data, then run() on vstack(A, B)
+int ob_builder_decompose_quantile(ob_ctx* ctx, const ob_column* cols, int32_t n_cols, int64_t n_rows,
+                                  const ob_builder_config* cfg, double quantile, ob_results** out) {
+  if (!ctx || !out) return ob::fail(OB_E_INVALID, "null pointer");
+  *out = nullptr;
+  ob::Frame f, df;
+  ob::Config c;
+  OB_TRY(ob::config_from(cfg, c));
+  OB_TRY(ob::load_frame(cols, n_cols, n_rows, f));
+  OB_TRY(ob::clean_dataframe(f, c, df));
+  ob::Split sp;
+  OB_TRY(ob::split_groups(df, c, sp));
+  const int yi = df.find(c.outcome);
+  if (df.cols[yi].kind != OB_COL_F64)
+    return ob::fail(OB_E_POLARS, "%sinvalid series dtype: expected `Float64`, got `%s`", ob::error_prefix(OB_E_POLARS),
+                    ob::dtype_name(df.cols[yi].kind));
+  std::vector<int64_t> order = sp.a;
+  order.insert(order.end(), sp.b.begin(), sp.b.end());
+  ob::Frame mod = ob::take(df, order);
+  const int mi = mod.find(c.outcome);
+  std::vector<double> ya(sp.a.size()), yb(sp.b.size()), ra(sp.a.size()), rb(sp.b.size());
+  for (size_t i = 0; i < sp.a.size(); ++i) ya[i] = mod.cols[mi].f[i];
+  for (size_t i = 0; i < sp.b.size(); ++i) yb[i] = mod.cols[mi].f[sp.a.size() + i];
+  ob::rif(ya.data(), (int64_t)ya.size(), quantile, ra.data());
+  ob::rif(yb.data(), (int64_t)yb.size(), quantile, rb.data());
+  for (size_t i = 0; i < sp.a.size(); ++i) mod.cols[mi].f[i] = ra[i];
+  for (size_t i = 0; i < sp.b.size(); ++i) mod.cols[mi].f[sp.a.size() + i] = rb[i];
+  c.has_selection = false;  // the new builder carries no Heckman settings (builder.rs:743-754)
+  return ob::run_all(ctx, mod, c, out);
+}
+
+int ob_builder_data_matrices(const ob_column* cols, int32_t n_cols, int64_t n_rows, const ob_builder_config* cfg,
+                             ob_matrices** out) {
+  if (!out) return ob::fail(OB_E_INVALID, "null pointer");
+  *out = nullptr;
+  ob::Frame f;
+  ob::Config c;
+  OB_TRY(ob::config_from(cfg, c));
+  OB_TRY(ob::load_frame(cols, n_cols, n_rows, f));
+  ob::Staged st;
+  OB_TRY(ob::stage(f, c, st));
+  ob::Design da, db;
+  OB_TRY(ob::prepare_data(st.df, st.split.a, c, st.dummy_names, false, da));
+  OB_TRY(ob::prepare_data(st.df, st.split.b, c, st.dummy_names, false, db));
+  ob_matrices* m = new ob_matrices();
+  m->k = (int32_t)(c.predictors.size() + st.dummy_names.size() + 1);
+  m->n_a = da.n;
+  m->n_b = db.n;
+  auto with_intercept = [&](const ob::Design& d, std::vector<double>& x) {
+    x.assign((size_t)d.n * m->k, 1.0);
+    std::copy(d.x.begin(), d.x.end(), x.begin() + d.n);
+  };
+  with_intercept(da, m->xa);
+  with_intercept(db, m->xb);
+  m->ya = da.y;
+  m->yb = db.y;
+  m->names = {"__ob_intercept__"};
+  m->names.insert(m->names.end(), c.predictors.begin(), c.predictors.end());
+  m->names.insert(m->names.end(), st.dummy_names.begin(), st.dummy_names.end());
+  *out = m;
+  return OB_OK;
+}
+
+double ob_results_total_gap(const ob_results* r) { return r ? r->total_gap : NAN; }
+int64_t ob_results_n_a(const ob_results* r) { return r ? r->n_a : 0; }
+int64_t ob_results_n_b(const ob_results* r) { return r ? r->n_b : 0; }
+int64_t ob_results_n_failed(const ob_results* r) { return r ? r->n_failed : 0; }
+
+int ob_results_count(const ob_results* r, int32_t table) {
+  if (!r || table < 0 || table > 4) return -1;
+  return (int)r->tables[table].size();
+}
+
+int ob_results_component(const ob_results* r, int32_t table, int32_t i, ob_component* out) {
+  if (!r || !out || table < 0 || table > 4 || i < 0 || i >= (int)r->tables[table].size())
+    return ob::fail(OB_E_INVALID, "component index out of range");
+  const auto& c = r->tables[table][i];
+  *out = {c.name.c_str(), c.estimate, c.std_err, c.t_stat, c.p_value, c.ci_lower, c.ci_upper};
+  return OB_OK;
+}
+
+int ob_results_vector(const ob_results* r, int32_t which, const double** data, int64_t* len) {
+  if (!r || !data || !len) return ob::fail(OB_E_INVALID, "null pointer");
+  const std::vector<double>* v = nullptr;
+  switch (which) {
+    case OB_VEC_RESIDUALS: v = &r->residuals; break;
+    case OB_VEC_XA_MEAN: v = &r->xa_mean; break;
+    case OB_VEC_XB_MEAN: v = &r->xb_mean; break;
+    case OB_VEC_BETA_STAR: v = &r->beta_star; break;
+    default: return ob::fail(OB_E_INVALID, "unknown vector %d", which);
+  }
+  *data = v->data();
+  *len = (int64_t)v->size();
+  return OB_OK;
+}
+
+void ob_results_free(ob_results* r) { delete r; }
+
+int ob_matrices_dims(const ob_matrices* m, int64_t* n_a, int64_t* n_b, int32_t* k) {
+  if (!m || !n_a || !n_b || !k) return ob::fail(OB_E_INVALID, "null pointer");
+  *n_a = m->n_a;
+  *n_b = m->n_b;
+  *k = m->k;
+  return OB_OK;
+}
+
+int ob_matrices_get(const ob_matrices* m, const double** x_a, const double** y_a, const double** x_b,
+                    const double** y_b) {
+  if (!m || !x_a || !y_a || !x_b || !y_b) return ob::fail(OB_E_INVALID, "null pointer");
+  *x_a = m->xa.data();
+  *y_a = m->ya.data();
+  *x_b = m->xb.data();
+  *y_b = m->yb.data();
+  return OB_OK;
+}
+
+const char* ob_matrices_name(const ob_matrices* m, int32_t i) {
+  if (!m || i < 0 || i >= (int32_t)m->names.size()) return nullptr;
+  return m->names[i].c_str();
+}
+
+void ob_matrices_free(ob_matrices* m) { delete m; }
+
+}  // extern "C"

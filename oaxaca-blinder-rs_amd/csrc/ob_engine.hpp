@@ -1,0 +1,64 @@
+// ob_engine.hpp -- device-side state of the bootstrap engine (HBM panel, workspaces, streams).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "ob_common.hpp"
+
+struct ob_ctx {
+  int device = 0;
+  int cus = 0;
+  hipStream_t stream = nullptr;
+};
+
+// Normalization lists (normalization.rs:5-51) in the layout the solve kernel reads.
+struct ob_norm_cfg {
+  int n_norm = 0;
+  int n_base = 0;
+  std::vector<int32_t> start, idx, m, pstart, pidx, has_base;
+};
+
+struct ob_panel {
+  ob_ctx* ctx = nullptr;
+  int p = 0;        // predictor columns
+  int k = 0;        // p + 1 (intercept)
+  int k1 = 0;       // p + 2: v = [1, x, y]
+  int e = 0;        // extended-Gram pairs
+  int e_pad = 0;    // multiple of 16
+  int ncb = 0;      // 16-wide column blocks
+  int n_num = 0;
+  int weighted = 0;
+  uint32_t n[2] = {0, 0};
+  int64_t ld[2] = {0, 0};      // padded rows (multiple of OB_TILE_ROWS)
+  uint32_t ntiles[2] = {0, 0};
+  double* d_cols[2] = {nullptr, nullptr};  // [col][ld]: x_1..x_p, y, (w)
+  ob_norm_cfg norm;
+  int32_t* d_norm = nullptr;               // packed norm lists
+  int row_len = 0;
+
+  // workspace, sized for `cap_reps` replicates per segment
+  uint32_t* d_m1 = nullptr;      // [tile][rep_pad]
+  double* d_partial = nullptr;   // [chunk][rep_pad][e_pad]
+  double* d_gram = nullptr;      // [rep_pad][2][e_pad]
+  uint32_t* d_chunks = nullptr;  // [chunk][3] = (g, t0, t1)
+  uint32_t* d_flags = nullptr;   // [0] = count overflow
+  double* d_rows_tmp = nullptr;  // host-API staging
+  uint8_t* d_ok_tmp = nullptr;
+  uint64_t tmp_reps = 0;
+
+  size_t cap_m1 = 0, cap_partial = 0, cap_gram = 0, cap_chunks = 0;
+  std::vector<hipEvent_t> seg_events;  // 5 per segment of the last boot run
+  ob_timing timing = {};
+  bool timing_pending = false;
+  hipStream_t last_stream = nullptr;
+  int pending_segments = 0;
+};
+
+namespace ob {
+int engine_point_estimate(ob_panel* p, int ref_mode, double* row, double* resid_b);
+int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps, int ref_mode,
+                double* d_rows, uint8_t* d_ok, hipStream_t stream);
+int engine_collect(ob_panel* p);
+}  // namespace ob

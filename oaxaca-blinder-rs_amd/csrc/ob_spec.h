@@ -1,0 +1,67 @@
+// ob_spec.h -- the OBRS-1 resample stream and the per-replicate row layout, shared by the HIP
+// kernels (device) and the host runtime. DESIGN.md §3 is the normative description.
+//
+// The reference resamples each group with polars `sample_n_literal(n_g, with_replacement=true,
+// shuffle=false, seed=None)` (oaxaca_blinder/src/builder.rs:822-827): n_g i.i.d. uniform row
+// draws per group, unseeded. OBRS-1 produces the same distribution (an exact multinomial with
+// cell probability 1/n_g) from a counter-based stream so that replicate r is reproducible from
+// (seed, r) alone on any GPU count:
+//   level 1: n_g draws idx = mulhi64(u64, n_g) -> tile = idx / OB_TILE_ROWS  (tile counts m_j)
+//   level 2: m_j draws local = mulhi64(u64, S_j) inside tile j (S_j = rows of tile j)
+// Conditional on the tile counts the level-2 draws are i.i.d. uniform in their tile, so the
+// joint law of per-row counts equals that of n_g i.i.d. uniform draws over the group.
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define OB_HD __host__ __device__ __forceinline__
+#else
+#define OB_HD static inline
+#endif
+
+#define OB_TILE_ROWS 512u
+#define OB_TILE_SHIFT 9u
+#define OB_TAG_L1 0x4F425231u /* "OBR1" */
+#define OB_TAG_L2 0x4F425232u /* "OBR2" */
+
+struct ob_u32x4 {
+  uint32_t x, y, z, w;
+};
+
+// Philox4x32-10 (Salmon, Moraes, Dror, Shaw, SC'11), Random123 constants.
+OB_HD ob_u32x4 ob_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+    const uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  ob_u32x4 o = {c0, c1, c2, c3};
+  return o;
+}
+
+// floor(u * s / 2^64), s < 2^32.
+OB_HD uint32_t ob_mulhi64(uint32_t lo, uint32_t hi, uint32_t s) {
+  const uint64_t h = (uint64_t)hi * s;
+  const uint64_t l = ((uint64_t)lo * s) >> 32;
+  return (uint32_t)((h + l) >> 32);
+}
+
+// ---- per-replicate result row (also include/oaxaca_boot.h OB_ROW_*) ------------------------
+// [0] explained [1] unexplained [2] endowments [3] coefficients [4] interaction [5] total_gap
+// [6, 6+Kd) detailed explained  [6+Kd, 6+2Kd) detailed unexplained   (Kd = K + n_base)
+// then beta_a[K], beta_b[K], xa_mean[K], xb_mean[K], beta_star[K]
+OB_HD int ob_row_len(int k, int n_base) { return 6 + 2 * (k + n_base) + 5 * k; }
+
+// Extended-Gram pair enumeration over v = [1, x_1..x_P, y] (K1 = P + 2 entries):
+// e -> (a, b), a <= b, a-major: (0,0),(0,1)..(0,K1-1),(1,1),...  E = K1 (K1 + 1) / 2.
+OB_HD int ob_pair_index(int a, int b, int k1) {  // requires a <= b
+  return a * k1 - (a * (a - 1)) / 2 + (b - a);
+}

@@ -1,0 +1,132 @@
+"""Hot-path binding: the two groups' design resident in HBM (``ob_panel``) and the bootstrap
+replicate kernel sequence (``ob_boot_run``). This is the layer a Rust ``run()`` would call in
+place of builder.rs:808-847; ``api.OaxacaBuilder`` drives it for frame inputs.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _native as N
+from .api import ReferenceCoefficients
+
+
+def row_layout(k: int, n_base: int = 0) -> dict:
+    """Offsets of the per-replicate row (include/oaxaca_boot.h OB_ROW_*)."""
+    kd = k + n_base
+    t = 6 + 2 * kd
+    return {"explained": 0, "unexplained": 1, "endowments": 2, "coefficients": 3, "interaction": 4,
+            "total_gap": 5, "detailed_explained": slice(6, 6 + kd), "detailed_unexplained": slice(6 + kd, 6 + 2 * kd),
+            "beta_a": slice(t, t + k), "beta_b": slice(t + k, t + 2 * k), "xa_mean": slice(t + 2 * k, t + 3 * k),
+            "xb_mean": slice(t + 3 * k, t + 4 * k), "beta_star": slice(t + 4 * k, t + 5 * k),
+            "len": t + 5 * k}
+
+
+def _dp(a):
+    return None if a is None else a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _ip(a):
+    return a.ctypes.data_as(C.POINTER(C.c_int32))
+
+
+class Panel:
+    """Two-group design (predictors only; intercept implicit) copied into HBM.
+
+    ``xa``/``xb``: (n_g, p) arrays; ``n_num`` numeric predictors precede dummy columns (the
+    pooled group indicator is inserted after them); ``norm`` optionally carries the
+    normalization lists (dict with start, idx, m, pstart, pidx, has_base).
+    """
+
+    def __init__(self, xa, ya, xb, yb, wa=None, wb=None, n_num=None, norm=None, device=None):
+        xa = np.asarray(xa, dtype=np.float64)
+        xb = np.asarray(xb, dtype=np.float64)
+        if xa.ndim != 2 or xb.ndim != 2 or xa.shape[1] != xb.shape[1]:
+            raise ValueError("xa/xb must be 2-D with the same number of columns")
+        self.p = xa.shape[1]
+        self._xa = np.asfortranarray(xa)
+        self._xb = np.asfortranarray(xb)
+        self._ya = np.ascontiguousarray(ya, dtype=np.float64)
+        self._yb = np.ascontiguousarray(yb, dtype=np.float64)
+        if len(self._ya) != xa.shape[0] or len(self._yb) != xb.shape[0]:
+            raise ValueError("y length mismatch")
+        weighted = wa is not None
+        if weighted != (wb is not None):
+            raise ValueError("weights must be given for both groups or neither")
+        self._wa = None if wa is None else np.ascontiguousarray(wa, dtype=np.float64)
+        self._wb = None if wb is None else np.ascontiguousarray(wb, dtype=np.float64)
+        d = N.ob_panel_desc()
+        d.p = self.p
+        d.n_num = self.p if n_num is None else int(n_num)
+        d.weighted = 1 if weighted else 0
+        d.a = N.ob_group_desc(xa.shape[0], _dp(self._xa), max(xa.shape[0], 1), _dp(self._ya), _dp(self._wa))
+        d.b = N.ob_group_desc(xb.shape[0], _dp(self._xb), max(xb.shape[0], 1), _dp(self._yb), _dp(self._wb))
+        self._norm_keep = []
+        if norm:
+            arrs = [np.ascontiguousarray(norm[k], dtype=np.int32)
+                    for k in ("start", "idx", "m", "pstart", "pidx", "has_base")]
+            self._norm_keep = arrs
+            d.n_norm = len(arrs[2])
+            (d.norm_start, d.norm_idx, d.norm_m, d.pooled_start, d.pooled_idx, d.has_base) = [_ip(a) for a in arrs]
+        self._h = C.c_void_p()
+        N.check(N.lib().ob_panel_create(N.context(device), C.byref(d), C.byref(self._h)))
+        self.k = N.lib().ob_panel_k(self._h)
+        self.n_base = N.lib().ob_panel_n_base(self._h)
+        self.row_len = N.lib().ob_panel_row_len(self._h)
+        self.layout = row_layout(self.k, self.n_base)
+        self.n_a, self.n_b = xa.shape[0], xb.shape[0]
+
+    def point_estimate(self, ref=ReferenceCoefficients.GroupA, residuals=False):
+        row = np.empty(self.row_len)
+        res = np.empty(self.n_b) if residuals else None
+        N.check(N.lib().ob_point_estimate(self._h, int(ref), _dp(row), _dp(res)))
+        return (row, res) if residuals else row
+
+    def boot(self, seed: int, first_rep: int, n_reps: int, ref=ReferenceCoefficients.GroupA):
+        rows = np.empty((n_reps, self.row_len))
+        ok = np.zeros(n_reps, dtype=np.uint8)
+        if n_reps:
+            N.check(N.lib().ob_boot_run(self._h, seed & ((1 << 64) - 1), first_rep, n_reps, int(ref), _dp(rows),
+                                        ok.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return rows, ok
+
+    def boot_device(self, seed: int, first_rep: int, n_reps: int, rows_ptr: int, ok_ptr: int,
+                    ref=ReferenceCoefficients.GroupA, stream: int | None = None):
+        N.check(N.lib().ob_boot_run_device(self._h, seed & ((1 << 64) - 1), first_rep, n_reps, int(ref),
+                                           C.c_void_p(rows_ptr), C.c_void_p(ok_ptr), C.c_void_p(stream or 0)))
+
+    def sync(self):
+        N.check(N.lib().ob_panel_sync(self._h))
+
+    def timing(self) -> dict:
+        t = N.ob_timing()
+        N.check(N.lib().ob_panel_last_timing(self._h, C.byref(t)))
+        return {f: getattr(t, f) for f, _ in N.ob_timing._fields_}
+
+    def close(self):
+        if self._h:
+            N.lib().ob_panel_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def bootstrap_stats(values, point_estimate: float = 0.0):
+    """inference.rs:4-34 -> (std_err, p_value, (ci_lower, ci_upper)) via the native routine."""
+    v = np.ascontiguousarray(values, dtype=np.float64)
+    out = np.empty(4)
+    N.check(N.lib().ob_bootstrap_stats(_dp(v), len(v), float(point_estimate), _dp(out)))
+    return out[0], out[1], (out[2], out[3])
+
+
+def rif(y, quantile: float):
+    """math/rif.rs:14-88 via the native routine."""
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    out = np.empty_like(y)
+    N.check(N.lib().ob_rif(_dp(y), len(y), float(quantile), _dp(out)))
+    return out

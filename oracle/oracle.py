@@ -1,0 +1,435 @@
+"""TEST INFRASTRUCTURE ONLY -- the CPU restatement of the reference bootstrap path.
+
+Imported by tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` leg, and only
+there, as the checker. The product package never imports it.
+
+Two layers:
+* ``liboboracle.so`` (ob_oracle.c): Philox/OBRS-1 resampling, ols() with nalgebra's Cholesky
+  order, run_single_pass, the reference-algorithm bootstrap driver (gather every column, full
+  X^T X per replicate, Rayon-like threads), bootstrap_stats, RIF.
+* ``OracleBuilder`` below: builder.rs's frame logic (clean_dataframe, create_dummies_manual,
+  split_groups, prepare_data, run, process_component/process_detailed_components,
+  decompose_quantile, get_data_matrices) restated in numpy, independent of the product's C++.
+
+Pinning: tests/test_oracle_kat.py checks this restatement against every known-answer test the
+reference holds for the path. Bootstrap SE/CI/p parity is defined on the shared
+OBRS-1 stream (the reference's resampling is unseeded, builder.rs:822-827).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboboracle.so")
+
+REF = {"group_a": 0, "group_b": 1, "pooled": 2, "weighted": 3, "cotton": 3, "neumark": 2}
+# product enum values (ReferenceCoefficients) -> oracle modes
+REF_FROM_ENUM = {0: 0, 1: 1, 2: 2, 3: 3, 4: 3, 5: 2}
+
+ORC_OK, ORC_E_INSUFFICIENT, ORC_E_CHOLESKY, ORC_E_NEGWEIGHT, ORC_E_GROUP = 0, 1, 2, 3, 4
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(LIB_PATH) or (
+            os.path.getmtime(LIB_PATH) < os.path.getmtime(os.path.join(HERE, "ob_oracle.c"))):
+        subprocess.check_call(["make", "-s", "-C", HERE], stdout=subprocess.DEVNULL)
+    return LIB_PATH
+
+
+class _Cfg(C.Structure):
+    _fields_ = [("k", C.c_int), ("pool_pos", C.c_int), ("ref_mode", C.c_int), ("weighted", C.c_int),
+                ("n_norm", C.c_int), ("norm_start", C.POINTER(C.c_int)), ("norm_idx", C.POINTER(C.c_int)),
+                ("norm_m", C.POINTER(C.c_int)), ("pooled_start", C.POINTER(C.c_int)),
+                ("pooled_idx", C.POINTER(C.c_int)), ("has_base", C.POINTER(C.c_int))]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(LIB_PATH)
+        D, U32, I64 = C.POINTER(C.c_double), C.POINTER(C.c_uint32), C.c_int64
+        L.orc_philox4x32_10.argtypes = [U32, U32, U32]
+        L.orc_level1_counts.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, U32]
+        L.orc_resample_indices.argtypes = [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, U32]
+        L.orc_ols.argtypes = [D, D, I64, C.c_int, D, D, D, C.c_int]
+        L.orc_ols.restype = C.c_int
+        L.orc_row_len.argtypes = [C.c_int, C.c_int]
+        L.orc_row_len.restype = C.c_int
+        L.orc_n_base.argtypes = [C.POINTER(_Cfg)]
+        L.orc_n_base.restype = C.c_int
+        L.orc_single_pass.argtypes = [C.POINTER(_Cfg), D, D, D, I64, D, D, D, I64, D, D, C.c_int]
+        L.orc_single_pass.restype = C.c_int
+        L.orc_boot_ref.argtypes = [C.POINTER(_Cfg), D, D, D, I64, D, D, D, I64, C.c_uint64, C.c_uint32,
+                                   C.c_uint32, C.c_int, C.c_int, D, C.POINTER(C.c_uint8)]
+        L.orc_bootstrap_stats.argtypes = [D, I64, D]
+        L.orc_rif.argtypes = [D, I64, C.c_double, D]
+        _lib = L
+    return _lib
+
+
+def _d(a):
+    return None if a is None else a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+# ---------------------------------------------------------------------------------------------
+# numeric layer
+# ---------------------------------------------------------------------------------------------
+def philox(ctr, key):
+    c = (C.c_uint32 * 4)(*[int(x) & 0xFFFFFFFF for x in ctr])
+    k = (C.c_uint32 * 2)(*[int(x) & 0xFFFFFFFF for x in key])
+    o = (C.c_uint32 * 4)()
+    lib().orc_philox4x32_10(c, k, o)
+    return list(o)
+
+
+def level1_counts(seed, rep, g, n):
+    m = np.zeros(max((n + 511) // 512, 1), dtype=np.uint32)
+    lib().orc_level1_counts(seed & (2**64 - 1), rep, g, n, m.ctypes.data_as(C.POINTER(C.c_uint32)))
+    return m[: (n + 511) // 512]
+
+
+def resample_indices(seed, rep, g, n):
+    out = np.zeros(max(n, 1), dtype=np.uint32)
+    lib().orc_resample_indices(seed & (2**64 - 1), rep, g, n, out.ctypes.data_as(C.POINTER(C.c_uint32)))
+    return out[:n]
+
+
+def ols(y, x, w=None, full=True):
+    """math/ols.rs:44-144 -> (rc, beta, residuals); x is (n, k) including the intercept."""
+    x = np.asfortranarray(x, dtype=np.float64)
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    w = None if w is None else np.ascontiguousarray(w, dtype=np.float64)
+    n, k = x.shape
+    beta = np.zeros(k)
+    res = np.zeros(max(n, 1))
+    rc = lib().orc_ols(_d(y), _d(x), n, k, _d(w), _d(beta), _d(res), 1 if full else 0)
+    return rc, beta, res[:n]
+
+
+class PassConfig:
+    """orc_cfg; keeps its arrays alive."""
+
+    def __init__(self, k, n_num, ref_mode, weighted, norm=None):
+        self._keep = []
+        self.c = _Cfg()
+        self.c.k, self.c.pool_pos, self.c.ref_mode, self.c.weighted = k, 1 + n_num, ref_mode, 1 if weighted else 0
+        norm = norm or {"start": [0], "idx": [], "m": [], "pstart": [0], "pidx": [], "has_base": []}
+        arrs = {}
+        for key in ("start", "idx", "m", "pstart", "pidx", "has_base"):
+            a = np.ascontiguousarray(np.asarray(norm[key], dtype=np.int32).reshape(-1))
+            if a.size == 0:
+                a = np.zeros(1, dtype=np.int32)
+            arrs[key] = a
+            self._keep.append(a)
+        self.c.n_norm = len(norm["m"])
+        P = C.POINTER(C.c_int)
+        self.c.norm_start = arrs["start"].ctypes.data_as(P)
+        self.c.norm_idx = arrs["idx"].ctypes.data_as(P)
+        self.c.norm_m = arrs["m"].ctypes.data_as(P)
+        self.c.pooled_start = arrs["pstart"].ctypes.data_as(P)
+        self.c.pooled_idx = arrs["pidx"].ctypes.data_as(P)
+        self.c.has_base = arrs["has_base"].ctypes.data_as(P)
+        self.k = k
+        self.n_base = lib().orc_n_base(C.byref(self.c))
+        self.row_len = lib().orc_row_len(k, self.n_base)
+
+
+def single_pass(cfg: PassConfig, xa, ya, wa, xb, yb, wb, residuals=False):
+    """run_single_pass on prepared matrices (x incl. intercept) -> (rc, row[, resid_b])."""
+    xa, xb = np.asfortranarray(xa, dtype=np.float64), np.asfortranarray(xb, dtype=np.float64)
+    ya, yb = np.ascontiguousarray(ya, dtype=np.float64), np.ascontiguousarray(yb, dtype=np.float64)
+    wa = None if wa is None else np.ascontiguousarray(wa, dtype=np.float64)
+    wb = None if wb is None else np.ascontiguousarray(wb, dtype=np.float64)
+    row = np.full(cfg.row_len, np.nan)
+    res = np.zeros(max(len(yb), 1))
+    rc = lib().orc_single_pass(C.byref(cfg.c), _d(xa), _d(ya), _d(wa), len(ya), _d(xb), _d(yb), _d(wb), len(yb),
+                               _d(row), _d(res), 1)
+    return (rc, row, res[: len(yb)]) if residuals else (rc, row)
+
+
+def boot_ref(cfg: PassConfig, xa, ya, wa, xb, yb, wb, seed, first_rep, n_reps, threads=None, full=True):
+    """Reference-algorithm bootstrap (builder.rs:816-839) on the OBRS-1 stream -> (rows, ok)."""
+    xa, xb = np.asfortranarray(xa, dtype=np.float64), np.asfortranarray(xb, dtype=np.float64)
+    ya, yb = np.ascontiguousarray(ya, dtype=np.float64), np.ascontiguousarray(yb, dtype=np.float64)
+    wa = None if wa is None else np.ascontiguousarray(wa, dtype=np.float64)
+    wb = None if wb is None else np.ascontiguousarray(wb, dtype=np.float64)
+    rows = np.full((n_reps, cfg.row_len), np.nan)
+    ok = np.zeros(n_reps, dtype=np.uint8)
+    threads = threads or min(os.cpu_count() or 1, 16)
+    if n_reps:
+        lib().orc_boot_ref(C.byref(cfg.c), _d(xa), _d(ya), _d(wa), len(ya), _d(xb), _d(yb), _d(wb), len(yb),
+                           seed & (2**64 - 1), first_rep, n_reps, 1 if full else 0, threads, _d(rows),
+                           ok.ctypes.data_as(C.POINTER(C.c_uint8)))
+    return rows, ok
+
+
+def bootstrap_stats(values):
+    """inference.rs:4-34 -> (std_err, p_value, (lo, hi))"""
+    v = np.ascontiguousarray(values, dtype=np.float64)
+    out = np.zeros(4)
+    lib().orc_bootstrap_stats(_d(v), len(v), _d(out))
+    return out[0], out[1], (out[2], out[3])
+
+
+def rif(y, tau):
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    out = np.zeros(max(len(y), 1))
+    lib().orc_rif(_d(y), len(y), float(tau), _d(out))
+    return out[: len(y)]
+
+
+# ---------------------------------------------------------------------------------------------
+# frame layer (builder.rs restated over dict-of-columns frames)
+# ---------------------------------------------------------------------------------------------
+class OracleError(RuntimeError):
+    def __init__(self, kind, msg):
+        super().__init__(msg)
+        self.kind = kind
+
+
+def _col(frame, name):
+    if name not in frame:
+        raise OracleError("ColumnNotFound", f"Column not found: {name}")
+    return frame[name]
+
+
+def _is_null(v):
+    return v is None
+
+
+def _kind(values):
+    present = [v for v in values if v is not None]
+    if present and all(isinstance(v, str) for v in present):
+        return "str"
+    if present and all(isinstance(v, (int, np.integer)) and not isinstance(v, bool) for v in present):
+        return "i64"
+    return "f64"
+
+
+class OracleBuilder:
+    """builder.rs:37-757 over ``{name: list}`` frames (None = null)."""
+
+    def __init__(self, frame, outcome, group, reference_group):
+        self.frame = {k: list(v) for k, v in frame.items()}
+        self.outcome, self.group, self.reference_group = outcome, group, reference_group
+        self.predictors, self.categorical, self.normalize_vars = [], [], []
+        self.reps, self.ref_mode, self.weights, self.seed = 20, 0, None, 0x0B5EED
+
+    # setters mirror builder.rs:165-246
+    def set(self, predictors=(), categorical=(), normalize=(), reps=20, ref_mode=0, weights=None, seed=0x0B5EED):
+        self.predictors, self.categorical, self.normalize_vars = list(predictors), list(categorical), list(normalize)
+        self.reps, self.ref_mode, self.weights, self.seed = reps, ref_mode, weights, seed
+        return self
+
+    def clean_dataframe(self, frame):  # builder.rs:760-784
+        cols = [self.outcome, self.group] + self.predictors + self.categorical + ([self.weights] if self.weights else [])
+        for c in cols:
+            _col(frame, c)
+        n = len(next(iter(frame.values()))) if frame else 0
+        keep = [i for i in range(n) if all(not _is_null(frame[c][i]) for c in cols)]
+        return {k: [v[i] for i in keep] for k, v in frame.items()}
+
+    def create_dummies(self, values, name):  # builder.rs:380-418
+        if _kind(values) != "str":
+            raise OracleError("PolarsError", "invalid series dtype: expected `String`")
+        levels = sorted(set(v for v in values if v is not None))
+        if not levels:
+            raise OracleError("InvalidGroupVariable", f"Could not get reference category for {name}")
+        dummies = {f"{name}_{lv}": [1.0 if v == lv else 0.0 for v in values] for lv in levels[1:]}
+        return dummies, len(levels), f"{name}_{levels[0]}"
+
+    def split_groups(self, frame):  # builder.rs:61-102
+        g = frame[self.group]
+        if _kind(g) != "str":
+            raise OracleError("PolarsError", "invalid series dtype: expected `String`")
+        levels = sorted(set(v for v in g if v is not None))
+        if len(levels) < 2:
+            raise OracleError("InvalidGroupVariable", "Invalid group variable: Not enough groups for comparison")
+        b = self.reference_group
+        a = levels[1] if levels[0] == b else levels[0]
+        ia = [i for i, v in enumerate(g) if v == a]
+        ib = [i for i, v in enumerate(g) if v == b]
+        return ia, ib, a
+
+    def prepare_data(self, frame, rows, dummy_names, extra=()):  # builder.rs:294-378
+        y = frame[self.outcome]
+        if _kind(y) != "f64":
+            raise OracleError("PolarsError", "invalid series dtype: expected `Float64`")
+        names = ["__ob_intercept__"] + self.predictors + list(extra) + list(dummy_names)
+        x = np.zeros((len(rows), len(names)))
+        x[:, 0] = 1.0
+        for j, nm in enumerate(names[1:], start=1):
+            if nm in frame:
+                x[:, j] = [float(frame[nm][i]) for i in rows]
+        yv = np.array([float(y[i]) for i in rows])
+        w = np.array([float(frame[self.weights][i]) for i in rows]) if self.weights else None
+        return x, yv, w, names
+
+    def _stage(self):
+        df = self.clean_dataframe(self.frame)
+        dummy_names, counts, bases = [], {}, {}
+        for cat in self.categorical:
+            d, m, base = self.create_dummies(df[cat], cat)
+            counts[cat], bases[cat] = m, base
+            dummy_names += list(d)
+            df.update(d)
+        return df, dummy_names, counts, bases
+
+    def _norm_lists(self, names, pooled_names, counts, bases):
+        st, idx, m, pst, pidx, has, base_names = [0], [], [], [0], [], [], []
+        for var in self.normalize_vars:
+            pre = var + "_"
+            idx += [i for i, nm in enumerate(names) if nm.startswith(pre)]
+            pidx += [i for i, nm in enumerate(pooled_names) if nm.startswith(pre)]
+            st.append(len(idx))
+            pst.append(len(pidx))
+            m.append(counts.get(var, -1))
+            has.append(1 if var in bases else 0)
+            if var in bases:
+                base_names.append(bases[var])
+        return {"start": st, "idx": idx, "m": m, "pstart": pst, "pidx": pidx, "has_base": has}, base_names
+
+    def prepared(self):
+        """Everything run() computes before the replicate loop."""
+        df, dummy_names, counts, bases = self._stage()
+        ia, ib, _ = self.split_groups(df)
+        if not ia or not ib:
+            raise OracleError("InvalidGroupVariable", "Invalid group variable: One group has no data")
+        xa, ya, wa, names = self.prepare_data(df, ia, dummy_names)
+        xb, yb, wb, _ = self.prepare_data(df, ib, dummy_names)
+        pooled = ["__ob_intercept__"] + self.predictors + ["__ob_group_indicator__"] + dummy_names
+        norm, base_names = self._norm_lists(names, pooled, counts, bases)
+        cfg = PassConfig(len(names), len(self.predictors), REF_FROM_ENUM[self.ref_mode], self.weights is not None,
+                         norm if self.normalize_vars else None)
+        return dict(xa=xa, ya=ya, wa=wa, xb=xb, yb=yb, wb=wb, names=names, detail_names=names + base_names,
+                    cfg=cfg, norm=norm if self.normalize_vars else None)
+
+    def point(self, prep):
+        rc, row, res = single_pass(prep["cfg"], prep["xa"], prep["ya"], prep["wa"], prep["xb"], prep["yb"],
+                                   prep["wb"], residuals=True)
+        if rc != ORC_OK:
+            raise OracleError({1: "InsufficientData", 2: "NalgebraError", 3: "InvalidGroupVariable",
+                               4: "InvalidGroupVariable"}[rc], f"single pass failed ({rc})")
+        return row, res
+
+    def boot_rows(self, prep, first_rep, n_reps, threads=None, full=False):
+        return boot_ref(prep["cfg"], prep["xa"], prep["ya"], prep["wa"], prep["xb"], prep["yb"], prep["wb"],
+                        self.seed, first_rep, n_reps, threads=threads, full=full)
+
+    def aggregate(self, prep, point_row, rows, ok, resid):
+        """builder.rs:841-950 -> dict shaped like OaxacaResults."""
+        k = prep["cfg"].k
+        kd = k + prep["cfg"].n_base
+        good = rows[ok.astype(bool)]
+
+        def comp(name, point, vals):
+            se, p, (lo, hi) = bootstrap_stats(vals)
+            t = point / se if abs(se) > 1e-9 else 0.0
+            return dict(name=name, estimate=point, std_err=se, t_stat=t, p_value=p, ci_lower=lo, ci_upper=hi)
+
+        def detailed(base):
+            out = []
+            names = prep["detail_names"]
+            for i in range(kd):
+                cols = [base + q for q in range(kd) if names[q] == names[i]]
+                vals = good[:, cols].reshape(-1) if len(good) else np.zeros(0)
+                out.append(comp(names[i], point_row[base + i], vals))
+            return out
+
+        tail = 6 + 2 * kd
+        return dict(
+            total_gap=point_row[5],
+            two_fold=dict(aggregate=[comp("explained", point_row[0], good[:, 0]),
+                                     comp("unexplained", point_row[1], good[:, 1])],
+                          detailed_explained=detailed(6), detailed_unexplained=detailed(6 + kd), detailed_selection=[]),
+            three_fold=dict(aggregate=[comp(n, point_row[2 + i], good[:, 2 + i])
+                                       for i, n in enumerate(("endowments", "coefficients", "interaction"))],
+                            detailed=[]),
+            n_a=len(prep["ya"]), n_b=len(prep["yb"]), residuals=resid,
+            xa_mean=point_row[tail + 2 * k: tail + 3 * k], xb_mean=point_row[tail + 3 * k: tail + 4 * k],
+            beta_star=point_row[tail + 4 * k: tail + 5 * k], n_failed=int(len(ok) - ok.sum()))
+
+    def run(self, threads=None):
+        prep = self.prepared()
+        point_row, resid = self.point(prep)
+        rows, ok = self.boot_rows(prep, 0, self.reps, threads=threads)
+        return self.aggregate(prep, point_row, rows, ok, resid)
+
+    def decompose_quantile(self, q, threads=None):  # builder.rs:711-757
+        df = self.clean_dataframe(self.frame)
+        ia, ib, _ = self.split_groups(df)
+        y = df[self.outcome]
+        ra = rif([y[i] for i in ia], q)
+        rb = rif([y[i] for i in ib], q)
+        order = ia + ib
+        mod = {k: [v[i] for i in order] for k, v in df.items()}
+        mod[self.outcome] = list(ra) + list(rb)
+        nb = OracleBuilder(mod, self.outcome, self.group, self.reference_group)
+        nb.set(self.predictors, self.categorical, self.normalize_vars, self.reps, self.ref_mode, self.weights, self.seed)
+        return nb.run(threads=threads)
+
+    def get_data_matrices(self):  # builder.rs:252-291
+        df, dummy_names, _, _ = self._stage()
+        ia, ib, _ = self.split_groups(df)
+        saved, self.weights = self.weights, None
+        try:
+            xa, ya, _, names = self.prepare_data(df, ia, dummy_names)
+            xb, yb, _, _ = self.prepare_data(df, ib, dummy_names)
+        finally:
+            self.weights = saved
+        return xa, ya, xb, yb, names
+
+
+# ---------------------------------------------------------------------------------------------
+# synthetic wage panel, deterministic from a seed
+# ---------------------------------------------------------------------------------------------
+def synthetic_panel(n, p, weighted, seed=20260424):
+    """Groups A ('M') and B ('F'), n/2 rows each. x1 education, x2 experience, x3 = x2^2/100,
+    x4.. ~ N(0,1) (+0.2 in A); y = [1, x] beta_g + N(0, 0.5^2), beta_A = beta_B + 0.05.
+    Returns dict(xa, ya, wa, xb, yb, wb) with predictor-only x (no intercept column)."""
+    rng = np.random.default_rng(seed)
+    out = {}
+    na = n // 2
+    nb = n - na
+    beta_b = np.concatenate([[5.0, 0.08, 0.03, -0.04], 0.1 * np.ones(max(p - 3, 0))])[: p + 1]
+    for g, ng in (("a", na), ("b", nb)):
+        x = np.empty((ng, p))
+        if p >= 1:
+            x[:, 0] = np.clip(np.round(rng.normal(13.0, 2.5, ng)), 8, 20)
+        if p >= 2:
+            x[:, 1] = rng.uniform(0.0, 40.0, ng)
+        if p >= 3:
+            x[:, 2] = x[:, 1] ** 2 / 100.0
+        if p >= 4:
+            x[:, 3:] = rng.normal(0.2 if g == "a" else 0.0, 1.0, (ng, p - 3))
+        beta = beta_b + (0.05 if g == "a" else 0.0)
+        y = beta[0] + x @ beta[1:] + rng.normal(0.0, 0.5, ng)
+        out["x" + g] = x
+        out["y" + g] = y
+        out["w" + g] = rng.uniform(0.5, 2.0, ng) if weighted else None
+    return out
+
+
+def with_intercept(x):
+    return np.hstack([np.ones((x.shape[0], 1)), x])
+
+
+def rel_close(a, b, rtol, scale=None):
+    """Mixed tolerance |a-b| <= rtol * max(|b|, scale)."""
+    a, b = np.asarray(a, dtype=float), np.asarray(b, dtype=float)
+    s = np.abs(b) if scale is None else np.maximum(np.abs(b), scale)
+    return np.all(np.abs(a - b) <= rtol * np.maximum(s, 1e-300)) or np.allclose(a, b, rtol=rtol, atol=0)
+
+
+if __name__ == "__main__":
+    print(philox([0, 0, 0, 0], [0, 0]))
+    print(math.pi)
