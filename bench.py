@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""Bootstrap replicates/s of the Oaxaca-Blinder bootstrap driver on MI355X.
+
+Workload = BASELINE.json configs[1]: a 1,000,000-row two-group panel (500k/500k) with 20 numeric
+predictors, two-fold WLS decomposition (builder default reference coefficients GroupA), 10,000
+bootstrap replicates per GPU per step. One step = one full bootstrap run with the panel already
+resident in HBM: OBRS-1 resampling + Gram + solves + OB terms for every replicate (HIP), the
+RCCL all-gather of the per-replicate rows over xGMI (N > 1), and the SE/p/CI aggregation of
+every reported component on rank 0 (builder.rs:841-930). Replicates are sharded across ranks
+(weak scaling: each rank runs its own 10,000 replicate ids per step).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints one JSON line (contract in the task brief); see DESIGN.md §5 for the roofline.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+F64_MFMA_PEAK_TFLOPS = 78.6  # MI355X dense FP64 matrix peak (v_mfma_f64_16x16x4_f64, 2.4 GHz)
+HBM_PEAK_GBPS = 8000.0
+
+
+def synthetic(rows, preds, weighted, seed=20260424):
+    """SURVEY.md §8d wage panel (same recipe as oracle.synthetic_panel, regenerated on-box)."""
+    rng = np.random.default_rng(seed)
+    na = rows // 2
+    nb = rows - na
+    beta_b = np.concatenate([[5.0, 0.08, 0.03, -0.04], 0.1 * np.ones(max(preds - 3, 0))])[: preds + 1]
+    out = {}
+    for g, ng in (("a", na), ("b", nb)):
+        x = np.empty((ng, preds), order="F")
+        x[:, 0] = np.clip(np.round(rng.normal(13.0, 2.5, ng)), 8, 20)
+        x[:, 1] = rng.uniform(0.0, 40.0, ng)
+        x[:, 2] = x[:, 1] ** 2 / 100.0
+        x[:, 3:] = rng.normal(0.2 if g == "a" else 0.0, 1.0, (ng, preds - 3))
+        beta = beta_b + (0.05 if g == "a" else 0.0)
+        out["x" + g] = x
+        out["y" + g] = beta[0] + x @ beta[1:] + rng.normal(0.0, 0.5, ng)
+        out["w" + g] = rng.uniform(0.5, 2.0, ng) if weighted else None
+    return out
+
+
+def cpu_baseline(d, preds, weighted, ref, target_s, threads):
+    """The oracle's reference-algorithm bootstrap (gather every column, full X^T W X, Cholesky,
+    solve, residuals, sigma^2, inverse -- builder.rs:816-839 + ols.rs:44-144) on host cores."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    cfg = O.PassConfig(preds + 1, preds, O.REF_FROM_ENUM[ref], weighted)
+    xa, xb = O.with_intercept(d["xa"]), O.with_intercept(d["xb"])
+    args = (cfg, xa, d["ya"], d["wa"], xb, d["yb"], d["wb"], 0x0B5EED)
+    t0 = time.perf_counter()
+    O.boot_ref(*args, 0, threads, threads=threads, full=True)  # one replicate per thread: calibrate
+    dt = time.perf_counter() - t0
+    n = min(max(threads, int(target_s / max(dt, 1e-6)) * threads), 100000)
+    t0 = time.perf_counter()
+    _, ok = O.boot_ref(*args, 1000, n, threads=threads, full=True)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "replicates/s", "cores": threads, "kind": "port",
+            "sample": f"{n} replicates of the same {d['ya'].size + d['yb'].size}-row x {preds}-predictor "
+                      f"{'WLS' if weighted else 'OLS'} panel, oracle/ob_oracle.c orc_boot_ref (full=1), "
+                      f"{threads} threads, {dt:.1f} s"}
+
+
+def load_traffic(rows, preds, reps):
+    """HBM bytes per ob_gram_kernel launch from the committed rocprofv3 PMC summary."""
+    path = os.path.join(ROOT, "profiles", "pmc_gram.json")
+    try:
+        with open(path) as f:
+            j = json.load(f)
+        if j.get("rows") == rows and j.get("preds") == preds and j.get("reps") == reps:
+            return j.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--reps", type=int, default=10000, help="replicates per GPU per step")
+    ap.add_argument("--rows", type=int, default=1_000_000)
+    ap.add_argument("--preds", type=int, default=20)
+    ap.add_argument("--ref", type=int, default=0, help="ReferenceCoefficients (0 = GroupA)")
+    ap.add_argument("--unweighted", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="0 disables the CPU baseline leg")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    ob = importlib.import_module("oaxaca-blinder-rs_amd")
+    weighted = not args.unweighted
+    d = synthetic(args.rows, args.preds, weighted)
+    panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"], d["wa"], d["wb"], device=local)
+    B, rl = args.reps, panel.row_len
+    dev = torch.device("cuda", local)
+    rows = torch.empty((B, rl), dtype=torch.float64, device=dev)
+    ok = torch.empty(B, dtype=torch.uint8, device=dev)
+    all_rows = torch.empty((world * B, rl), dtype=torch.float64, device=dev) if world > 1 else rows
+    all_ok = torch.empty(world * B, dtype=torch.uint8, device=dev) if world > 1 else ok
+    kd = panel.k + panel.n_base
+    stat_cols = np.arange(6 + 2 * kd, dtype=np.int32)  # every reported component (+ total_gap)
+    seed = 0x0B5EED
+
+    def step(i):
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        first = (i * world + rank) * B
+        panel.boot_device(seed, first, B, rows.data_ptr(), ok.data_ptr(), args.ref, stream=stream)
+        if world > 1:
+            dist.all_gather_into_tensor(all_rows, rows)
+            dist.all_gather_into_tensor(all_ok, ok)
+        if rank == 0:
+            h_rows = all_rows.cpu().numpy()
+            h_ok = all_ok.cpu().numpy()
+            stats = ob.aggregate(h_rows, h_ok, stat_cols)
+        else:
+            torch.cuda.current_stream(dev).synchronize()
+            stats = None
+        panel.sync()
+        return stats, panel.timing()
+
+    for i in range(args.warmup):
+        step(i)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    gram_ms = 0.0
+    launches = 0
+    stats = None
+    for i in range(args.steps):
+        stats, tm = step(args.warmup + i)
+        gram_ms += tm["gram_ms"]
+        launches += tm["gram_launches"]
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed, gram_ms / max(launches, 1)], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, gram_launch_ms = float(t[0]), float(t[1])
+
+    if rank == 0:
+        total_reps = world * B * args.steps
+        value = total_reps / elapsed
+        k = args.preds + 1
+        flops_rep = 2.0 * args.rows * (k * (k + 1) / 2 + k)
+        bytes_rep = args.rows * (args.preds + (2 if weighted else 1)) * 8.0
+        reps_per_launch = B / max(launches / args.steps, 1)
+        achieved = flops_rep * reps_per_launch / (gram_launch_ms * 1e-3) / 1e12
+        traffic = load_traffic(args.rows, args.preds, B)
+        out = {
+            "metric": "bootstrap replicates/sec on 1M-row×20-pred panel at 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "replicates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (SURVEY.md §8d wage panel, numpy seed 20260424; OBRS-1 bootstrap seed 0x0B5EED)",
+            "config": {"workload": "configs[1]: two-fold WLS bootstrap, GroupA reference coefficients",
+                       "rows": args.rows, "predictors": args.preds, "weighted": weighted,
+                       "replicates_per_gpu_per_step": B, "parallelism": f"replicates sharded x{world}, RCCL all-gather"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": F64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / F64_MFMA_PEAK_TFLOPS, "traffic": traffic,
+                         "kernel": "ob_gram_kernel", "avg_launch_ms": gram_launch_ms,
+                         "flops_per_replicate": flops_rep},
+            "gather_equivalent": {"algorithmic_bytes_per_replicate": bytes_rep,
+                                  "GBps": bytes_rep * value / world / 1e9,
+                                  "frac_of_hbm_peak": bytes_rep * value / world / 1e9 / HBM_PEAK_GBPS},
+        }
+        if world == 1 and args.cpu_seconds > 0:
+            out["cpu_baseline"] = cpu_baseline(d, args.preds, weighted, args.ref, args.cpu_seconds, args.cpu_threads)
+        else:
+            out["cpu_baseline"] = None
+        out["check"] = {"explained_se": float(stats[0][0]), "unexplained_se": float(stats[1][0]),
+                        "ok_replicates": int(all_ok.sum().item())}
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

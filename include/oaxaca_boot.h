@@ -89,7 +89,8 @@ typedef struct {
   int32_t n_norm;
   const int32_t* norm_start;   /* n_norm + 1 offsets into norm_idx */
   const int32_t* norm_idx;     /* columns named "{var}_*" (normalization.rs:11-16) */
-  const int32_t* norm_m;       /* category_counts[var] or matches + 1 */
+  const int32_t* norm_m;       /* category_counts[var], or -1 for a non-categorical var
+                                  (then matches + 1, normalization.rs:28-31) */
   const int32_t* pooled_start; /* the same on the pooled predictor list (indicator inserted) */
   const int32_t* pooled_idx;
   const int32_t* has_base;     /* 1 if var has a base category (adds a detailed term) */
@@ -137,6 +138,11 @@ int ob_panel_sync(ob_panel* panel);
 /* ---- inference (host) --------------------------------------------------------------------- */
 /* inference.rs:4-34: out = {std_err, p_value, ci_lower, ci_upper}; n = 0 gives NaNs. */
 int ob_bootstrap_stats(const double* estimates, int64_t n, double point_estimate, double out[4]);
+/* process_component over replicate rows (builder.rs:849-865): bootstrap_stats of row column
+   cols[c] over the rows with ok != 0, in replicate order; out: n_cols x {std_err, p_value,
+   ci_lower, ci_upper}. Multithreaded on the host. */
+int ob_aggregate(const double* rows, const uint8_t* ok, uint64_t n_reps, int32_t row_len, const int32_t* cols,
+                 int32_t n_cols, double* out);
 /* math/rif.rs:14-88 (R type-7 quantile, Silverman bandwidth, Gaussian KDE). */
 int ob_rif(const double* y, int64_t n, double tau, double* out);
 

@@ -8,11 +8,11 @@ from . import _native
 from ._native import OaxacaError
 from .api import (BudgetAdjustment, ComponentResult, DecompositionDetail, OaxacaBlinder, OaxacaBuilder,
                   OaxacaResults, PreparedRun, ReferenceCoefficients, TwoFoldResults, parse_formula)
-from .engine import Panel, bootstrap_stats, rif, row_layout
+from .engine import Panel, aggregate, bootstrap_stats, rif, row_layout
 from .frame import Frame
 
 __all__ = [
     "OaxacaBuilder", "OaxacaBlinder", "OaxacaResults", "TwoFoldResults", "DecompositionDetail",
     "ComponentResult", "BudgetAdjustment", "ReferenceCoefficients", "OaxacaError", "PreparedRun",
-    "Panel", "Frame", "bootstrap_stats", "rif", "row_layout", "parse_formula",
+    "Panel", "Frame", "aggregate", "bootstrap_stats", "rif", "row_layout", "parse_formula",
 ]

@@ -27,7 +27,7 @@ EXPORTED = (
     "ob_last_error", "ob_version", "ob_device_count", "ob_ctx_create", "ob_ctx_destroy",
     "ob_panel_create", "ob_panel_destroy", "ob_panel_row_len", "ob_panel_k", "ob_panel_n_base",
     "ob_point_estimate", "ob_boot_run", "ob_boot_run_device", "ob_panel_last_timing", "ob_panel_sync",
-    "ob_bootstrap_stats", "ob_rif",
+    "ob_bootstrap_stats", "ob_aggregate", "ob_rif",
     "ob_builder_prepare", "ob_prepared_row_len", "ob_prepared_seed", "ob_prepared_panel",
     "ob_prepared_boot", "ob_prepared_boot_device", "ob_prepared_finish", "ob_prepared_destroy",
     "ob_builder_run", "ob_builder_decompose_quantile", "ob_builder_data_matrices",
@@ -106,6 +106,7 @@ _SIGS = {
     "ob_panel_last_timing": (C.c_int, [_P, C.POINTER(ob_timing)]),
     "ob_panel_sync": (C.c_int, [_P]),
     "ob_bootstrap_stats": (C.c_int, [_D, C.c_int64, C.c_double, _D]),
+    "ob_aggregate": (C.c_int, [_D, _U8, C.c_uint64, C.c_int32, C.POINTER(C.c_int32), C.c_int32, _D]),
     "ob_rif": (C.c_int, [_D, C.c_int64, C.c_double, _D]),
     "ob_builder_prepare": (C.c_int, [_P, C.POINTER(ob_column), C.c_int32, C.c_int64,
                                      C.POINTER(ob_builder_config), C.POINTER(_P)]),
@@ -140,9 +141,23 @@ _lib = None
 _lib_lock = threading.Lock()
 
 
+def _share_torch_runtime():
+    """PyTorch-ROCm bundles its own libamdhip64.so.7. Loading ours first would put two HIP
+    runtimes in the process (torch's stream/allocations would then be foreign handles), so when
+    torch is installed it is imported first and the engine binds to its runtime (same soname)."""
+    if os.environ.get("OB_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def lib() -> C.CDLL:
     """Load the engine library once; raise loudly if it was not built."""
     global _lib
+    if _lib is None:
+        _share_torch_runtime()
     with _lib_lock:
         if _lib is None:
             if not os.path.exists(LIB_PATH):

@@ -482,10 +482,8 @@ static int prepare(ob_ctx* ctx, const Frame& input, const Config& c, ob_prepared
 // builder.rs:841-950 over successful rows in replicate order.
 static int finish(const ob_prepared* pr, const double* rows, const uint8_t* ok, uint64_t n_reps, ob_results** out) {
   const int k = pr->k, kd = k + pr->n_base, rl = pr->row_len;
-  std::vector<uint64_t> good;
-  for (uint64_t r = 0; r < n_reps; ++r)
-    if (ok[r]) good.push_back(r);
-  const uint64_t ng = good.size();
+  uint64_t ng = 0;
+  for (uint64_t r = 0; r < n_reps; ++r) ng += ok[r] ? 1 : 0;
   if (ng < n_reps)
     fprintf(stderr,
             "Warning: %llu out of %llu bootstrap replications failed and were discarded. The analysis is based on "
@@ -524,32 +522,15 @@ static int finish(const ob_prepared* pr, const double* rows, const uint8_t* ok, 
       jobs.push_back(std::move(j));
     }
   }
+  std::vector<std::vector<int>> groups;
+  for (const Job& j : jobs) groups.push_back(j.cols);
+  std::vector<double> st(4 * jobs.size());
+  aggregate(rows, ok, n_reps, rl, groups, st.data());
   std::vector<ob_results::Comp> comps(jobs.size());
-  auto work = [&](size_t lo, size_t hi) {
-    std::vector<double> v;
-    for (size_t ji = lo; ji < hi; ++ji) {
-      const Job& j = jobs[ji];
-      v.clear();
-      v.reserve(ng * j.cols.size());
-      for (uint64_t r : good)
-        for (int c : j.cols) v.push_back(rows[r * rl + c]);
-      double st[4];
-      bootstrap_stats(v.data(), (int64_t)v.size(), st);
-      const double t = std::fabs(st[0]) > 1e-9 ? j.point / st[0] : 0.0;  // builder.rs:851-855
-      comps[ji] = {j.name, j.point, st[0], t, st[1], st[2], st[3]};
-    }
-  };
-  const size_t nth = std::min<size_t>({jobs.size(), 16, std::max(1u, std::thread::hardware_concurrency())});
-  if (nth <= 1 || ng < 4096) {
-    work(0, jobs.size());
-  } else {
-    std::vector<std::thread> th;
-    const size_t per = (jobs.size() + nth - 1) / nth;
-    for (size_t t = 0; t < nth; ++t) {
-      const size_t lo = t * per, hi = std::min(jobs.size(), lo + per);
-      if (lo < hi) th.emplace_back(work, lo, hi);
-    }
-    for (auto& t : th) t.join();
+  for (size_t ji = 0; ji < jobs.size(); ++ji) {
+    const double* s4 = st.data() + 4 * ji;
+    const double t = std::fabs(s4[0]) > 1e-9 ? jobs[ji].point / s4[0] : 0.0;  // builder.rs:851-855
+    comps[ji] = {jobs[ji].name, jobs[ji].point, s4[0], t, s4[1], s4[2], s4[3]};
   }
   for (size_t ji = 0; ji < jobs.size(); ++ji) res->tables[jobs[ji].table].push_back(comps[ji]);
   *out = res;

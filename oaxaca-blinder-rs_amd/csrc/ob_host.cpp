@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "ob_common.hpp"
@@ -93,9 +94,54 @@ void rif(const double* y, int64_t n, double tau, double* out) {
   for (int64_t i = 0; i < n; ++i) out[i] = q + (tau - (y[i] <= q ? 1.0 : 0.0)) / dens;
 }
 
+void aggregate(const double* rows, const uint8_t* ok, uint64_t n_reps, int row_len,
+               const std::vector<std::vector<int>>& groups, double* out) {
+  std::vector<uint64_t> good;
+  good.reserve(n_reps);
+  for (uint64_t r = 0; r < n_reps; ++r)
+    if (ok[r]) good.push_back(r);
+  auto work = [&](size_t lo, size_t hi) {
+    std::vector<double> v;
+    for (size_t g = lo; g < hi; ++g) {
+      v.clear();
+      v.reserve(good.size() * groups[g].size());
+      for (uint64_t r : good)
+        for (int c : groups[g]) v.push_back(rows[r * (uint64_t)row_len + c]);
+      bootstrap_stats(v.data(), (int64_t)v.size(), out + 4 * g);
+    }
+  };
+  const size_t ng = groups.size();
+  const size_t nth = std::min<size_t>({ng, 16, std::max(1u, std::thread::hardware_concurrency())});
+  if (nth <= 1 || good.size() < 4096) {
+    work(0, ng);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < nth; ++t) {  // strided split keeps the per-thread work even
+    th.emplace_back([&, t]() {
+      for (size_t g = t; g < ng; g += nth) work(g, g + 1);
+    });
+  }
+  for (auto& t : th) t.join();
+}
+
 }  // namespace ob
 
 extern "C" {
+
+int ob_aggregate(const double* rows, const uint8_t* ok, uint64_t n_reps, int32_t row_len, const int32_t* cols,
+                 int32_t n_cols, double* out) {
+  if (n_cols < 0 || row_len <= 0 || (n_cols > 0 && (!cols || !out)) || (n_reps > 0 && (!rows || !ok)))
+    return ob::fail(OB_E_INVALID, "bad arguments");
+  std::vector<std::vector<int>> groups((size_t)n_cols);
+  for (int32_t c = 0; c < n_cols; ++c) {
+    if (cols[c] < 0 || cols[c] >= row_len) return ob::fail(OB_E_INVALID, "column %d out of range", cols[c]);
+    groups[c] = {cols[c]};
+  }
+  ob::aggregate(rows, ok, n_reps, row_len, groups, out);
+  return OB_OK;
+}
+
 
 const char* ob_last_error(void) { return ob::last_error().c_str(); }
 

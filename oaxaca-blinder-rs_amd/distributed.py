@@ -1,0 +1,80 @@
+"""Replicate sharding across ranks (one process per GPU) with one all-gather of the
+per-replicate rows -- the only collective the bootstrap needs.
+
+The reference runs every replicate in one process on a Rayon pool (builder.rs:816-839).
+Here rank r computes replicate ids [r*per, (r+1)*per) of the OBRS-1 stream (results are a pure
+function of (seed, replicate id), so the gathered rows equal a single-GPU run bit for bit), the
+rows are all-gathered (RCCL over xGMI on GPUs; gloo on CPU tests), and rank 0 aggregates
+(builder.rs:841-950). Launch with torch.distributed.run; MASTER_ADDR=127.0.0.1.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def shard(n_reps: int, rank: int, world: int):
+    """Replicate range of ``rank``: equal-sized shards (the last one padded)."""
+    per = -(-n_reps // world) if world else n_reps
+    first = min(rank * per, n_reps)
+    return first, max(0, min(n_reps, first + per) - first), per
+
+
+def gather_rows(prepared, n_reps: int, group=None, device=None):
+    """Compute this rank's replicates and all-gather every rank's rows.
+
+    ``prepared`` is anything with ``row_len``, ``boot(first, n) -> (rows, ok)`` and, for the
+    device path, ``boot_device(first, n, rows_ptr, ok_ptr, stream)`` + ``sync()``
+    (``api.PreparedRun`` provides all of them). Returns (rows, ok) for all ``n_reps`` replicates
+    in replicate order on every rank.
+    """
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    first, count, per = shard(n_reps, rank, world)
+    rl = prepared.row_len
+    on_gpu = device is not None and dist.is_initialized() and dist.get_backend(group) == "nccl"
+    if on_gpu:
+        rows = torch.empty((per, rl), dtype=torch.float64, device=device)
+        ok = torch.zeros(per, dtype=torch.uint8, device=device)
+        if count:
+            stream = torch.cuda.current_stream(device).cuda_stream
+            prepared.boot_device(first, count, rows.data_ptr(), ok.data_ptr(), stream)
+        if count < per:
+            rows[count:].fill_(float("nan"))
+    else:
+        r, o = prepared.boot(first, count) if count else (np.zeros((0, rl)), np.zeros(0, np.uint8))
+        rows = torch.full((per, rl), float("nan"), dtype=torch.float64)
+        ok = torch.zeros(per, dtype=torch.uint8)
+        rows[:count] = torch.from_numpy(np.ascontiguousarray(r))
+        ok[:count] = torch.from_numpy(np.ascontiguousarray(o))
+    if world > 1:
+        all_rows = torch.empty((world * per, rl), dtype=rows.dtype, device=rows.device)
+        all_ok = torch.empty(world * per, dtype=ok.dtype, device=ok.device)
+        dist.all_gather_into_tensor(all_rows, rows, group=group)
+        dist.all_gather_into_tensor(all_ok, ok, group=group)
+    else:
+        all_rows, all_ok = rows, ok
+    if on_gpu:
+        prepared.sync()
+    return all_rows[:n_reps].cpu().numpy(), all_ok[:n_reps].cpu().numpy()
+
+
+def fit_sharded(builder, group=None, device=None):
+    """``OaxacaBuilder.run()`` over all ranks: every rank prepares the same panel (rank 0's seed
+    is broadcast when the builder is unseeded), computes its shard, all ranks gather, rank 0
+    returns the OaxacaResults (other ranks return None)."""
+    import torch.distributed as dist
+
+    if dist.is_initialized() and builder._seed is None:
+        seed = [int(np.random.SeedSequence().generate_state(1, np.uint64)[0])]
+        dist.broadcast_object_list(seed, src=0, group=group)
+        builder.seed(seed[0])
+    prep = builder.prepare()
+    try:
+        rows, ok = gather_rows(prep, builder._bootstrap_reps, group=group, device=device)
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        return prep.finish(rows, ok) if rank == 0 else None
+    finally:
+        prep.close()

@@ -124,6 +124,18 @@ def bootstrap_stats(values, point_estimate: float = 0.0):
     return out[0], out[1], (out[2], out[3])
 
 
+def aggregate(rows, ok, cols):
+    """ob_aggregate: bootstrap_stats of each row column over ok rows -> (n_cols, 4) array of
+    (std_err, p_value, ci_lower, ci_upper)."""
+    rows = np.ascontiguousarray(rows, dtype=np.float64)
+    ok = np.ascontiguousarray(ok, dtype=np.uint8)
+    cols = np.ascontiguousarray(cols, dtype=np.int32)
+    out = np.empty((len(cols), 4))
+    N.check(N.lib().ob_aggregate(_dp(rows), ok.ctypes.data_as(C.POINTER(C.c_uint8)), len(ok), rows.shape[1],
+                                 _ip(cols), len(cols), _dp(out)))
+    return out
+
+
 def rif(y, quantile: float):
     """math/rif.rs:14-88 via the native routine."""
     y = np.ascontiguousarray(y, dtype=np.float64)

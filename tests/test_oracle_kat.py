@@ -1,0 +1,216 @@
+"""Pins the oracle (CPU restatement) to every known-answer test the reference holds for the
+bootstrap path, plus an exact rational cross-check of its OLS. CPU only."""
+import json
+import os
+from fractions import Fraction
+
+import numpy as np
+import pytest
+
+KAT = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "reference_kat.json")))
+
+
+def test_philox_random123_vectors(O):
+    for ctr, key, want in KAT["philox4x32_10"]["cases"]:
+        assert O.philox(ctr, key) == want
+
+
+def test_ols_simple(O):  # ols.rs:151-162
+    k = KAT["ols_simple"]
+    rc, beta, _ = O.ols(np.array(k["y"], float), np.array(k["x"], float))
+    assert rc == O.ORC_OK
+    assert np.allclose(beta, k["beta"], atol=k["tol"], rtol=0)
+
+
+def test_ols_singular(O):  # ols.rs:164-181
+    k = KAT["ols_singular"]
+    rc, _, _ = O.ols(np.array(k["y"], float), np.array(k["x"], float))
+    assert rc == O.ORC_E_CHOLESKY
+
+
+def test_ols_insufficient(O):  # ols.rs:183-209
+    k = KAT["ols_insufficient"]
+    rc, _, _ = O.ols(np.array(k["y"], float), np.array(k["x"], float))
+    assert rc == O.ORC_E_INSUFFICIENT
+
+
+def test_ols_negative_weight(O):  # ols.rs:60-66
+    x = np.array([[1, 0], [1, 1], [1, 2.0]])
+    rc, _, _ = O.ols(np.array([1, 2, 3.0]), x, np.array([1.0, -1.0, 1.0]))
+    assert rc == O.ORC_E_NEGWEIGHT
+
+
+def _exact_ols(x, y, w=None):
+    """Normal equations in exact rationals (independent of the oracle's float Cholesky)."""
+    n, k = len(x), len(x[0])
+    w = w or [1] * n
+    A = [[sum(Fraction(w[i]) * Fraction(x[i][a]) * Fraction(x[i][b]) for i in range(n)) for b in range(k)]
+         for a in range(k)]
+    rhs = [sum(Fraction(w[i]) * Fraction(x[i][a]) * Fraction(y[i]) for i in range(n)) for a in range(k)]
+    for c in range(k):  # Gauss-Jordan
+        piv = next(r for r in range(c, k) if A[r][c] != 0)
+        A[c], A[piv], rhs[c], rhs[piv] = A[piv], A[c], rhs[piv], rhs[c]
+        for r in range(k):
+            if r != c and A[r][c] != 0:
+                f = A[r][c] / A[c][c]
+                A[r] = [A[r][j] - f * A[c][j] for j in range(k)]
+                rhs[r] -= f * rhs[c]
+    return [float(rhs[i] / A[i][i]) for i in range(k)]
+
+
+def test_ols_matches_exact_rationals(O):
+    rng = np.random.default_rng(3)
+    x = np.column_stack([np.ones(40), rng.integers(0, 20, 40), rng.integers(-5, 5, 40)]).astype(float)
+    y = rng.integers(0, 100, 40).astype(float)
+    w = rng.integers(1, 4, 40).astype(float)
+    for weights in (None, w):
+        rc, beta, _ = O.ols(y, x, weights)
+        exact = _exact_ols(x.tolist(), y.tolist(), None if weights is None else weights.tolist())
+        assert rc == 0
+        assert np.allclose(beta, exact, rtol=1e-12, atol=1e-12)
+
+
+def _pass(O, xa, ya, xb, yb, ref, norm=None, n_num=None, weights=(None, None)):
+    k = xa.shape[1]
+    cfg = O.PassConfig(k, k - 1 if n_num is None else n_num, ref, weights[0] is not None, norm)
+    rc, row = O.single_pass(cfg, xa, ya, weights[0], xb, yb, weights[1])
+    assert rc == 0
+    return cfg, row
+
+
+def _exact_groups():
+    # group A: x mean 5, y = 2 + 4x exactly; group B: x mean 3, y = 1 + 3x exactly (decomposition.rs:131-134)
+    xa = np.array([[1, 4], [1, 5], [1, 6.0]])
+    xb = np.array([[1, 2], [1, 3], [1, 4.0]])
+    return xa, 2 + 4 * xa[:, 1], xb, 1 + 3 * xb[:, 1]
+
+
+def test_three_fold_kat(O):  # decomposition.rs:129-139
+    k = KAT["three_fold"]
+    xa, ya, xb, yb = _exact_groups()
+    _, row = _pass(O, xa, ya, xb, yb, O.REF["group_b"])
+    assert abs(row[2] - k["endowments"]) < k["tol"]
+    assert abs(row[3] - k["coefficients"]) < k["tol"]
+    assert abs(row[4] - k["interaction"]) < k["tol"]
+
+
+@pytest.mark.parametrize("ref", ["group_b", "group_a"])
+def test_detailed_sums_kat(O, ref):  # decomposition.rs:141-184
+    xa, ya, xb, yb = _exact_groups()
+    cfg, row = _pass(O, xa, ya, xb, yb, O.REF[ref])
+    kd = cfg.k + cfg.n_base
+    assert abs(row[6:6 + kd].sum() - row[0]) < 1e-9
+    assert abs(row[6 + kd:6 + 2 * kd].sum() - row[1]) < 1e-9
+
+
+def test_p_values_kat(O):  # inference.rs:40-57
+    for vals, p in KAT["p_values"]["cases"]:
+        assert abs(O.bootstrap_stats(vals)[1] - p) < 1e-9
+
+
+def test_bootstrap_stats_conventions(O):  # inference.rs:4-34
+    se, p, (lo, hi) = O.bootstrap_stats([])
+    assert np.isnan(se) and np.isnan(p) and np.isnan(lo) and np.isnan(hi)
+    v = np.arange(100.0)
+    se, p, (lo, hi) = O.bootstrap_stats(v[::-1])
+    assert abs(se - np.std(v, ddof=1)) < 1e-12
+    assert lo == 2.0 and hi == 97.0  # floor(0.025 n), floor(0.975 n)
+    _, _, (lo, hi) = O.bootstrap_stats([3.0])
+    assert lo == 3.0 and hi == 3.0
+
+
+def test_normalization_kat(O):  # normalization.rs:58-111
+    # both groups: y = 10 + 2 [B] + 4 [C] exactly -> beta = [10, 2, 4] -> normalized [12, 0, 2]
+    lv = np.array([0, 1, 2, 0, 1, 2, 0, 1, 2])
+    x = np.column_stack([np.ones(9), lv == 1, lv == 2]).astype(float)
+    y = 10 + 2 * x[:, 1] + 4 * x[:, 2]
+    norm = {"start": [0, 2], "idx": [1, 2], "m": [3], "pstart": [0, 2], "pidx": [2, 3], "has_base": [1]}
+    cfg, row = _pass(O, x, y, x, y, O.REF["group_a"], norm=norm, n_num=0)
+    k, kd = cfg.k, cfg.k + cfg.n_base
+    beta_a = row[6 + 2 * kd: 6 + 2 * kd + k]
+    assert np.allclose(beta_a, KAT["normalization"]["expected"], atol=1e-9)
+
+
+def _frame(d, keys):
+    return {k: d[k] for k in keys}
+
+
+@pytest.mark.parametrize("mode", [1, 0, 2, 3])
+def test_integration_runs(O, mode):  # tests/integration_test.rs:105-144
+    k = KAT["integration_frame"]
+    ob = O.OracleBuilder(_frame(k, ["wage", "education", "gender"]), "wage", "gender", "F")
+    ob.set(predictors=["education"], reps=5, ref_mode=mode)
+    r = ob.run(threads=2)
+    assert abs(r["total_gap"] - 10.0) < 1e-9
+    agg = {c["name"]: c["estimate"] for c in r["two_fold"]["aggregate"]}
+    assert abs(agg["explained"] + agg["unexplained"] - r["total_gap"]) < 1e-9
+    assert r["n_a"] == 10 and r["n_b"] == 10
+
+
+def test_integration_categorical_normalize(O):  # tests/integration_test.rs:146-163
+    k = KAT["integration_categorical"]
+    ob = O.OracleBuilder(_frame(k, ["wage", "education", "gender", "union"]), "wage", "gender", "F")
+    ob.set(predictors=["education"], categorical=["union"], normalize=["union"], reps=5)
+    r = ob.run(threads=2)
+    agg = {c["name"]: c["estimate"] for c in r["two_fold"]["aggregate"]}
+    assert abs(r["total_gap"] - 10.0) < 1e-9
+    assert abs(agg["explained"] + agg["unexplained"] - r["total_gap"]) < 1e-9
+    names = [c["name"] for c in r["two_fold"]["detailed_explained"]]
+    assert names == ["__ob_intercept__", "education", "union_union", "union_union_plus", "union_none"]
+
+
+def test_weights_kat(O):  # tests/weights_test.rs
+    k = KAT["weights"]
+    fr = _frame(k, ["outcome", "group", "weight", "x"])
+    ob = O.OracleBuilder(fr, "outcome", "group", "B").set(predictors=["x"], reps=0)
+    assert abs(ob.run()["total_gap"] - k["gap_unweighted"]) < k["tol"]
+    ob = O.OracleBuilder(fr, "outcome", "group", "B").set(predictors=["x"], reps=0, weights="weight")
+    assert abs(ob.run()["total_gap"] - k["gap_weighted"]) < k["tol"]
+
+
+def test_null_handling_kat(O):  # tests/null_handling_test.rs
+    k = KAT["nulls"]
+    ob = O.OracleBuilder(_frame(k, ["outcome", "group", "education"]), "outcome", "group", "B")
+    ob.set(predictors=["education"], reps=20)
+    # each group: 3 rows, K = 2 -> the point estimate is solvable; gap = 11 - 16
+    r = ob.run(threads=2)
+    assert r["n_a"] == 3 and r["n_b"] == 3
+
+
+def test_rif_kat(O):  # tests/rif_test.rs
+    k = KAT["rif"]
+    ob = O.OracleBuilder(_frame(k, ["wage", "group", "education"]), "wage", "group", "F")
+    ob.set(predictors=["education"], reps=10)
+    assert ob.decompose_quantile(0.9, threads=2)["total_gap"] > 0.0
+
+
+def test_budget_gap_kat(O):  # tests/optimize_budget_test.rs:34
+    k = KAT["budget"]
+    ob = O.OracleBuilder(_frame(k, ["wage", "education", "group"]), "wage", "group", "B")
+    ob.set(predictors=["education"], reps=0)
+    r = ob.run()
+    assert abs(r["total_gap"] - 16.0) < 1e-9
+    assert sorted(np.round(r["residuals"], 9).tolist()) == [-5, -5, 0, 0, 5, 5]
+
+
+@pytest.mark.parametrize("mode", [3, 2])
+def test_reference_groups_kat(O, mode):  # tests/features_test.rs:14-35 (Cotton, Neumark)
+    k = KAT["reference_groups"]
+    ob = O.OracleBuilder(_frame(k, ["wage", "education", "experience", "gender"]), "wage", "gender", "F")
+    ob.set(predictors=["education", "experience"], reps=20, ref_mode=mode)
+    assert ob.run(threads=2)["total_gap"] > 0.0
+
+
+def test_resample_is_multinomial(O):
+    """OBRS-1 draws: exact count n per replicate and a uniform per-row law (chi-square)."""
+    n = 1500
+    tot = np.zeros(n)
+    for rep in range(200):
+        idx = O.resample_indices(0xABC, rep, 1, n)
+        assert len(idx) == n and idx.max() < n
+        tot += np.bincount(idx, minlength=n)
+    exp = 200.0
+    chi2 = ((tot - exp) ** 2 / exp).sum()
+    assert abs(chi2 - (n - 1)) < 6 * np.sqrt(2 * (n - 1))
+    m = O.level1_counts(0xABC, 7, 0, 100_000)
+    assert m.sum() == 100_000 and len(m) == (100_000 + 511) // 512
