@@ -20,6 +20,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -31,11 +33,15 @@ typedef double ob_d4 __attribute__((ext_vector_type(4)));
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kCntStride = 129;  // u32 words per replicate row of the u8 count image (+1 pad)
+constexpr int kCntStride = OB_TILE_ROWS / 4 + 1;  // u32 words per replicate row of the u8 count image (+1 pad)
 constexpr int kCntBytes = 64 * kCntStride * 4;
-constexpr int kAuxBytes = 1024;  // prefix sums + level-1 counts of the batch
+constexpr int kAuxBytes = 1024;  // level-1 counts [64] + call prefix [65] of the current tile
 constexpr int kXtOffset = kCntBytes + kAuxBytes;
 constexpr uint64_t kSegReps = 16384;
+#ifndef OB_GRAM_WAVES
+#define OB_GRAM_WAVES 2
+#endif
+constexpr int kColStride = 65;  // doubles per staged column (64 rows + 1: odd stride)
 
 #define HIP_OK(expr)                                                                     \
   do {                                                                                   \
@@ -45,21 +51,12 @@ constexpr uint64_t kSegReps = 16384;
                       __LINE__);                                                         \
   } while (0)
 
-// LDS row stride (doubles) of the staged 64-row sub-tile: >= k1 + 1 (w) and == 17 mod 32, so
-// the ds_write_b64 of a column (rows on lanes) and the ds_read_b64 of 16 consecutive pair
-// columns on two rows are both conflict-free.
-inline int lds_row_stride(int k1) {
-  int rs = 17;
-  while (rs < k1 + 1) rs += 32;
-  return rs;
-}
-
 struct GramArgs {
-  const double* cols0;
-  const double* cols1;
+  const double* gcols0;  // Gram panel of group A: column c (c_first <= c < k1) at gcols0 + (c - c_first) * ld0
+  const double* gcols1;
   int64_t ld0, ld1;
   uint32_t n0, n1;
-  int p, k1, e, ncb, rs, n_cg;
+  int k1, c_first, e, ncb, n_cg;
   uint32_t nb_rep;
   const uint32_t* chunks;  // [chunk][3] = (group, first tile, end tile)
   const uint32_t* m1;      // [tile (group 0 then group 1)][rep_pad]
@@ -71,6 +68,8 @@ struct GramArgs {
   double* partial;  // [chunk][rep_pad][e_pad]
   int e_pad;
   uint32_t* flags;
+  int diag;  // ablation bits (OB_GRAM_DIAG, tools/gram_ablate.py): 1 no level-2 draws, 2 no MFMAs,
+            // 4 no sub-tile DMA, 8 no A image, 64 force v1, 128 no draw atomics, 256 no Philox
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -99,37 +98,50 @@ __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t
 }
 
 // ---------------------------------------------------------------------------------------------
-// Gram: per block 64 replicates x (4 * CB * 16) pair columns x one row chunk of one group.
+// Shared pieces of the two Gram kernels.
+//
+// v = [1, x_1..x_p, y] scaled by sqrt(w) when weighted (the reference's own WLS formulation,
+// ols.rs:68-78), so G[r][e] = sum_i c[r][i] v_i[a(e)] v_i[b(e)] with A = counts only.
+// Staged sub-tile image: column-major [col][kColStride] doubles; row r of the 64-row sub-tile
+// sits at position (r & 3) * 16 + (r >> 2): the 4 rows of a k-step are 16 doubles (32 banks)
+// apart, and the 16 consecutive pair columns a 16-lane group reads fall on distinct banks.
+// Column 0 is the intercept: ones (unweighted, filled once) or sqrt(w) (weighted, staged).
 // ---------------------------------------------------------------------------------------------
-template <int CB, bool WEIGHTED, bool UNIT>
-__global__ __launch_bounds__(kBlock, 2) void ob_gram_kernel(const GramArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(smem);
-  uint32_t* pref = reinterpret_cast<uint32_t*>(smem + kCntBytes);  // 65 entries
-  uint32_t* mcnt = pref + 72;                                       // 64 entries
-  double* xt = reinterpret_cast<double*>(smem + kXtOffset);         // [64][rs]
+struct Work {
+  uint32_t rb, cg, chunk, g, t0, t1, n, rep0;
+  const double* X;
+  int64_t ld;
+};
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-
+__device__ __forceinline__ Work map_work(const GramArgs& a) {
   // XCD-aware bijective remap: consecutive work items (same chunk, successive replicate
-  // batches) land on one XCD so their X sub-tiles are shared through that XCD's L2.
+  // batches) land on one XCD so the chunk's sub-tiles are shared through that XCD's L2.
   const uint32_t nwg = gridDim.x, bid = blockIdx.x;
   const uint32_t xcd = bid & 7u, slot = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7u;
   const uint32_t wi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
-  const uint32_t rb = wi % a.nb_rep;
+  Work w;
+  w.rb = wi % a.nb_rep;
   const uint32_t tq = wi / a.nb_rep;
-  const uint32_t cg = tq % (uint32_t)a.n_cg;
-  const uint32_t chunk = tq / (uint32_t)a.n_cg;
-  const uint32_t g = a.chunks[chunk * 3], t0 = a.chunks[chunk * 3 + 1], t1 = a.chunks[chunk * 3 + 2];
-  const double* X = g ? a.cols1 : a.cols0;
-  const int64_t ld = g ? a.ld1 : a.ld0;
-  const uint32_t n = g ? a.n1 : a.n0;
-  const uint32_t rep0 = rb * 64;
-  const int rs = a.rs;
+  w.cg = tq % (uint32_t)a.n_cg;
+  w.chunk = tq / (uint32_t)a.n_cg;
+  w.g = a.chunks[w.chunk * 3];
+  w.t0 = a.chunks[w.chunk * 3 + 1];
+  w.t1 = a.chunks[w.chunk * 3 + 2];
+  w.X = w.g ? a.gcols1 : a.gcols0;
+  w.ld = w.g ? a.ld1 : a.ld0;
+  w.n = w.g ? a.n1 : a.n0;
+  w.rep0 = w.rb * 64;
+  return w;
+}
 
-  const int cb0 = ((int)cg * 4 + wave) * CB;
-  const bool wave_active = cb0 < a.ncb;
-  int offa[CB], offb[CB];
+// Block barrier for LDS hand-offs only. __syncthreads() also drains this wave's global loads
+// (s_waitcnt vmcnt(0)), which would stall the producers on the sub-tile DMA they just issued;
+// the DMA is waited for explicitly (vmcnt) before the barrier that publishes it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Per-lane LDS offsets of the pair (a(e), b(e)) for each of the wave's CB column blocks.
+template <int CB>
+__device__ __forceinline__ void pair_offsets(const GramArgs& a, int cb0, int lane, int (&offa)[CB], int (&offb)[CB]) {
 #pragma unroll
   for (int c = 0; c < CB; ++c) {
     const int e = (cb0 + c) * 16 + (lane & 15);
@@ -142,91 +154,231 @@ __global__ __launch_bounds__(kBlock, 2) void ob_gram_kernel(const GramArgs a) {
       }
       pb = pa + rem;
     }
-    offa[c] = pa;
-    offb[c] = pb;
+    offa[c] = pa * kColStride + (lane >> 4) * 16;
+    offb[c] = pb * kColStride + (lane >> 4) * 16;
   }
+}
+
+// LDS-DMA (global_load_lds_dword) of one 64-row sub-tile: no staging registers. Lane i of a
+// wave-instruction writes dword i of a 256-byte half column; waves [w_lo, w_lo+nw) take the
+// 2 x (k1 - c_first) instructions round-robin.
+__device__ __forceinline__ void stage_dma(const GramArgs& a, const Work& w, uint32_t xt_byte_off, size_t gbase,
+                                          int wave, int w_lo, int nw, int lane,
+                                          __attribute__((address_space(3))) unsigned char* lds3) {
+  const int ncl = a.k1 - a.c_first;
+  for (int t = wave - w_lo; t < 2 * ncl; t += nw) {
+    const int cc = t >> 1, half = t & 1;
+    const int p2 = half * 32 + (lane >> 1);
+    const int row = ((p2 & 15) << 2) | (p2 >> 4);  // inverse of the row interleave
+    const char* src = reinterpret_cast<const char*>(w.X + (size_t)cc * w.ld + gbase + row) + (lane & 1) * 4;
+    const uint32_t dst = xt_byte_off + (uint32_t)((cc + a.c_first) * kColStride + half * 32) * 8u;
+    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(lds3 + dst), 4, 0, 0);
+  }
+}
+
+// Level-2 draws of `tile` into a u8 count image (OBRS-1, ob_spec.h: full tiles take sixteen
+// 8-bit draws per Philox call, the partial last tile two 64-bit ones). Wave wv of nw owns
+// replicates [64 wv / nw, 64 (wv+1) / nw); its work is the concatenation of their Philox-call
+// lists (cum = per-tile prefix of calls, tile_counts), which its 64 lanes walk in stride; part k
+// of nparts takes the slice [C k / nparts, C (k+1) / nparts). A lane finds its replicate from
+// the boundaries held one per lane (readlane), with no dependent LDS reads. The atomics return
+// nothing: check_counts catches overflow.
+static_assert(OB_TILE_ROWS == 256u, "full-tile draws are bytes");
+__device__ __forceinline__ bool full_tile(const Work& w, uint32_t tile) {
+  return w.n - tile * OB_TILE_ROWS >= OB_TILE_ROWS;
+}
+
+__device__ __forceinline__ void level2_draws(const GramArgs& a, const Work& w, uint32_t tile, uint32_t* cnt,
+                                             const uint32_t* mc, const uint32_t* cum, int k, int nparts, int wv,
+                                             int nw, int lane) {
+  const uint32_t S = min(OB_TILE_ROWS, w.n - tile * OB_TILE_ROWS);
+  const bool full = S == OB_TILE_ROWS;
+  const int r_lo = 64 * wv / nw, r_hi = 64 * (wv + 1) / nw, nr = r_hi - r_lo;
+  if (nr <= 0) return;
+  const uint32_t c_lo = cum[r_lo], C = cum[r_hi] - c_lo;
+  const uint32_t f_lo = c_lo + C * (uint32_t)k / (uint32_t)nparts;
+  const uint32_t f_hi = c_lo + C * (uint32_t)(k + 1) / (uint32_t)nparts;
+  const uint32_t bnd = lane < nr ? cum[r_lo + 1 + lane] : 0xFFFFFFFFu;  // end of replicate r_lo + lane
+  const uint32_t c2 = (tile << 1) | w.g;
+  for (uint32_t f0 = f_lo; f0 < f_hi; f0 += 64) {
+    const uint32_t f = f0 + lane;
+    if (f < f_hi) {
+      int r = r_lo;
+      uint32_t base = c_lo;
+      for (int i = 0; i < nr - 1; ++i) {
+        const uint32_t b = __builtin_amdgcn_readlane(bnd, i);
+        if (f >= b) {
+          r = r_lo + i + 1;
+          base = b;
+        }
+      }
+      const uint32_t m = mc[r], pp = f - base;
+      ob_u32x4 u;
+      if (a.diag & 256) {  // ablation: no Philox
+        const uint32_t h = pp * 0x9E3779B9u ^ (uint32_t)r * 0x85EBCA6Bu;
+        u = {h, h * 3u, h * 5u, h * 7u};
+      } else {
+        u = ob_philox(pp, a.first_rep + w.rep0 + r, c2, OB_TAG_L2, a.key0, a.key1);
+      }
+      uint32_t* row = cnt + r * kCntStride;
+      if (a.diag & 128) {  // ablation: no LDS atomics
+        if ((u.x ^ u.y ^ u.z ^ u.w) == 0x12345678u) row[0] = 1u;
+        continue;
+      }
+      if (full) {
+        const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
+        const uint32_t nd = min(16u, m - 16 * pp);
+#pragma unroll
+        for (uint32_t d = 0; d < 16; ++d) {
+          if (d < nd) {
+            const uint32_t lr = (wd[d >> 2] >> (8 * (d & 3))) & 0xFFu;
+            atomicAdd(&row[lr >> 2], 1u << ((lr & 3u) * 8u));
+          }
+        }
+      } else {
+        uint32_t lr = ob_mulhi64(u.x, u.y, S);
+        atomicAdd(&row[lr >> 2], 1u << ((lr & 3u) * 8u));
+        if (2 * pp + 1 < m) {
+          lr = ob_mulhi64(u.z, u.w, S);
+          atomicAdd(&row[lr >> 2], 1u << ((lr & 3u) * 8u));
+        }
+      }
+    }
+  }
+}
+
+
+// A row drawn 256+ times wraps its byte and carries into the next one, which lowers the
+// replicate's byte sum below m: comparing sums with the level-1 counts is an exact check.
+// Four threads per replicate (consecutive lanes); threads my in [0, 256). With zero, each thread
+// then clears the 16 words it checked, recycling the image without another barrier.
+__device__ __forceinline__ void check_counts(const GramArgs& a, uint32_t* cnt, const uint32_t* mc, int my,
+                                             bool zero = false) {
+  const int r = my >> 2, part = my & 3;
+  uint32_t* row = cnt + r * kCntStride + part * 16;
+  uint32_t sum = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) sum = __builtin_amdgcn_sad_u8(row[i], 0u, sum);
+  if (zero)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) row[i] = 0u;
+  sum += __shfl_xor(sum, 1);
+  sum += __shfl_xor(sum, 2);
+  if (part == 0 && sum != mc[r] && !(a.diag & 384)) atomicOr(a.flags, 1u);
+}
+
+__device__ __forceinline__ uint32_t level1_count(const GramArgs& a, const Work& w, uint32_t tile, uint32_t r) {
+  const uint32_t rep = w.rep0 + r;
+  return rep < a.n_reps ? a.m1[(size_t)(w.g ? a.tiles0 + tile : tile) * a.rep_pad + rep] : 0u;
+}
+
+__device__ __forceinline__ void publish_counts(const Work& w, uint32_t tile, uint32_t m, uint32_t* mc, uint32_t* cum,
+                                               int lane) {
+  mc[lane] = m;
+  const uint32_t lg = full_tile(w, tile) ? 4u : 1u;
+  uint32_t v = (m + (1u << lg) - 1) >> lg;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(v, o);
+    if (lane >= o) v += t;
+  }
+  cum[lane + 1] = v;
+  if (lane == 0) cum[0] = 0;
+}
+
+__device__ __forceinline__ void tile_counts(const GramArgs& a, const Work& w, uint32_t tile, uint32_t* mc,
+                                            uint32_t* cum, int lane) {
+  publish_counts(w, tile, level1_count(a, w, tile, lane), mc, cum, lane);
+}
+
+template <int CB>
+__device__ __forceinline__ void store_partials(const GramArgs& a, const Work& w, int cb0, int lane,
+                                               const ob_d4 (&acc)[4][CB]) {
+#pragma unroll
+  for (int c = 0; c < CB; ++c) {
+    if (cb0 + c >= a.ncb) continue;
+    const int e = (cb0 + c) * 16 + (lane & 15);
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t rep = w.rep0 + q4 * 16 + (lane >> 4) + 4 * r;
+        if (rep < a.n_reps) a.partial[((size_t)w.chunk * a.rep_pad + rep) * a.e_pad + e] = acc[q4][c][r];
+      }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Gram v1 (fallback for wide designs, p > 58): 256 threads, 2 blocks per CU. Per 256-row tile:
+// level-2 draws by all waves, then 4 sub-tiles; the count bytes are read in the k-loop.
+// ---------------------------------------------------------------------------------------------
+template <int CB, bool UNIT>
+__global__ __launch_bounds__(kBlock, 2) void ob_gram_kernel(const GramArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(smem);
+  uint32_t* mcnt = reinterpret_cast<uint32_t*>(smem + kCntBytes);
+  uint32_t* cum = mcnt + 64;
+  double* xt = reinterpret_cast<double*>(smem + kXtOffset);  // 2 x [k1][kColStride]
+  __attribute__((address_space(3))) unsigned char* lds3 = (__attribute__((address_space(3))) unsigned char*)smem;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const Work w = map_work(a);
+  const int cb0 = ((int)w.cg * 4 + wave) * CB;
+  const bool mma = cb0 < a.ncb && !(a.diag & 2);
+  int offa[CB], offb[CB];
+  pair_offsets<CB>(a, cb0, lane, offa, offb);
   ob_d4 acc[4][CB];
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int c = 0; c < CB; ++c) acc[r][c] = (ob_d4){0.0, 0.0, 0.0, 0.0};
-
-  if (tid < 64) xt[tid * rs] = 1.0;  // v[0] = intercept, never overwritten
-  const int ncl = a.p + 1 + (WEIGHTED ? 1 : 0);
-
-  for (uint32_t tile = t0; tile < t1; ++tile) {
+  const int buf_dbl = a.k1 * kColStride;
+  if (a.c_first == 1)
+    for (int i = tid; i < 64; i += kBlock) {
+      xt[i] = 1.0;
+      xt[buf_dbl + i] = 1.0;
+    }
+  const bool draws = !UNIT && !(a.diag & 1);
+  int buf = 0;
+  if (w.t0 < w.t1) stage_dma(a, w, kXtOffset, (size_t)w.t0 * OB_TILE_ROWS, wave, 0, 4, lane, lds3);
+  for (uint32_t tile = w.t0; tile < w.t1; ++tile) {
     const uint32_t row0 = tile * OB_TILE_ROWS;
-    const uint32_t S = min(OB_TILE_ROWS, n - row0);
-    if (!UNIT) {
+    const uint32_t S = min(OB_TILE_ROWS, w.n - row0);
+    if (draws) {
+      __syncthreads();  // the previous tile's k-loops are done with the count image
       for (int i = tid; i < 64 * kCntStride; i += kBlock) cnt[i] = 0u;
-      if (tid < 64) {
-        const uint32_t rep = rep0 + tid;
-        const uint32_t m =
-            rep < a.n_reps ? a.m1[(size_t)(g ? a.tiles0 + tile : tile) * a.rep_pad + rep] : 0u;
-        mcnt[tid] = m;
-        uint32_t s = (m + 1) >> 1;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-          const uint32_t o = __shfl_up(s, off);
-          if (lane >= off) s += o;
-        }
-        pref[tid + 1] = s;
-        if (tid == 0) pref[0] = 0u;
-      }
+      if (wave == 0) tile_counts(a, w, tile, mcnt, cum, lane);
       __syncthreads();
-      const uint32_t total = pref[64];
-      int r = 0;
-      uint32_t ovf = 0;
-      for (uint32_t gp = tid; gp < total; gp += kBlock) {
-        while (pref[r + 1] <= gp) ++r;
-        const uint32_t pp = gp - pref[r];
-        const ob_u32x4 u =
-            ob_philox(pp, a.first_rep + rep0 + r, (tile << 1) | g, OB_TAG_L2, a.key0, a.key1);
-        uint32_t lr = ob_mulhi64(u.x, u.y, S);
-        uint32_t sh = (lr & 3u) * 8u;
-        uint32_t old = atomicAdd(&cnt[r * kCntStride + (lr >> 2)], 1u << sh);
-        ovf |= ((old >> sh) & 0xFFu) == 0xFFu;
-        if (2 * pp + 1 < mcnt[r]) {
-          lr = ob_mulhi64(u.z, u.w, S);
-          sh = (lr & 3u) * 8u;
-          old = atomicAdd(&cnt[r * kCntStride + (lr >> 2)], 1u << sh);
-          ovf |= ((old >> sh) & 0xFFu) == 0xFFu;
-        }
-      }
-      if (ovf) atomicOr(a.flags, 1u);
+      level2_draws(a, w, tile, cnt, mcnt, cum, 0, 1, wave, kBlock / 64, lane);
       __syncthreads();
+      check_counts(a, cnt, mcnt, tid);
     }
     const uint32_t nsub = (S + 63) >> 6;
     for (uint32_t s = 0; s < nsub; ++s) {
       const size_t gbase = (size_t)row0 + s * 64;
-      for (int idx = tid; idx < ncl * 64; idx += kBlock) {
-        const int c = idx >> 6, rr = idx & 63;
-        xt[rr * rs + 1 + c] = X[(size_t)c * ld + gbase + rr];
-      }
-      __syncthreads();
-      if (wave_active) {
-#pragma unroll 1
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // staged sub-tile visible; the other buffer is free
+      if (s + 1 < nsub)
+        stage_dma(a, w, kXtOffset + (buf ^ 1) * buf_dbl * 8, gbase + 64, wave, 0, 4, lane, lds3);
+      else if (tile + 1 < w.t1)
+        stage_dma(a, w, kXtOffset + (buf ^ 1) * buf_dbl * 8, (size_t)(tile + 1) * OB_TILE_ROWS, wave, 0, 4, lane,
+                  lds3);
+      const double* xb = xt + buf * buf_dbl;
+      if (mma) {
+        const uint32_t sh = (uint32_t)(lane >> 4) * 8u;
+#pragma unroll 2
         for (int ks = 0; ks < 16; ++ks) {
-          const int rloc = ks * 4 + (lane >> 4);
-          const double* xr = xt + rloc * rs;
-          const double wv = WEIGHTED ? xr[a.k1] : 1.0;
-          double af[4];
+          double af[4], bf[CB];
 #pragma unroll
           for (int q4 = 0; q4 < 4; ++q4) {
-            double cv;
             if (UNIT) {
-              cv = (gbase + rloc < n) ? 1.0 : 0.0;
+              af[q4] = (gbase + ks * 4 + (lane >> 4) < w.n) ? 1.0 : 0.0;
             } else {
-              const int rep = q4 * 16 + (lane & 15);
-              const uint32_t trow = s * 64 + rloc;
-              const uint32_t word = cnt[rep * kCntStride + (trow >> 2)];
-              cv = (double)((word >> ((trow & 3u) * 8u)) & 0xFFu);
+              const uint32_t word = cnt[(q4 * 16 + (lane & 15)) * kCntStride + s * 16 + ks];
+              af[q4] = (double)((word >> sh) & 0xFFu);
             }
-            af[q4] = cv * wv;
           }
-          double bf[CB];
 #pragma unroll
-          for (int c = 0; c < CB; ++c) bf[c] = xr[offa[c]] * xr[offb[c]];
+          for (int c = 0; c < CB; ++c) bf[c] = xb[offa[c] + ks] * xb[offb[c] + ks];
 #pragma unroll
           for (int q4 = 0; q4 < 4; ++q4)
 #pragma unroll
@@ -234,24 +386,182 @@ __global__ __launch_bounds__(kBlock, 2) void ob_gram_kernel(const GramArgs a) {
               acc[q4][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[q4], bf[c], acc[q4][c], 0, 0, 0);
         }
       }
-      __syncthreads();
+      buf ^= 1;
     }
   }
+  if (mma) store_partials<CB>(a, w, cb0, lane, acc);
+}
 
-  if (wave_active) {
+// ---------------------------------------------------------------------------------------------
+// Gram v2 (default for p <= 38): one block of 8 waves per CU, two per SIMD, every wave on the
+// MFMA stream (a single MFMA wave per SIMD leaves the f64 pipe idle across its own LDS waits:
+// tools/mfma_f64_waves.hip). One 64-row sub-tile per step and one LDS barrier per step. Per
+// step, wave `wave` runs its 16 k-steps (4 A fragments from the prebuilt f64 count image, CB
+// pair products of staged values, 4 x CB v_mfma_f64_16x16x4_f64 each) in four k-groups, and
+// between them its 1/8 share of the step's side work, staggered against the other wave on its
+// SIMD:
+//   DMA      global_load_lds of the next sub-tile (issued first: it has the whole step to land)
+//   draws    a slice of the NEXT tile's level-2 draws (steps 0..ns-2 of a tile, second image)
+//   image    1/8 of the next sub-tile's f64 A image
+//   recycle  at a tile's last step: exact overflow check + zeroing of its count image, and the
+//            level-1 counts of tile + 2 (loaded at the tile's first step) published
+// ---------------------------------------------------------------------------------------------
+constexpr int kV2Waves = 8;
+constexpr int kV2Threads = kV2Waves * 64;
+constexpr int kAimgDbl = 16 * 4 * 64;              // [ks][rb][lane]
+constexpr int kV2Cnt = 64 * kCntStride * 4;        // bytes per count image
+constexpr int kV2Aux = 3 * 129 * 4 + 4;            // mcnt[3][64] + cum[3][65], 8-byte aligned end
+constexpr int kV2AimgOff = 2 * kV2Cnt + kV2Aux;
+constexpr int kV2XtOff = kV2AimgOff + 2 * kAimgDbl * 8;
+static_assert(kV2AimgOff % 16 == 0, "A images must stay 16-byte aligned");
+
+template <int CB, bool UNIT>
+__global__ __launch_bounds__(kV2Threads, 1) void ob_gram2_kernel(const GramArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t* cntb = reinterpret_cast<uint32_t*>(smem);                 // [2][64][kCntStride]
+  uint32_t* mcntb = reinterpret_cast<uint32_t*>(smem + 2 * kV2Cnt);   // [3][64]
+  uint32_t* cumb = mcntb + 3 * 64;                                     // [3][65]
+  double* aimg = reinterpret_cast<double*>(smem + kV2AimgOff);        // [2][kAimgDbl]
+  double* xt = reinterpret_cast<double*>(smem + kV2XtOff);            // [2][k1][kColStride]
+  __attribute__((address_space(3))) unsigned char* lds3 = (__attribute__((address_space(3))) unsigned char*)smem;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const Work w = map_work(a);
+  const int cb0 = ((int)w.cg * kV2Waves + wave) * CB;
+  const bool mma = cb0 < a.ncb && !(a.diag & 2);
+  const bool draws = !UNIT && !(a.diag & 1);
+  const bool dma = !(a.diag & 4), imaging = !(a.diag & 8);
+  const int buf_dbl = a.k1 * kColStride;
+  auto cnt_img = [&](uint32_t t) { return cntb + (t & 1) * 64 * kCntStride; };
+  auto mc_of = [&](uint32_t t) { return mcntb + (t % 3) * 64; };
+  auto cum_of = [&](uint32_t t) { return cumb + (t % 3) * 65; };
+  auto tile_rows = [&](uint32_t t) { return min(OB_TILE_ROWS, w.n - t * OB_TILE_ROWS); };
+  // 1/8 of the A image of one sub-tile: aimg[abuf][(ks*4 + rb)*64 + ln] = count of (rep, row)
+  auto build_a = [&](int abuf, uint32_t t, uint32_t s_in_tile, size_t gbase) {
+    const uint32_t* cimg = cnt_img(t);
 #pragma unroll
-    for (int c = 0; c < CB; ++c) {
-      if (cb0 + c >= a.ncb) continue;
-      const int e = (cb0 + c) * 16 + (lane & 15);
+    for (int i = 0; i < 8; ++i) {
+      const int ent = i * kV2Threads + tid;  // (ks, rb, ln)
+      const int ks = ent >> 8, rb = (ent >> 6) & 3, ln = ent & 63;
+      double c;
+      if (UNIT)
+        c = (gbase + ks * 4 + (ln >> 4) < w.n) ? 1.0 : 0.0;
+      else
+        c = (double)((cimg[(rb * 16 + (ln & 15)) * kCntStride + s_in_tile * 16 + ks] >> ((ln >> 4) * 8)) & 0xFFu);
+      aimg[abuf * kAimgDbl + ent] = c;
+    }
+  };
+
+  // ---- prologue: counts of the first two tiles, the first tile drawn, its first sub-tile
+  // staged and imaged ----
+  if (w.t0 < w.t1) {
+    if (draws) {
+      for (int i = tid; i < 2 * 64 * kCntStride; i += kV2Threads) cntb[i] = 0u;
+      if (wave == 0) tile_counts(a, w, w.t0, mc_of(w.t0), cum_of(w.t0), lane);
+      if (wave == 1 && w.t0 + 1 < w.t1) tile_counts(a, w, w.t0 + 1, mc_of(w.t0 + 1), cum_of(w.t0 + 1), lane);
+    }
+    if (a.c_first == 1)
+      for (int i = tid; i < 64; i += kV2Threads) {
+        xt[i] = 1.0;
+        xt[buf_dbl + i] = 1.0;
+      }
+    stage_dma(a, w, kV2XtOff, (size_t)w.t0 * OB_TILE_ROWS, wave, 0, kV2Waves, lane, lds3);
+    __syncthreads();
+    if (draws) level2_draws(a, w, w.t0, cnt_img(w.t0), mc_of(w.t0), cum_of(w.t0), 0, 1, wave, kV2Waves, lane);
+    __syncthreads();
+    build_a(0, w.t0, 0, (size_t)w.t0 * OB_TILE_ROWS);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  int offa[CB], offb[CB];
+  pair_offsets<CB>(a, cb0, lane, offa, offb);
+  ob_d4 acc[4][CB];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < CB; ++c) acc[r][c] = (ob_d4){0.0, 0.0, 0.0, 0.0};
+  // k-steps [4g, 4g + 4) of the current sub-tile; fragments of k-step ks+1 are read before the
+  // MFMAs of ks (register double buffer) so a wave never waits on LDS right behind its MFMAs.
+  double af[4], bf[CB];
+  auto load_k = [&](const double* ab, const double* xb, int ks) {
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) af[q4] = ab[(ks * 4 + q4) * 64];
+#pragma unroll
+    for (int c = 0; c < CB; ++c) bf[c] = xb[offa[c] + ks] * xb[offb[c] + ks];
+  };
+  auto mma4 = [&](const double* ab, const double* xb, int g) {
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int ks = g * 4 + kk;
+      double an[4], na[CB], nb[CB];
+      if (ks < 15) {
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) an[q4] = ab[((ks + 1) * 4 + q4) * 64];
+#pragma unroll
+        for (int c = 0; c < CB; ++c) {
+          na[c] = xb[offa[c] + ks + 1];
+          nb[c] = xb[offb[c] + ks + 1];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int q4 = 0; q4 < 4; ++q4)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const uint32_t rep = rep0 + q4 * 16 + (lane >> 4) + 4 * r;
-          if (rep < a.n_reps) a.partial[((size_t)chunk * a.rep_pad + rep) * a.e_pad + e] = acc[q4][c][r];
+        for (int c = 0; c < CB; ++c)
+          acc[q4][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[q4], bf[c], acc[q4][c], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (ks < 15) {
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) af[q4] = an[q4];
+#pragma unroll
+        for (int c = 0; c < CB; ++c) bf[c] = na[c] * nb[c];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // ---- steady state ----
+  const int rot = wave >= 4 ? 2 : 0;  // the two waves of a SIMD do their side work apart
+  uint32_t m_next = 0;                // level-1 count of tile + 2 for replicate `lane` (wave 0)
+  int j = 0;
+  for (uint32_t tile = w.t0; tile < w.t1; ++tile) {
+    const uint32_t ns = (tile_rows(tile) + 63) >> 6;
+    for (uint32_t s = 0; s < ns; ++s, ++j) {
+      const int cur = j & 1;
+      const bool last_sub = s + 1 == ns;
+      const bool has_next = !last_sub || tile + 1 < w.t1;
+      const uint32_t ntile = last_sub ? tile + 1 : tile;
+      const uint32_t nsub_i = last_sub ? 0 : s + 1;
+      const size_t ngbase = (size_t)ntile * OB_TILE_ROWS + nsub_i * 64;
+      const double* ab = aimg + cur * kAimgDbl + lane;
+      const double* xb = xt + cur * buf_dbl;
+      if (has_next && dma) stage_dma(a, w, kV2XtOff + (cur ^ 1) * buf_dbl * 8, ngbase, wave, 0, kV2Waves, lane, lds3);
+      if (draws && wave == 0 && s == 0 && tile + 2 < w.t1) m_next = level1_count(a, w, tile + 2, lane);
+      if (mma) load_k(ab, xb, 0);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        if (mma) mma4(ab, xb, g);
+        const int task = (g + rot) & 3;
+        if (task == 0) {
+          // draws: the next tile's calls in slices over steps 0..ns-2 (the last step images it)
+          if (draws && !last_sub && tile + 1 < w.t1)
+            level2_draws(a, w, tile + 1, cnt_img(tile + 1), mc_of(tile + 1), cum_of(tile + 1), (int)s,
+                         (int)ns - 1, wave, kV2Waves, lane);
+        } else if (task == 1) {
+          if (has_next && imaging) build_a(cur ^ 1, ntile, nsub_i, ngbase);
+        } else if (task == 2) {
+          if (draws && last_sub) {
+            if (wave < 4) check_counts(a, cnt_img(tile), mc_of(tile), tid, true);
+            if (wave == 0 && tile + 2 < w.t1) publish_counts(w, tile + 2, m_next, mc_of(tile + 2), cum_of(tile + 2), lane);
+          }
         }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next sub-tile has landed
+      lds_barrier();
     }
   }
+  if (mma) store_partials<CB>(a, w, cb0, lane, acc);
 }
 
 // Sum of partial Grams over each group's chunks, chunk order fixed -> bitwise reproducible.
@@ -549,70 +859,100 @@ struct Plan {
   int n_chunks() const { return (int)(chunks.size() / 3); }
 };
 
-int pick_cb(int ncb) { return ncb > 8 ? 4 : (ncb > 4 ? 2 : 1); }
+int diag_mode() {
+  static int m = [] {
+    const char* e = getenv("OB_GRAM_DIAG");
+    return e ? atoi(e) : 0;
+  }();
+  return m;
+}
 
-Plan make_plan(const ob_panel* p, uint64_t n_reps) {
+size_t gram2_lds_bytes(const ob_panel* p) { return (size_t)kV2XtOff + 2 * (size_t)p->k1 * kColStride * 8; }
+bool use_v2(const ob_panel* p) { return gram2_lds_bytes(p) <= 160 * 1024 && !(diag_mode() & 64); }
+
+// The chunking is a function of the panel only (never of the replicate count or the launch),
+// so a replicate's Gram -- summed over chunks in a fixed order -- is bitwise the same however
+// the replicates are segmented or sharded. Each group splits into balanced chunks; about
+// kTargetChunks in all, so a 16384-replicate segment (256 batches of 64) is a whole number of
+// rounds over 256 CUs.
+constexpr uint32_t kTargetChunks = 64;
+
+Plan make_plan(const ob_panel* p, uint64_t n_reps, bool unit) {
   Plan pl;
   pl.nb_rep = (uint32_t)((n_reps + 63) / 64);
   pl.rep_pad = pl.nb_rep * 64;
-  pl.cb = pick_cb(p->ncb);
-  pl.n_cg = (uint32_t)((p->ncb + 4 * pl.cb - 1) / (4 * pl.cb));
-  const uint32_t tA = p->ntiles[0], tB = p->ntiles[1], tT = tA + tB;
-  const double conc = (double)std::max(p->ctx->cus, 1) * 2.0;
-  // chunk size in tiles: pick the one whose grid fills whole rounds of resident blocks
-  uint32_t best_tpc = tT;
-  double best = -1.0;
-  for (uint32_t c = 2; c <= std::min<uint32_t>(tT, 96); ++c) {
-    const uint32_t tpc = (tT + c - 1) / c;
-    const uint32_t nch = (tA + tpc - 1) / tpc + (tB + tpc - 1) / tpc;
-    const double blocks = (double)pl.nb_rep * pl.n_cg * nch;
-    const double rounds = std::ceil(blocks / conc);
-    const double score = blocks / (rounds * conc) - 0.002 * nch;
-    if (score > best + 1e-12) {
-      best = score;
-      best_tpc = tpc;
-    }
-  }
-  if (tT < 2) best_tpc = 1;
+  const int waves = use_v2(p) ? kV2Waves : 4;
+  if (use_v2(p))
+    pl.cb = p->ncb > kV2Waves ? 2 : 1;
+  else
+    pl.cb = (p->ncb > 8 && !unit) ? 4 : (p->ncb > 4 ? 2 : 1);  // unit variant: CB <= 2 (no spills)
+  pl.n_cg = (uint32_t)((p->ncb + waves * pl.cb - 1) / (waves * pl.cb));
+  const uint32_t tT = p->ntiles[0] + p->ntiles[1];
   for (uint32_t g = 0; g < 2; ++g) {
-    const uint32_t tg = g ? tB : tA;
-    for (uint32_t t = 0; t < tg; t += best_tpc) {
+    const uint32_t tg = p->ntiles[g];
+    if (tg == 0) continue;
+    const uint32_t want = (uint32_t)std::max<uint64_t>(1, ((uint64_t)kTargetChunks * tg + tT / 2) / std::max(tT, 1u));
+    const uint32_t nc = std::min(tg, std::max(want, (tg + 4095) / 4096));
+    for (uint32_t c = 0; c < nc; ++c) {
       pl.chunks.push_back(g);
-      pl.chunks.push_back(t);
-      pl.chunks.push_back(std::min(tg, t + best_tpc));
+      pl.chunks.push_back((uint32_t)((uint64_t)tg * c / nc));
+      pl.chunks.push_back((uint32_t)((uint64_t)tg * (c + 1) / nc));
     }
   }
   return pl;
 }
 
-size_t gram_lds_bytes(const ob_panel* p) { return (size_t)kXtOffset + (size_t)64 * lds_row_stride(p->k1) * 8; }
+size_t gram_lds_bytes(const ob_panel* p) { return (size_t)kXtOffset + 2 * (size_t)p->k1 * kColStride * 8; }
 size_t solve_lds_bytes(const ob_panel* p) {
   const int kp = p->k + 1;
   return sizeof(double) * ((size_t)kp * kp + 6 * kp + 3 * (size_t)std::max(p->norm.n_norm, 1));
 }
 
-template <int CB, bool W, bool U>
-hipError_t launch_gram_t(const GramArgs& ga, uint32_t blocks, size_t lds, hipStream_t s) {
-  auto kern = ob_gram_kernel<CB, W, U>;
-  hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+template <int CB, bool U>
+hipError_t launch_gram_v1(const GramArgs& ga, uint32_t blocks, size_t lds, hipStream_t s) {
+  hipError_t e = hipFuncSetAttribute((const void*)ob_gram_kernel<CB, U>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(kern, dim3(blocks), dim3(kBlock), lds, s, ga);
+  hipLaunchKernelGGL((ob_gram_kernel<CB, U>), dim3(blocks), dim3(kBlock), lds, s, ga);
   return hipGetLastError();
 }
 
-template <bool W, bool U>
-hipError_t launch_gram_w(int cb, const GramArgs& ga, uint32_t blocks, size_t lds, hipStream_t s) {
+template <int CB, bool U>
+hipError_t launch_gram_v2(const GramArgs& ga, uint32_t blocks, size_t lds, hipStream_t s) {
+  hipError_t e = hipFuncSetAttribute((const void*)ob_gram2_kernel<CB, U>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((ob_gram2_kernel<CB, U>), dim3(blocks), dim3(kV2Threads), lds, s, ga);
+  return hipGetLastError();
+}
+
+template <bool U>
+hipError_t launch_gram_u(const ob_panel* p, int cb, const GramArgs& ga, uint32_t blocks, hipStream_t s) {
+  if (use_v2(p)) {
+    const size_t lds = gram2_lds_bytes(p);
+    return cb == 2 ? launch_gram_v2<2, U>(ga, blocks, lds, s) : launch_gram_v2<1, U>(ga, blocks, lds, s);
+  }
+  const size_t lds = gram_lds_bytes(p);
   switch (cb) {
-    case 4: return launch_gram_t<4, W, U>(ga, blocks, lds, s);
-    case 2: return launch_gram_t<2, W, U>(ga, blocks, lds, s);
-    default: return launch_gram_t<1, W, U>(ga, blocks, lds, s);
+    case 4:
+      if constexpr (!U) return launch_gram_v1<4, U>(ga, blocks, lds, s);  // unit plans use CB <= 2
+      [[fallthrough]];
+    case 2: return launch_gram_v1<2, U>(ga, blocks, lds, s);
+    default: return launch_gram_v1<1, U>(ga, blocks, lds, s);
   }
 }
 
-hipError_t launch_gram(int cb, bool weighted, bool unit, const GramArgs& ga, uint32_t blocks, size_t lds,
-                       hipStream_t s) {
-  if (weighted) return unit ? launch_gram_w<true, true>(cb, ga, blocks, lds, s) : launch_gram_w<true, false>(cb, ga, blocks, lds, s);
-  return unit ? launch_gram_w<false, true>(cb, ga, blocks, lds, s) : launch_gram_w<false, false>(cb, ga, blocks, lds, s);
+hipError_t launch_gram(const ob_panel* p, int cb, bool unit, const GramArgs& ga, uint32_t blocks, hipStream_t s) {
+  return unit ? launch_gram_u<true>(p, cb, ga, blocks, s) : launch_gram_u<false>(p, cb, ga, blocks, s);
+}
+
+// Gram panel of a weighted design: [sqrt(w), sqrt(w) x_1..x_p, sqrt(w) y] (ols.rs:68-78).
+__global__ __launch_bounds__(kBlock) void ob_scale_kernel(const double* cols, int64_t ld, int p, double* gcols) {
+  const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i >= (size_t)ld) return;
+  const double sw = sqrt(cols[(size_t)(p + 1) * ld + i]);
+  gcols[i] = sw;
+  for (int c = 0; c <= p; ++c) gcols[(size_t)(c + 1) * ld + i] = sw * cols[(size_t)c * ld + i];
 }
 
 template <typename T>
@@ -651,17 +991,16 @@ SolveArgs solve_args(const ob_panel* p, int ref_mode) {
 
 GramArgs gram_args(const ob_panel* p, const Plan& pl) {
   GramArgs ga{};
-  ga.cols0 = p->d_cols[0];
-  ga.cols1 = p->d_cols[1];
+  ga.gcols0 = p->weighted ? p->d_gcols[0] : p->d_cols[0];
+  ga.gcols1 = p->weighted ? p->d_gcols[1] : p->d_cols[1];
+  ga.c_first = p->weighted ? 0 : 1;
   ga.ld0 = p->ld[0];
   ga.ld1 = p->ld[1];
   ga.n0 = p->n[0];
   ga.n1 = p->n[1];
-  ga.p = p->p;
   ga.k1 = p->k1;
   ga.e = p->e;
   ga.ncb = p->ncb;
-  ga.rs = lds_row_stride(p->k1);
   ga.n_cg = (int)pl.n_cg;
   ga.nb_rep = pl.nb_rep;
   ga.tiles0 = p->ntiles[0];
@@ -679,7 +1018,7 @@ int engine_point_estimate(ob_panel* p, int ref_mode, double* row, double* resid_
   ob_ctx* ctx = p->ctx;
   HIP_OK(hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
-  Plan pl = make_plan(p, 1);
+  Plan pl = make_plan(p, 1, true);
   const int nch = pl.n_chunks();
   double *d_partial = nullptr, *d_gram = nullptr, *d_row = nullptr, *d_gout = nullptr, *d_beta = nullptr,
          *d_res = nullptr;
@@ -719,7 +1058,7 @@ int engine_point_estimate(ob_panel* p, int ref_mode, double* row, double* resid_
     ga.first_rep = 0;
     ga.partial = d_partial;
     const uint32_t blocks = pl.nb_rep * pl.n_cg * (uint32_t)nch;
-    PE_OK(launch_gram(pl.cb, p->weighted != 0, true, ga, blocks, gram_lds_bytes(p), s));
+    PE_OK(launch_gram(p, pl.cb, true, ga, blocks, s));
     const size_t nred = (size_t)1 * p->e_pad;
     hipLaunchKernelGGL(ob_reduce_kernel, dim3((unsigned)((nred + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
                        (const double*)d_partial, (const uint32_t*)d_chunks, nch, pl.rep_pad, p->e_pad, 1u, d_gram);
@@ -777,13 +1116,16 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     return ob::fail(OB_E_INVALID, "replicate ids must stay below 2^32 (OBRS-1 counter word)");
   hipStream_t s = stream ? stream : ctx->stream;
   const uint64_t seg = std::min<uint64_t>(n_reps, kSegReps);
-  Plan pl = make_plan(p, seg);
+  Plan pl = make_plan(p, seg, false);
+  const uint64_t tail = n_reps % seg;
+  Plan pl_tail = tail ? make_plan(p, tail, false) : pl;  // same chunks, fewer replicate batches
   const int nch = pl.n_chunks();
   const uint32_t tiles = p->ntiles[0] + p->ntiles[1];
+  const size_t need_partial = std::max((size_t)nch * pl.rep_pad, (size_t)pl_tail.n_chunks() * pl_tail.rep_pad);
   OB_TRY(ensure_buf(&p->d_m1, p->cap_m1, (size_t)tiles * pl.rep_pad));
-  OB_TRY(ensure_buf(&p->d_partial, p->cap_partial, (size_t)nch * pl.rep_pad * p->e_pad));
+  OB_TRY(ensure_buf(&p->d_partial, p->cap_partial, need_partial * p->e_pad));
   OB_TRY(ensure_buf(&p->d_gram, p->cap_gram, (size_t)2 * pl.rep_pad * p->e_pad));
-  OB_TRY(ensure_buf(&p->d_chunks, p->cap_chunks, pl.chunks.size()));
+  OB_TRY(ensure_buf(&p->d_chunks, p->cap_chunks, std::max(pl.chunks.size(), pl_tail.chunks.size())));
   HIP_OK(hipMemcpyAsync(p->d_chunks, pl.chunks.data(), sizeof(uint32_t) * pl.chunks.size(), hipMemcpyHostToDevice, s));
   HIP_OK(hipStreamSynchronize(s));  // the host vector dies with this call
   HIP_OK(hipMemsetAsync(p->d_flags, 0, sizeof(uint32_t), s));
@@ -805,8 +1147,8 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   }
   for (uint64_t s0 = 0; s0 < n_reps; s0 += seg) {
     const uint32_t ns = (uint32_t)std::min<uint64_t>(seg, n_reps - s0);
-    Plan plx = (ns == seg) ? pl : make_plan(p, ns);
-    if (plx.chunks != pl.chunks || plx.rep_pad != pl.rep_pad) {
+    const Plan& plx = (ns == seg) ? pl : pl_tail;
+    if (plx.chunks != pl.chunks) {
       HIP_OK(hipStreamSynchronize(s));
       HIP_OK(hipMemcpyAsync(p->d_chunks, plx.chunks.data(), sizeof(uint32_t) * plx.chunks.size(),
                             hipMemcpyHostToDevice, s));
@@ -829,8 +1171,9 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     ga.key0 = key0;
     ga.key1 = key1;
     ga.partial = p->d_partial;
+    ga.diag = diag_mode();
     const uint32_t blocks = plx.nb_rep * plx.n_cg * (uint32_t)nchx;
-    HIP_OK(launch_gram(plx.cb, p->weighted != 0, false, ga, blocks, gram_lds_bytes(p), s));
+    HIP_OK(launch_gram(p, plx.cb, false, ga, blocks, s));
     if (timed) HIP_OK(hipEventRecord(ev[2], s));
     const size_t nred = (size_t)ns * p->e_pad;
     hipLaunchKernelGGL(ob_reduce_kernel, dim3((unsigned)((nred + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
@@ -932,7 +1275,7 @@ void ob_ctx_destroy(ob_ctx* ctx) {
 int ob_panel_create(ob_ctx* ctx, const ob_panel_desc* d, ob_panel** out) {
   if (!ctx || !d || !out) return ob::fail(OB_E_INVALID, "null pointer");
   *out = nullptr;
-  if (d->p < 0 || d->p > 126) return ob::fail(OB_E_UNSUPPORTED, "predictor columns must be in [0, 126], got %d", d->p);
+  if (d->p < 0 || d->p > 120) return ob::fail(OB_E_UNSUPPORTED, "predictor columns must be in [0, 120], got %d", d->p);
   if (d->n_num < 0 || d->n_num > d->p) return ob::fail(OB_E_INVALID, "n_num out of range");
   const ob_group_desc* gd[2] = {&d->a, &d->b};
   for (int g = 0; g < 2; ++g) {
@@ -1001,6 +1344,16 @@ int ob_panel_create(ob_ctx* ctx, const ob_panel_desc* d, ob_panel** out) {
       }
     }
   }
+  for (int g = 0; g < 2 && rc == OB_OK && p->weighted; ++g) {
+    hipError_t e = hipMalloc(&p->d_gcols[g], sizeof(double) * (size_t)p->k1 * p->ld[g]);
+    if (e == hipSuccess) {
+      hipLaunchKernelGGL(ob_scale_kernel, dim3((unsigned)((p->ld[g] + kBlock - 1) / kBlock)), dim3(kBlock), 0, 0,
+                         (const double*)p->d_cols[g], p->ld[g], p->p, p->d_gcols[g]);
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) bad(e, __LINE__);
+  }
   if (rc == OB_OK) {
     std::vector<int32_t> packed;
     packed.insert(packed.end(), nc.start.begin(), nc.start.end());
@@ -1027,7 +1380,10 @@ void ob_panel_destroy(ob_panel* p) {
   if (!p) return;
   (void)hipSetDevice(p->ctx->device);
   if (p->timing_pending) (void)hipStreamSynchronize(p->last_stream);
-  for (int g = 0; g < 2; ++g) (void)hipFree(p->d_cols[g]);
+  for (int g = 0; g < 2; ++g) {
+    (void)hipFree(p->d_cols[g]);
+    (void)hipFree(p->d_gcols[g]);
+  }
   (void)hipFree(p->d_norm);
   (void)hipFree(p->d_m1);
   (void)hipFree(p->d_partial);

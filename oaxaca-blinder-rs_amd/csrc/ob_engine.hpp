@@ -33,7 +33,8 @@ struct ob_panel {
   uint32_t n[2] = {0, 0};
   int64_t ld[2] = {0, 0};      // padded rows (multiple of OB_TILE_ROWS)
   uint32_t ntiles[2] = {0, 0};
-  double* d_cols[2] = {nullptr, nullptr};  // [col][ld]: x_1..x_p, y, (w)
+  double* d_cols[2] = {nullptr, nullptr};   // [col][ld]: x_1..x_p, y, (w)
+  double* d_gcols[2] = {nullptr, nullptr};  // weighted: [k1][ld] = sqrt(w) * [1, x, y]
   ob_norm_cfg norm;
   int32_t* d_norm = nullptr;               // packed norm lists
   int row_len = 0;

@@ -7,7 +7,10 @@
 // cell probability 1/n_g) from a counter-based stream so that replicate r is reproducible from
 // (seed, r) alone on any GPU count:
 //   level 1: n_g draws idx = mulhi64(u64, n_g) -> tile = idx / OB_TILE_ROWS  (tile counts m_j)
-//   level 2: m_j draws local = mulhi64(u64, S_j) inside tile j (S_j = rows of tile j)
+//   level 2: m_j draws inside tile j (S_j rows). Full tiles (S_j = OB_TILE_ROWS = 2^8): Philox
+//            call p yields draws 16p..16p+15, draw 16p + 4i + b = byte b (LSB first) of output
+//            word i (exactly uniform, independent). The partial last tile: call p yields draws
+//            2p, 2p+1, local = mulhi64(u64, S_j) of words (x,y) and (z,w).
 // Conditional on the tile counts the level-2 draws are i.i.d. uniform in their tile, so the
 // joint law of per-row counts equals that of n_g i.i.d. uniform draws over the group.
 #pragma once
@@ -19,8 +22,8 @@
 #define OB_HD static inline
 #endif
 
-#define OB_TILE_ROWS 512u
-#define OB_TILE_SHIFT 9u
+#define OB_TILE_ROWS 256u
+#define OB_TILE_SHIFT 8u
 #define OB_TAG_L1 0x4F425231u /* "OBR1" */
 #define OB_TAG_L2 0x4F425232u /* "OBR2" */
 

@@ -28,7 +28,7 @@
 /* OBRS-1 resample stream (our spec; the reference uses polars' unseeded sample_n_literal,    */
 /* builder.rs:822-827, i.e. n_g i.i.d. uniform draws with replacement per group).            */
 /* ------------------------------------------------------------------------------------------ */
-#define ORC_TILE 512u
+#define ORC_TILE 256u
 #define ORC_TAG_L1 0x4F425231u /* "OBR1" */
 #define ORC_TAG_L2 0x4F425232u /* "OBR2" */
 
@@ -86,13 +86,23 @@ void orc_resample_indices(uint64_t seed, uint32_t rep, uint32_t g, uint32_t n, u
     for (uint32_t j = 0; j < ntiles; ++j) {
         uint32_t base = j * ORC_TILE;
         uint32_t s = (n - base < ORC_TILE) ? (n - base) : ORC_TILE;
-        for (uint32_t p = 0; 2u * p < m[j]; ++p) {
-            uint32_t ctr[4] = {p, rep, (j << 1) | g, ORC_TAG_L2}, w[4];
-            orc_philox4x32_10(ctr, key, w);
-            for (int h = 0; h < 2; ++h) {
-                uint32_t q = 2u * p + (uint32_t)h;
-                if (q >= m[j]) break;
-                idx_out[pos++] = base + orc_mulhi64(orc_draw_u64(w, h), s);
+        if (s == ORC_TILE) { /* full tile: 16 exact 8-bit draws per Philox call,
+                                 draw 16p + 4i + b = byte b (LSB first) of word i */
+            for (uint32_t p = 0; 16u * p < m[j]; ++p) {
+                uint32_t ctr[4] = {p, rep, (j << 1) | g, ORC_TAG_L2}, w[4];
+                orc_philox4x32_10(ctr, key, w);
+                for (uint32_t d = 0; d < 16 && 16u * p + d < m[j]; ++d)
+                    idx_out[pos++] = base + ((w[d >> 2] >> (8u * (d & 3u))) & 0xFFu);
+            }
+        } else { /* partial tile: 2 draws per call, 64-bit uniform mapped onto [0, s) */
+            for (uint32_t p = 0; 2u * p < m[j]; ++p) {
+                uint32_t ctr[4] = {p, rep, (j << 1) | g, ORC_TAG_L2}, w[4];
+                orc_philox4x32_10(ctr, key, w);
+                for (int h = 0; h < 2; ++h) {
+                    uint32_t q = 2u * p + (uint32_t)h;
+                    if (q >= m[j]) break;
+                    idx_out[pos++] = base + orc_mulhi64(orc_draw_u64(w, h), s);
+                }
             }
         }
     }

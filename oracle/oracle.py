@@ -92,9 +92,9 @@ def philox(ctr, key):
 
 
 def level1_counts(seed, rep, g, n):
-    m = np.zeros(max((n + 511) // 512, 1), dtype=np.uint32)
+    m = np.zeros(max((n + 255) // 256, 1), dtype=np.uint32)
     lib().orc_level1_counts(seed & (2**64 - 1), rep, g, n, m.ctypes.data_as(C.POINTER(C.c_uint32)))
-    return m[: (n + 511) // 512]
+    return m[: (n + 255) // 256]
 
 
 def resample_indices(seed, rep, g, n):

@@ -213,4 +213,4 @@ def test_resample_is_multinomial(O):
     chi2 = ((tot - exp) ** 2 / exp).sum()
     assert abs(chi2 - (n - 1)) < 6 * np.sqrt(2 * (n - 1))
     m = O.level1_counts(0xABC, 7, 0, 100_000)
-    assert m.sum() == 100_000 and len(m) == (100_000 + 511) // 512
+    assert m.sum() == 100_000 and len(m) == (100_000 + 255) // 256
