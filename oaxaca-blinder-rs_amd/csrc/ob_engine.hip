@@ -9,11 +9,11 @@
 //
 // Kernels (DESIGN.md §4 has the rooflines):
 //   ob_level1_kernel   one block per (replicate, group): n_g Philox draws -> LDS tile histogram
-//   ob_gram_kernel     one block per (row chunk, 64-replicate batch, column group): per 512-row
-//                      tile, level-2 draws -> u8 count image in LDS, then
-//                      G[r][e] += sum_i c[r][i] w_i v_i[a(e)] v_i[b(e)] with
-//                      v_mfma_f64_16x16x4_f64 (A = counts x weight, 16 replicates x 4 rows;
-//                      B = pair products, 4 rows x 16 pairs)
+//   ob_gram_kernel     one block per (row chunk, 64-replicate batch, column group), two per CU:
+//                      per 256-row tile, level-2 draws -> u8 count image in LDS (pipelined one
+//                      tile ahead), then G[r][e] += sum_i c[r][i] v_i[a(e)] v_i[b(e)] with
+//                      v_mfma_f64_16x16x4_f64 (A = counts, 16 replicates x 4 rows; B = pair
+//                      products of the staged rows, 4 rows x 16 pairs; v = sqrt(w) [1, x, y])
 //   ob_reduce_kernel   sums the per-chunk partial Grams in a fixed order (deterministic)
 //   ob_solve_kernel    one wave per replicate: normal equations, Cholesky, beta*, OB terms
 #include <hip/hip_runtime.h>
@@ -35,12 +35,7 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kCntStride = OB_TILE_ROWS / 4 + 1;  // u32 words per replicate row of the u8 count image (+1 pad)
 constexpr int kCntBytes = 64 * kCntStride * 4;
-constexpr int kAuxBytes = 1024;  // level-1 counts [64] + call prefix [65] of the current tile
-constexpr int kXtOffset = kCntBytes + kAuxBytes;
 constexpr uint64_t kSegReps = 16384;
-#ifndef OB_GRAM_WAVES
-#define OB_GRAM_WAVES 2
-#endif
 constexpr int kColStride = 65;  // doubles per staged column (64 rows + 1: odd stride)
 
 #define HIP_OK(expr)                                                                     \
@@ -69,7 +64,7 @@ struct GramArgs {
   int e_pad;
   uint32_t* flags;
   int diag;  // ablation bits (OB_GRAM_DIAG, tools/gram_ablate.py): 1 no level-2 draws, 2 no MFMAs,
-            // 4 no sub-tile DMA, 8 no A image, 64 force v1, 128 no draw atomics, 256 no Philox
+            // 4 no sub-tile DMA
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -98,7 +93,7 @@ __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t
 }
 
 // ---------------------------------------------------------------------------------------------
-// Shared pieces of the two Gram kernels.
+// Pieces of the Gram kernel.
 //
 // v = [1, x_1..x_p, y] scaled by sqrt(w) when weighted (the reference's own WLS formulation,
 // ols.rs:68-78), so G[r][e] = sum_i c[r][i] v_i[a(e)] v_i[b(e)] with A = counts only.
@@ -178,14 +173,20 @@ __device__ __forceinline__ void stage_dma(const GramArgs& a, const Work& w, uint
 
 // Level-2 draws of `tile` into a u8 count image (OBRS-1, ob_spec.h: full tiles take sixteen
 // 8-bit draws per Philox call, the partial last tile two 64-bit ones). Wave wv of nw owns
-// replicates [64 wv / nw, 64 (wv+1) / nw); its work is the concatenation of their Philox-call
-// lists (cum = per-tile prefix of calls, tile_counts), which its 64 lanes walk in stride; part k
-// of nparts takes the slice [C k / nparts, C (k+1) / nparts). A lane finds its replicate from
-// the boundaries held one per lane (readlane), with no dependent LDS reads. The atomics return
-// nothing: check_counts catches overflow.
+// replicates [64 wv / nw, 64 (wv+1) / nw). Full tile: replicate r's draws are floor(m/16) whole
+// calls plus, when m % 16 != 0, one part call (index floor(m/16)). The whole calls of the wave's
+// replicates form one list (cum = its prefix, publish_counts) walked by the 64 lanes in stride,
+// unmasked; part k of nparts takes the slice [C k / nparts, C (k+1) / nparts), and the last part
+// also takes the part calls, one lane per replicate. A lane finds its replicate with a uniform
+// cursor plus the few boundaries inside its 64-call window (readlane, no LDS chains). The
+// atomics return nothing: check_counts catches overflow.
 static_assert(OB_TILE_ROWS == 256u, "full-tile draws are bytes");
 __device__ __forceinline__ bool full_tile(const Work& w, uint32_t tile) {
   return w.n - tile * OB_TILE_ROWS >= OB_TILE_ROWS;
+}
+
+__device__ __forceinline__ void add_draw(uint32_t* row, uint32_t lr) {
+  atomicAdd(&row[lr >> 2], 1u << ((lr & 3u) * 8u));
 }
 
 __device__ __forceinline__ void level2_draws(const GramArgs& a, const Work& w, uint32_t tile, uint32_t* cnt,
@@ -200,53 +201,48 @@ __device__ __forceinline__ void level2_draws(const GramArgs& a, const Work& w, u
   const uint32_t f_hi = c_lo + C * (uint32_t)(k + 1) / (uint32_t)nparts;
   const uint32_t bnd = lane < nr ? cum[r_lo + 1 + lane] : 0xFFFFFFFFu;  // end of replicate r_lo + lane
   const uint32_t c2 = (tile << 1) | w.g;
+  const uint32_t rep0 = a.first_rep + w.rep0;
+  int rr = r_lo;  // uniform: replicate of the window's first call
   for (uint32_t f0 = f_lo; f0 < f_hi; f0 += 64) {
+    while (rr < r_hi - 1 && (uint32_t)__builtin_amdgcn_readlane(bnd, rr - r_lo) <= f0) ++rr;
     const uint32_t f = f0 + lane;
+    int r = rr;
+    uint32_t base = rr > r_lo ? (uint32_t)__builtin_amdgcn_readlane(bnd, rr - r_lo - 1) : c_lo;
+    for (int i = rr; i < r_hi - 1; ++i) {
+      const uint32_t b = (uint32_t)__builtin_amdgcn_readlane(bnd, i - r_lo);
+      if (b > f0 + 63) break;
+      if (f >= b) {
+        r = i + 1;
+        base = b;
+      }
+    }
     if (f < f_hi) {
-      int r = r_lo;
-      uint32_t base = c_lo;
-      for (int i = 0; i < nr - 1; ++i) {
-        const uint32_t b = __builtin_amdgcn_readlane(bnd, i);
-        if (f >= b) {
-          r = r_lo + i + 1;
-          base = b;
-        }
-      }
-      const uint32_t m = mc[r], pp = f - base;
-      ob_u32x4 u;
-      if (a.diag & 256) {  // ablation: no Philox
-        const uint32_t h = pp * 0x9E3779B9u ^ (uint32_t)r * 0x85EBCA6Bu;
-        u = {h, h * 3u, h * 5u, h * 7u};
-      } else {
-        u = ob_philox(pp, a.first_rep + w.rep0 + r, c2, OB_TAG_L2, a.key0, a.key1);
-      }
+      const uint32_t pp = f - base;
+      const ob_u32x4 u = ob_philox(pp, rep0 + r, c2, OB_TAG_L2, a.key0, a.key1);
       uint32_t* row = cnt + r * kCntStride;
-      if (a.diag & 128) {  // ablation: no LDS atomics
-        if ((u.x ^ u.y ^ u.z ^ u.w) == 0x12345678u) row[0] = 1u;
-        continue;
-      }
       if (full) {
         const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
-        const uint32_t nd = min(16u, m - 16 * pp);
 #pragma unroll
-        for (uint32_t d = 0; d < 16; ++d) {
-          if (d < nd) {
-            const uint32_t lr = (wd[d >> 2] >> (8 * (d & 3))) & 0xFFu;
-            atomicAdd(&row[lr >> 2], 1u << ((lr & 3u) * 8u));
-          }
-        }
+        for (int d = 0; d < 16; ++d) add_draw(row, (wd[d >> 2] >> (8 * (d & 3))) & 0xFFu);
       } else {
-        uint32_t lr = ob_mulhi64(u.x, u.y, S);
-        atomicAdd(&row[lr >> 2], 1u << ((lr & 3u) * 8u));
-        if (2 * pp + 1 < m) {
-          lr = ob_mulhi64(u.z, u.w, S);
-          atomicAdd(&row[lr >> 2], 1u << ((lr & 3u) * 8u));
-        }
+        add_draw(row, ob_mulhi64(u.x, u.y, S));
+        if (2 * pp + 1 < mc[r]) add_draw(row, ob_mulhi64(u.z, u.w, S));
       }
     }
   }
+  if (full && k == nparts - 1 && lane < nr) {  // the part calls
+    const int r = r_lo + lane;
+    const uint32_t m = mc[r], nd = m & 15u;
+    if (nd) {
+      const ob_u32x4 u = ob_philox(m >> 4, rep0 + r, c2, OB_TAG_L2, a.key0, a.key1);
+      const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
+      uint32_t* row = cnt + r * kCntStride;
+#pragma unroll
+      for (uint32_t d = 0; d < 15; ++d)
+        if (d < nd) add_draw(row, (wd[d >> 2] >> (8 * (d & 3))) & 0xFFu);
+    }
+  }
 }
-
 
 // A row drawn 256+ times wraps its byte and carries into the next one, which lowers the
 // replicate's byte sum below m: comparing sums with the level-1 counts is an exact check.
@@ -264,7 +260,7 @@ __device__ __forceinline__ void check_counts(const GramArgs& a, uint32_t* cnt, c
     for (int i = 0; i < 16; ++i) row[i] = 0u;
   sum += __shfl_xor(sum, 1);
   sum += __shfl_xor(sum, 2);
-  if (part == 0 && sum != mc[r] && !(a.diag & 384)) atomicOr(a.flags, 1u);
+  if (part == 0 && sum != mc[r]) atomicOr(a.flags, 1u);
 }
 
 __device__ __forceinline__ uint32_t level1_count(const GramArgs& a, const Work& w, uint32_t tile, uint32_t r) {
@@ -275,8 +271,8 @@ __device__ __forceinline__ uint32_t level1_count(const GramArgs& a, const Work& 
 __device__ __forceinline__ void publish_counts(const Work& w, uint32_t tile, uint32_t m, uint32_t* mc, uint32_t* cum,
                                                int lane) {
   mc[lane] = m;
-  const uint32_t lg = full_tile(w, tile) ? 4u : 1u;
-  uint32_t v = (m + (1u << lg) - 1) >> lg;
+  // calls in the whole-call list: full tile floor(m/16) (the part call goes apart), else ceil(m/2)
+  uint32_t v = full_tile(w, tile) ? m >> 4 : (m + 1) >> 1;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t t = __shfl_up(v, o);
@@ -309,167 +305,55 @@ __device__ __forceinline__ void store_partials(const GramArgs& a, const Work& w,
 }
 
 // ---------------------------------------------------------------------------------------------
-// Gram v1 (fallback for wide designs, p > 58): 256 threads, 2 blocks per CU. Per 256-row tile:
-// level-2 draws by all waves, then 4 sub-tiles; the count bytes are read in the k-loop.
+// Gram: 4 waves (one per SIMD) per block, two blocks per CU, CB column blocks per wave; the
+// two blocks on a CU drift apart, so one block's barrier never drains a SIMD's MFMA pipe. One
+// 64-row sub-tile per step and one LDS barrier per step; A fragments are the count bytes of the
+// current tile (ds_read_b32 + convert), prefetched one k-step ahead. Per tile t the side work
+// rides between k-groups of its steps:
+//   step 0      recycle tile t-1's count image (exact overflow check + zeroing, all threads),
+//               publish tile t+1's level-1 counts (loaded at tile t-1's first step), load t+2's
+//   steps 1..ns-2  the level-2 draws of tile t+1 into the recycled image, in slices
+//   every step  LDS-DMA of the next sub-tile, first thing, so it has the whole step to land
 // ---------------------------------------------------------------------------------------------
+constexpr int kAux = 3 * 129 * 4 + 4;  // mcnt[3][64] + cum[3][65], 16-byte aligned end
+constexpr int kXtOff = 2 * kCntBytes + kAux;
+static_assert(kXtOff % 16 == 0, "staged sub-tiles must stay 16-byte aligned");
+
 template <int CB, bool UNIT>
 __global__ __launch_bounds__(kBlock, 2) void ob_gram_kernel(const GramArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint32_t* cnt = reinterpret_cast<uint32_t*>(smem);
-  uint32_t* mcnt = reinterpret_cast<uint32_t*>(smem + kCntBytes);
-  uint32_t* cum = mcnt + 64;
-  double* xt = reinterpret_cast<double*>(smem + kXtOffset);  // 2 x [k1][kColStride]
+  uint32_t* cntb = reinterpret_cast<uint32_t*>(smem);                    // [2][64][kCntStride]
+  uint32_t* mcntb = reinterpret_cast<uint32_t*>(smem + 2 * kCntBytes);   // [3][64]
+  uint32_t* cumb = mcntb + 3 * 64;                                        // [3][65]
+  double* xt = reinterpret_cast<double*>(smem + kXtOff);               // [2][k1][kColStride]
   __attribute__((address_space(3))) unsigned char* lds3 = (__attribute__((address_space(3))) unsigned char*)smem;
+
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const Work w = map_work(a);
   const int cb0 = ((int)w.cg * 4 + wave) * CB;
   const bool mma = cb0 < a.ncb && !(a.diag & 2);
-  int offa[CB], offb[CB];
-  pair_offsets<CB>(a, cb0, lane, offa, offb);
-  ob_d4 acc[4][CB];
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int c = 0; c < CB; ++c) acc[r][c] = (ob_d4){0.0, 0.0, 0.0, 0.0};
-  const int buf_dbl = a.k1 * kColStride;
-  if (a.c_first == 1)
-    for (int i = tid; i < 64; i += kBlock) {
-      xt[i] = 1.0;
-      xt[buf_dbl + i] = 1.0;
-    }
   const bool draws = !UNIT && !(a.diag & 1);
-  int buf = 0;
-  if (w.t0 < w.t1) stage_dma(a, w, kXtOffset, (size_t)w.t0 * OB_TILE_ROWS, wave, 0, 4, lane, lds3);
-  for (uint32_t tile = w.t0; tile < w.t1; ++tile) {
-    const uint32_t row0 = tile * OB_TILE_ROWS;
-    const uint32_t S = min(OB_TILE_ROWS, w.n - row0);
-    if (draws) {
-      __syncthreads();  // the previous tile's k-loops are done with the count image
-      for (int i = tid; i < 64 * kCntStride; i += kBlock) cnt[i] = 0u;
-      if (wave == 0) tile_counts(a, w, tile, mcnt, cum, lane);
-      __syncthreads();
-      level2_draws(a, w, tile, cnt, mcnt, cum, 0, 1, wave, kBlock / 64, lane);
-      __syncthreads();
-      check_counts(a, cnt, mcnt, tid);
-    }
-    const uint32_t nsub = (S + 63) >> 6;
-    for (uint32_t s = 0; s < nsub; ++s) {
-      const size_t gbase = (size_t)row0 + s * 64;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();  // staged sub-tile visible; the other buffer is free
-      if (s + 1 < nsub)
-        stage_dma(a, w, kXtOffset + (buf ^ 1) * buf_dbl * 8, gbase + 64, wave, 0, 4, lane, lds3);
-      else if (tile + 1 < w.t1)
-        stage_dma(a, w, kXtOffset + (buf ^ 1) * buf_dbl * 8, (size_t)(tile + 1) * OB_TILE_ROWS, wave, 0, 4, lane,
-                  lds3);
-      const double* xb = xt + buf * buf_dbl;
-      if (mma) {
-        const uint32_t sh = (uint32_t)(lane >> 4) * 8u;
-#pragma unroll 2
-        for (int ks = 0; ks < 16; ++ks) {
-          double af[4], bf[CB];
-#pragma unroll
-          for (int q4 = 0; q4 < 4; ++q4) {
-            if (UNIT) {
-              af[q4] = (gbase + ks * 4 + (lane >> 4) < w.n) ? 1.0 : 0.0;
-            } else {
-              const uint32_t word = cnt[(q4 * 16 + (lane & 15)) * kCntStride + s * 16 + ks];
-              af[q4] = (double)((word >> sh) & 0xFFu);
-            }
-          }
-#pragma unroll
-          for (int c = 0; c < CB; ++c) bf[c] = xb[offa[c] + ks] * xb[offb[c] + ks];
-#pragma unroll
-          for (int q4 = 0; q4 < 4; ++q4)
-#pragma unroll
-            for (int c = 0; c < CB; ++c)
-              acc[q4][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[q4], bf[c], acc[q4][c], 0, 0, 0);
-        }
-      }
-      buf ^= 1;
-    }
-  }
-  if (mma) store_partials<CB>(a, w, cb0, lane, acc);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Gram v2 (default for p <= 38): one block of 8 waves per CU, two per SIMD, every wave on the
-// MFMA stream (a single MFMA wave per SIMD leaves the f64 pipe idle across its own LDS waits:
-// tools/mfma_f64_waves.hip). One 64-row sub-tile per step and one LDS barrier per step. Per
-// step, wave `wave` runs its 16 k-steps (4 A fragments from the prebuilt f64 count image, CB
-// pair products of staged values, 4 x CB v_mfma_f64_16x16x4_f64 each) in four k-groups, and
-// between them its 1/8 share of the step's side work, staggered against the other wave on its
-// SIMD:
-//   DMA      global_load_lds of the next sub-tile (issued first: it has the whole step to land)
-//   draws    a slice of the NEXT tile's level-2 draws (steps 0..ns-2 of a tile, second image)
-//   image    1/8 of the next sub-tile's f64 A image
-//   recycle  at a tile's last step: exact overflow check + zeroing of its count image, and the
-//            level-1 counts of tile + 2 (loaded at the tile's first step) published
-// ---------------------------------------------------------------------------------------------
-constexpr int kV2Waves = 8;
-constexpr int kV2Threads = kV2Waves * 64;
-constexpr int kAimgDbl = 16 * 4 * 64;              // [ks][rb][lane]
-constexpr int kV2Cnt = 64 * kCntStride * 4;        // bytes per count image
-constexpr int kV2Aux = 3 * 129 * 4 + 4;            // mcnt[3][64] + cum[3][65], 8-byte aligned end
-constexpr int kV2AimgOff = 2 * kV2Cnt + kV2Aux;
-constexpr int kV2XtOff = kV2AimgOff + 2 * kAimgDbl * 8;
-static_assert(kV2AimgOff % 16 == 0, "A images must stay 16-byte aligned");
-
-template <int CB, bool UNIT>
-__global__ __launch_bounds__(kV2Threads, 1) void ob_gram2_kernel(const GramArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint32_t* cntb = reinterpret_cast<uint32_t*>(smem);                 // [2][64][kCntStride]
-  uint32_t* mcntb = reinterpret_cast<uint32_t*>(smem + 2 * kV2Cnt);   // [3][64]
-  uint32_t* cumb = mcntb + 3 * 64;                                     // [3][65]
-  double* aimg = reinterpret_cast<double*>(smem + kV2AimgOff);        // [2][kAimgDbl]
-  double* xt = reinterpret_cast<double*>(smem + kV2XtOff);            // [2][k1][kColStride]
-  __attribute__((address_space(3))) unsigned char* lds3 = (__attribute__((address_space(3))) unsigned char*)smem;
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const Work w = map_work(a);
-  const int cb0 = ((int)w.cg * kV2Waves + wave) * CB;
-  const bool mma = cb0 < a.ncb && !(a.diag & 2);
-  const bool draws = !UNIT && !(a.diag & 1);
-  const bool dma = !(a.diag & 4), imaging = !(a.diag & 8);
+  const bool dma = !(a.diag & 4);
   const int buf_dbl = a.k1 * kColStride;
   auto cnt_img = [&](uint32_t t) { return cntb + (t & 1) * 64 * kCntStride; };
   auto mc_of = [&](uint32_t t) { return mcntb + (t % 3) * 64; };
   auto cum_of = [&](uint32_t t) { return cumb + (t % 3) * 65; };
   auto tile_rows = [&](uint32_t t) { return min(OB_TILE_ROWS, w.n - t * OB_TILE_ROWS); };
-  // 1/8 of the A image of one sub-tile: aimg[abuf][(ks*4 + rb)*64 + ln] = count of (rep, row)
-  auto build_a = [&](int abuf, uint32_t t, uint32_t s_in_tile, size_t gbase) {
-    const uint32_t* cimg = cnt_img(t);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int ent = i * kV2Threads + tid;  // (ks, rb, ln)
-      const int ks = ent >> 8, rb = (ent >> 6) & 3, ln = ent & 63;
-      double c;
-      if (UNIT)
-        c = (gbase + ks * 4 + (ln >> 4) < w.n) ? 1.0 : 0.0;
-      else
-        c = (double)((cimg[(rb * 16 + (ln & 15)) * kCntStride + s_in_tile * 16 + ks] >> ((ln >> 4) * 8)) & 0xFFu);
-      aimg[abuf * kAimgDbl + ent] = c;
-    }
-  };
 
-  // ---- prologue: counts of the first two tiles, the first tile drawn, its first sub-tile
-  // staged and imaged ----
   if (w.t0 < w.t1) {
     if (draws) {
-      for (int i = tid; i < 2 * 64 * kCntStride; i += kV2Threads) cntb[i] = 0u;
+      for (int i = tid; i < 2 * 64 * kCntStride; i += kBlock) cntb[i] = 0u;
       if (wave == 0) tile_counts(a, w, w.t0, mc_of(w.t0), cum_of(w.t0), lane);
       if (wave == 1 && w.t0 + 1 < w.t1) tile_counts(a, w, w.t0 + 1, mc_of(w.t0 + 1), cum_of(w.t0 + 1), lane);
     }
     if (a.c_first == 1)
-      for (int i = tid; i < 64; i += kV2Threads) {
+      for (int i = tid; i < 64; i += kBlock) {
         xt[i] = 1.0;
         xt[buf_dbl + i] = 1.0;
       }
-    stage_dma(a, w, kV2XtOff, (size_t)w.t0 * OB_TILE_ROWS, wave, 0, kV2Waves, lane, lds3);
+    stage_dma(a, w, kXtOff, (size_t)w.t0 * OB_TILE_ROWS, wave, 0, 4, lane, lds3);
     __syncthreads();
-    if (draws) level2_draws(a, w, w.t0, cnt_img(w.t0), mc_of(w.t0), cum_of(w.t0), 0, 1, wave, kV2Waves, lane);
-    __syncthreads();
-    build_a(0, w.t0, 0, (size_t)w.t0 * OB_TILE_ROWS);
+    if (draws) level2_draws(a, w, w.t0, cnt_img(w.t0), mc_of(w.t0), cum_of(w.t0), 0, 1, wave, 4, lane);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -481,30 +365,33 @@ __global__ __launch_bounds__(kV2Threads, 1) void ob_gram2_kernel(const GramArgs 
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int c = 0; c < CB; ++c) acc[r][c] = (ob_d4){0.0, 0.0, 0.0, 0.0};
-  // k-steps [4g, 4g + 4) of the current sub-tile; fragments of k-step ks+1 are read before the
-  // MFMAs of ks (register double buffer) so a wave never waits on LDS right behind its MFMAs.
-  double af[4], bf[CB];
-  auto load_k = [&](const double* ab, const double* xb, int ks) {
+  const uint32_t sh = (uint32_t)(lane >> 4) * 8u;
+  // A fragment of replicate block q4, k-step ks: count byte of (rep q4*16 + lane&15, row 4ks + lane>>4)
+  uint32_t aw[4];
+  double bf[CB];
+  size_t gbase = 0;
+  auto read_k = [&](const uint32_t* cw, const double* xb, int ks, uint32_t (&w4)[4], double (&va)[CB],
+                    double (&vb)[CB]) {
 #pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) af[q4] = ab[(ks * 4 + q4) * 64];
+    for (int q4 = 0; q4 < 4; ++q4) w4[q4] = UNIT ? 0u : cw[q4 * 16 * kCntStride + ks];
 #pragma unroll
-    for (int c = 0; c < CB; ++c) bf[c] = xb[offa[c] + ks] * xb[offb[c] + ks];
+    for (int c = 0; c < CB; ++c) {
+      va[c] = xb[offa[c] + ks];
+      vb[c] = xb[offb[c] + ks];
+    }
   };
-  auto mma4 = [&](const double* ab, const double* xb, int g) {
+  auto mma4 = [&](const uint32_t* cw, const double* xb, int g) {
 #pragma unroll
     for (int kk = 0; kk < 4; ++kk) {
       const int ks = g * 4 + kk;
-      double an[4], na[CB], nb[CB];
-      if (ks < 15) {
-#pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4) an[q4] = ab[((ks + 1) * 4 + q4) * 64];
-#pragma unroll
-        for (int c = 0; c < CB; ++c) {
-          na[c] = xb[offa[c] + ks + 1];
-          nb[c] = xb[offb[c] + ks + 1];
-        }
-      }
+      uint32_t an[4];
+      double na[CB], nb[CB];
+      if (ks < 15) read_k(cw, xb, ks + 1, an, na, nb);
       __builtin_amdgcn_sched_barrier(0);
+      double af[4];
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4)
+        af[q4] = UNIT ? ((gbase + ks * 4 + (lane >> 4) < w.n) ? 1.0 : 0.0) : (double)((aw[q4] >> sh) & 0xFFu);
 #pragma unroll
       for (int q4 = 0; q4 < 4; ++q4)
 #pragma unroll
@@ -513,7 +400,7 @@ __global__ __launch_bounds__(kV2Threads, 1) void ob_gram2_kernel(const GramArgs 
       __builtin_amdgcn_sched_barrier(0);
       if (ks < 15) {
 #pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4) af[q4] = an[q4];
+        for (int q4 = 0; q4 < 4; ++q4) aw[q4] = an[q4];
 #pragma unroll
         for (int c = 0; c < CB; ++c) bf[c] = na[c] * nb[c];
       }
@@ -521,9 +408,7 @@ __global__ __launch_bounds__(kV2Threads, 1) void ob_gram2_kernel(const GramArgs 
     }
   };
 
-  // ---- steady state ----
-  const int rot = wave >= 4 ? 2 : 0;  // the two waves of a SIMD do their side work apart
-  uint32_t m_next = 0;                // level-1 count of tile + 2 for replicate `lane` (wave 0)
+  uint32_t m_next = 0;  // wave 0: level-1 count of a later tile for replicate `lane`
   int j = 0;
   for (uint32_t tile = w.t0; tile < w.t1; ++tile) {
     const uint32_t ns = (tile_rows(tile) + 63) >> 6;
@@ -531,36 +416,38 @@ __global__ __launch_bounds__(kV2Threads, 1) void ob_gram2_kernel(const GramArgs 
       const int cur = j & 1;
       const bool last_sub = s + 1 == ns;
       const bool has_next = !last_sub || tile + 1 < w.t1;
-      const uint32_t ntile = last_sub ? tile + 1 : tile;
-      const uint32_t nsub_i = last_sub ? 0 : s + 1;
-      const size_t ngbase = (size_t)ntile * OB_TILE_ROWS + nsub_i * 64;
-      const double* ab = aimg + cur * kAimgDbl + lane;
+      const size_t ngbase = last_sub ? (size_t)(tile + 1) * OB_TILE_ROWS : (size_t)tile * OB_TILE_ROWS + (s + 1) * 64;
+      gbase = (size_t)tile * OB_TILE_ROWS + s * 64;
+      const uint32_t* cw = cnt_img(tile) + (lane & 15) * kCntStride + s * 16;
       const double* xb = xt + cur * buf_dbl;
-      if (has_next && dma) stage_dma(a, w, kV2XtOff + (cur ^ 1) * buf_dbl * 8, ngbase, wave, 0, kV2Waves, lane, lds3);
-      if (draws && wave == 0 && s == 0 && tile + 2 < w.t1) m_next = level1_count(a, w, tile + 2, lane);
-      if (mma) load_k(ab, xb, 0);
+      if (has_next && dma) stage_dma(a, w, kXtOff + (cur ^ 1) * buf_dbl * 8, ngbase, wave, 0, 4, lane, lds3);
+      if (mma) {
+        double va[CB], vb[CB];
+        read_k(cw, xb, 0, aw, va, vb);
+#pragma unroll
+        for (int c = 0; c < CB; ++c) bf[c] = va[c] * vb[c];
+      }
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        if (mma) mma4(ab, xb, g);
-        const int task = (g + rot) & 3;
-        if (task == 0) {
-          // draws: the next tile's calls in slices over steps 0..ns-2 (the last step images it)
-          if (draws && !last_sub && tile + 1 < w.t1)
-            level2_draws(a, w, tile + 1, cnt_img(tile + 1), mc_of(tile + 1), cum_of(tile + 1), (int)s,
-                         (int)ns - 1, wave, kV2Waves, lane);
-        } else if (task == 1) {
-          if (has_next && imaging) build_a(cur ^ 1, ntile, nsub_i, ngbase);
-        } else if (task == 2) {
-          if (draws && last_sub) {
-            if (wave < 4) check_counts(a, cnt_img(tile), mc_of(tile), tid, true);
-            if (wave == 0 && tile + 2 < w.t1) publish_counts(w, tile + 2, m_next, mc_of(tile + 2), cum_of(tile + 2), lane);
+        if (mma) mma4(cw, xb, g);
+        if (g == 0 && draws) {
+          if (s == 0) {
+            if (tile > w.t0) check_counts(a, cnt_img(tile - 1), mc_of(tile - 1), tid, true);
+          } else if (s + 1 < ns && tile + 1 < w.t1) {
+            level2_draws(a, w, tile + 1, cnt_img(tile + 1), mc_of(tile + 1), cum_of(tile + 1), (int)s - 1,
+                         (int)ns - 2, wave, 4, lane);
           }
+        }
+        if (g == 1 && draws && s == 0 && wave == 0) {
+          if (tile > w.t0 && tile + 1 < w.t1) publish_counts(w, tile + 1, m_next, mc_of(tile + 1), cum_of(tile + 1), lane);
+          if (tile + 2 < w.t1) m_next = level1_count(a, w, tile + 2, lane);
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next sub-tile has landed
       lds_barrier();
     }
   }
+  if (draws && w.t0 < w.t1) check_counts(a, cnt_img(w.t1 - 1), mc_of(w.t1 - 1), tid);
   if (mma) store_partials<CB>(a, w, cb0, lane, acc);
 }
 
@@ -867,8 +754,7 @@ int diag_mode() {
   return m;
 }
 
-size_t gram2_lds_bytes(const ob_panel* p) { return (size_t)kV2XtOff + 2 * (size_t)p->k1 * kColStride * 8; }
-bool use_v2(const ob_panel* p) { return gram2_lds_bytes(p) <= 160 * 1024 && !(diag_mode() & 64); }
+size_t gram_lds_bytes(const ob_panel* p) { return (size_t)kXtOff + 2 * (size_t)p->k1 * kColStride * 8; }
 
 // The chunking is a function of the panel only (never of the replicate count or the launch),
 // so a replicate's Gram -- summed over chunks in a fixed order -- is bitwise the same however
@@ -881,12 +767,8 @@ Plan make_plan(const ob_panel* p, uint64_t n_reps, bool unit) {
   Plan pl;
   pl.nb_rep = (uint32_t)((n_reps + 63) / 64);
   pl.rep_pad = pl.nb_rep * 64;
-  const int waves = use_v2(p) ? kV2Waves : 4;
-  if (use_v2(p))
-    pl.cb = p->ncb > kV2Waves ? 2 : 1;
-  else
-    pl.cb = (p->ncb > 8 && !unit) ? 4 : (p->ncb > 4 ? 2 : 1);  // unit variant: CB <= 2 (no spills)
-  pl.n_cg = (uint32_t)((p->ncb + waves * pl.cb - 1) / (waves * pl.cb));
+  pl.cb = (p->ncb > 8 && !unit) ? 4 : (p->ncb > 4 ? 2 : 1);  // the unit variant stays at CB <= 2
+  pl.n_cg = (uint32_t)((p->ncb + 4 * pl.cb - 1) / (4 * pl.cb));
   const uint32_t tT = p->ntiles[0] + p->ntiles[1];
   for (uint32_t g = 0; g < 2; ++g) {
     const uint32_t tg = p->ntiles[g];
@@ -902,14 +784,13 @@ Plan make_plan(const ob_panel* p, uint64_t n_reps, bool unit) {
   return pl;
 }
 
-size_t gram_lds_bytes(const ob_panel* p) { return (size_t)kXtOffset + 2 * (size_t)p->k1 * kColStride * 8; }
 size_t solve_lds_bytes(const ob_panel* p) {
   const int kp = p->k + 1;
   return sizeof(double) * ((size_t)kp * kp + 6 * kp + 3 * (size_t)std::max(p->norm.n_norm, 1));
 }
 
 template <int CB, bool U>
-hipError_t launch_gram_v1(const GramArgs& ga, uint32_t blocks, size_t lds, hipStream_t s) {
+hipError_t launch_gram_t(const GramArgs& ga, uint32_t blocks, size_t lds, hipStream_t s) {
   hipError_t e = hipFuncSetAttribute((const void*)ob_gram_kernel<CB, U>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)lds);
   if (e != hipSuccess) return e;
@@ -917,28 +798,15 @@ hipError_t launch_gram_v1(const GramArgs& ga, uint32_t blocks, size_t lds, hipSt
   return hipGetLastError();
 }
 
-template <int CB, bool U>
-hipError_t launch_gram_v2(const GramArgs& ga, uint32_t blocks, size_t lds, hipStream_t s) {
-  hipError_t e = hipFuncSetAttribute((const void*)ob_gram2_kernel<CB, U>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)lds);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((ob_gram2_kernel<CB, U>), dim3(blocks), dim3(kV2Threads), lds, s, ga);
-  return hipGetLastError();
-}
-
 template <bool U>
 hipError_t launch_gram_u(const ob_panel* p, int cb, const GramArgs& ga, uint32_t blocks, hipStream_t s) {
-  if (use_v2(p)) {
-    const size_t lds = gram2_lds_bytes(p);
-    return cb == 2 ? launch_gram_v2<2, U>(ga, blocks, lds, s) : launch_gram_v2<1, U>(ga, blocks, lds, s);
-  }
   const size_t lds = gram_lds_bytes(p);
   switch (cb) {
     case 4:
-      if constexpr (!U) return launch_gram_v1<4, U>(ga, blocks, lds, s);  // unit plans use CB <= 2
+      if constexpr (!U) return launch_gram_t<4, U>(ga, blocks, lds, s);
       [[fallthrough]];
-    case 2: return launch_gram_v1<2, U>(ga, blocks, lds, s);
-    default: return launch_gram_v1<1, U>(ga, blocks, lds, s);
+    case 2: return launch_gram_t<2, U>(ga, blocks, lds, s);
+    default: return launch_gram_t<1, U>(ga, blocks, lds, s);
   }
 }
 

@@ -1,7 +1,7 @@
 """Ablation timing of the Gram kernel at the bench shape (1M x 20 WLS panel).
 
-OB_GRAM_DIAG bits (read once per process): 1 no level-2 draws, 2 no MFMAs, 4 no sub-tile DMA,
-8 no A image, 64 force the v1 kernel. Prints min/median of 5 runs.
+OB_GRAM_DIAG bits (read once per process): 1 no level-2 draws, 2 no MFMAs, 4 no sub-tile DMA.
+Prints min/median of 5 runs.
 """
 import importlib, os, statistics, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
