@@ -81,11 +81,23 @@ __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t
   const uint32_t ntiles = (n + OB_TILE_ROWS - 1) >> OB_TILE_SHIFT;
   for (uint32_t i = threadIdx.x; i < ntiles; i += kBlock) hist[i] = 0;
   __syncthreads();
-  const uint32_t npairs = (n + 1) >> 1;
-  for (uint32_t p = threadIdx.x; p < npairs; p += kBlock) {
+  const uint32_t ncalls = (n + 3) >> 2, thresh = (0u - n) % n;
+  for (uint32_t p = threadIdx.x; p < ncalls; p += kBlock) {
     const ob_u32x4 u = ob_philox(p, rep, g, OB_TAG_L1, key0, key1);
-    atomicAdd(&hist[ob_mulhi64(u.x, u.y, n) >> OB_TILE_SHIFT], 1u);
-    if (2 * p + 1 < n) atomicAdd(&hist[ob_mulhi64(u.z, u.w, n) >> OB_TILE_SHIFT], 1u);
+    const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (uint32_t h = 0; h < 4; ++h) {
+      const uint32_t d = 4 * p + h;
+      if (d < n) {
+        uint64_t m = (uint64_t)wd[h] * n;
+        for (uint32_t j = 0; (uint32_t)m < thresh; ++j) {  // Lemire rejection, p < n / 2^32
+          const ob_u32x4 r = ob_philox(d, rep, g, OB_TAG_RETRY + (j >> 2), key0, key1);
+          const uint32_t rw[4] = {r.x, r.y, r.z, r.w};
+          m = (uint64_t)rw[j & 3] * n;
+        }
+        atomicAdd(&hist[(uint32_t)(m >> 32) >> OB_TILE_SHIFT], 1u);
+      }
+    }
   }
   __syncthreads();
   const uint32_t toff = g ? tiles0 : 0;

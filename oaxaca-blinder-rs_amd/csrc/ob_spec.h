@@ -6,7 +6,10 @@
 // draws per group, unseeded. OBRS-1 produces the same distribution (an exact multinomial with
 // cell probability 1/n_g) from a counter-based stream so that replicate r is reproducible from
 // (seed, r) alone on any GPU count:
-//   level 1: n_g draws idx = mulhi64(u64, n_g) -> tile = idx / OB_TILE_ROWS  (tile counts m_j)
+//   level 1: n_g draws, four per Philox call (words x,y,z,w of call p -> draws 4p..4p+3), each an
+//            exact uniform idx on [0, n_g) by Lemire's multiply-and-reject on the 32-bit word
+//            (reject iff low32(x n_g) < 2^32 mod n_g; draw d retries on its own stream
+//            {d, rep, g, OB_TAG_RETRY + (j >> 2)}, word j & 3); tile = idx / OB_TILE_ROWS -> m_j
 //   level 2: m_j draws inside tile j (S_j rows). Full tiles (S_j = OB_TILE_ROWS = 2^8): Philox
 //            call p yields draws 16p..16p+15, draw 16p + 4i + b = byte b (LSB first) of output
 //            word i (exactly uniform, independent). The partial last tile: call p yields draws
@@ -26,6 +29,7 @@
 #define OB_TILE_SHIFT 8u
 #define OB_TAG_L1 0x4F425231u /* "OBR1" */
 #define OB_TAG_L2 0x4F425232u /* "OBR2" */
+#define OB_TAG_RETRY 0x52455452u /* "RETR" */
 
 struct ob_u32x4 {
   uint32_t x, y, z, w;

@@ -31,6 +31,7 @@
 #define ORC_TILE 256u
 #define ORC_TAG_L1 0x4F425231u /* "OBR1" */
 #define ORC_TAG_L2 0x4F425232u /* "OBR2" */
+#define ORC_TAG_RETRY 0x52455452u /* "RETR" (+ j >> 2) */
 
 /* Philox4x32-10 (Salmon et al., SC'11; Random123 reference constants). */
 void orc_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
@@ -59,20 +60,33 @@ static inline uint64_t orc_draw_u64(const uint32_t w[4], int odd) {
     return odd ? (((uint64_t)w[3] << 32) | w[2]) : (((uint64_t)w[1] << 32) | w[0]);
 }
 
-/* Level 1: multinomial tile counts m[tile] for (seed, rep, group) from n draws over [0,n). */
+/* Level 1 row index of draw d (exact uniform on [0, n), Lemire's multiply-and-reject on a
+ * 32-bit word x): m = x * n; reject iff low32(m) < (2^32 - n) mod n; accept -> high32(m).
+ * A rejected draw d takes its retries from its own stream: retry j is word (j & 3) of
+ * Philox({d, rep, g, ORC_TAG_RETRY + (j >> 2)}). Rejection probability < n / 2^32. */
+static inline uint32_t orc_level1_index(uint32_t x, uint32_t d, uint32_t rep, uint32_t g, uint32_t n,
+                                        uint32_t thresh, const uint32_t key[2]) {
+    uint64_t m = (uint64_t)x * n;
+    for (uint32_t j = 0; (uint32_t)m < thresh; ++j) {
+        uint32_t ctr[4] = {d, rep, g, ORC_TAG_RETRY + (j >> 2)}, w[4];
+        orc_philox4x32_10(ctr, key, w);
+        m = (uint64_t)w[j & 3] * n;
+    }
+    return (uint32_t)(m >> 32);
+}
+
+/* Level 1: multinomial tile counts m[tile] for (seed, rep, group) from n draws over [0,n):
+ * Philox call p = {p, rep, g, ORC_TAG_L1} gives draws 4p..4p+3 from its words x, y, z, w. */
 void orc_level1_counts(uint64_t seed, uint32_t rep, uint32_t g, uint32_t n, uint32_t* m) {
     uint32_t ntiles = (n + ORC_TILE - 1) / ORC_TILE;
     memset(m, 0, sizeof(uint32_t) * ntiles);
     uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
-    for (uint32_t p = 0; 2u * p < n; ++p) {
+    uint32_t thresh = (0u - n) % n;
+    for (uint32_t p = 0; 4u * p < n; ++p) {
         uint32_t ctr[4] = {p, rep, g, ORC_TAG_L1}, w[4];
         orc_philox4x32_10(ctr, key, w);
-        for (int h = 0; h < 2; ++h) {
-            uint64_t t = 2ull * p + (uint64_t)h;
-            if (t >= n) break;
-            uint32_t idx = orc_mulhi64(orc_draw_u64(w, h), n);
-            m[idx / ORC_TILE]++;
-        }
+        for (uint32_t h = 0; h < 4 && 4u * p + h < n; ++h)
+            m[orc_level1_index(w[h], 4u * p + h, rep, g, n, thresh, key) / ORC_TILE]++;
     }
 }
 
