@@ -94,6 +94,10 @@ typedef struct {
   const int32_t* pooled_start; /* the same on the pooled predictor list (indicator inserted) */
   const int32_t* pooled_idx;
   const int32_t* has_base;     /* 1 if var has a base category (adds a detailed term) */
+  /* outcomes (RIF multi-tau): 0 or 1 = one outcome; n_y > 1: each group's
+     y is an n x n_y column-major block with leading dimension ldx, and every replicate yields
+     n_y rows (one per outcome) from one Gram pass. */
+  int32_t n_y;
 } ob_panel_desc;
 
 typedef struct ob_panel ob_panel;
@@ -105,15 +109,19 @@ void ob_panel_destroy(ob_panel* panel);
 int ob_panel_row_len(const ob_panel* panel);
 int ob_panel_k(const ob_panel* panel);
 int ob_panel_n_base(const ob_panel* panel);
+int ob_panel_n_y(const ob_panel* panel);
 
 /* Point estimate: run_single_pass on the unresampled data (builder.rs:810-811).
-   resid_b (n_b entries, may be NULL) receives y_B - X_B beta_B (OaxacaResults::residuals). */
+   resid_b (n_b entries, may be NULL) receives y_B - X_B beta_B (OaxacaResults::residuals).
+   With n_y outcomes: row holds n_y x row_len, resid_b n_y x n_b (outcome-major). */
 int ob_point_estimate(ob_panel* panel, int ref_mode, double* row, double* resid_b);
 
 /* Bootstrap replicates [first_rep, first_rep + n_reps) of the OBRS-1 stream keyed by seed.
    rows: n_reps x ob_panel_row_len(); ok[r] = 0 marks a replicate the reference would drop
    (filter_map + .ok(), builder.rs:816-839): Cholesky failure or zero total weight. Results are
-   a pure function of (seed, replicate id): identical on 1 or 8 GPUs. */
+   a pure function of (seed, replicate id): identical on 1 or 8 GPUs. With n_y outcomes rows
+   holds n_y x n_reps x row_len and ok n_y x n_reps (outcome-major blocks); each outcome's block
+   is bitwise the rows a one-outcome panel of that y gives. */
 int ob_boot_run(ob_panel* panel, uint64_t seed, uint64_t first_rep, uint64_t n_reps, int ref_mode,
                 double* rows, uint8_t* ok);
 /* Same, rows/ok in device memory, enqueued on hip_stream (hipStream_t; NULL = engine stream).
@@ -187,6 +195,7 @@ typedef struct ob_matrices ob_matrices;
 int ob_builder_prepare(ob_ctx* ctx, const ob_column* cols, int32_t n_cols, int64_t n_rows,
                        const ob_builder_config* cfg, ob_prepared** out);
 int ob_prepared_row_len(const ob_prepared* prep);
+int ob_prepared_n_y(const ob_prepared* prep);
 uint64_t ob_prepared_seed(const ob_prepared* prep);
 ob_panel* ob_prepared_panel(ob_prepared* prep);
 int ob_prepared_boot(ob_prepared* prep, uint64_t first_rep, uint64_t n_reps, double* rows, uint8_t* ok);
@@ -203,6 +212,12 @@ int ob_builder_run(ob_ctx* ctx, const ob_column* cols, int32_t n_cols, int64_t n
 /* OaxacaBuilder::decompose_quantile (builder.rs:711-757). */
 int ob_builder_decompose_quantile(ob_ctx* ctx, const ob_column* cols, int32_t n_cols, int64_t n_rows,
                                   const ob_builder_config* cfg, double quantile, ob_results** out);
+/* Several quantiles in one run: out[t] = decompose_quantile(taus[t]),
+   bitwise, from one panel whose outcomes are the n_taus RIF columns, so one Gram pass and one
+   resample per replicate serve every tau. out must hold n_taus slots. */
+int ob_builder_decompose_quantiles(ob_ctx* ctx, const ob_column* cols, int32_t n_cols, int64_t n_rows,
+                                   const ob_builder_config* cfg, const double* taus, int32_t n_taus,
+                                   ob_results** out);
 /* OaxacaBuilder::get_data_matrices (builder.rs:252-291). Host only: needs no GPU. */
 int ob_builder_data_matrices(const ob_column* cols, int32_t n_cols, int64_t n_rows,
                              const ob_builder_config* cfg, ob_matrices** out);

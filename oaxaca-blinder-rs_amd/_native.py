@@ -25,12 +25,13 @@ OB_VEC_RESIDUALS, OB_VEC_XA_MEAN, OB_VEC_XB_MEAN, OB_VEC_BETA_STAR = 0, 1, 2, 3
 # Every exported entry point of include/oaxaca_boot.h (tests/test_capi_exports.py checks both ways).
 EXPORTED = (
     "ob_last_error", "ob_version", "ob_device_count", "ob_ctx_create", "ob_ctx_destroy",
-    "ob_panel_create", "ob_panel_destroy", "ob_panel_row_len", "ob_panel_k", "ob_panel_n_base",
+    "ob_panel_create", "ob_panel_destroy", "ob_panel_row_len", "ob_panel_k", "ob_panel_n_base", "ob_panel_n_y",
     "ob_point_estimate", "ob_boot_run", "ob_boot_run_device", "ob_panel_last_timing", "ob_panel_sync",
     "ob_bootstrap_stats", "ob_aggregate", "ob_rif",
-    "ob_builder_prepare", "ob_prepared_row_len", "ob_prepared_seed", "ob_prepared_panel",
+    "ob_builder_prepare", "ob_prepared_row_len", "ob_prepared_n_y", "ob_prepared_seed", "ob_prepared_panel",
     "ob_prepared_boot", "ob_prepared_boot_device", "ob_prepared_finish", "ob_prepared_destroy",
-    "ob_builder_run", "ob_builder_decompose_quantile", "ob_builder_data_matrices",
+    "ob_builder_run", "ob_builder_decompose_quantile", "ob_builder_decompose_quantiles",
+    "ob_builder_data_matrices",
     "ob_results_total_gap", "ob_results_n_a", "ob_results_n_b", "ob_results_n_failed",
     "ob_results_count", "ob_results_component", "ob_results_vector", "ob_results_free",
     "ob_matrices_dims", "ob_matrices_get", "ob_matrices_name", "ob_matrices_free",
@@ -55,7 +56,8 @@ class ob_panel_desc(C.Structure):
                 ("a", ob_group_desc), ("b", ob_group_desc), ("n_norm", C.c_int32),
                 ("norm_start", C.POINTER(C.c_int32)), ("norm_idx", C.POINTER(C.c_int32)),
                 ("norm_m", C.POINTER(C.c_int32)), ("pooled_start", C.POINTER(C.c_int32)),
-                ("pooled_idx", C.POINTER(C.c_int32)), ("has_base", C.POINTER(C.c_int32))]
+                ("pooled_idx", C.POINTER(C.c_int32)), ("has_base", C.POINTER(C.c_int32)),
+                ("n_y", C.c_int32)]
 
 
 class ob_timing(C.Structure):
@@ -100,6 +102,7 @@ _SIGS = {
     "ob_panel_row_len": (C.c_int, [_P]),
     "ob_panel_k": (C.c_int, [_P]),
     "ob_panel_n_base": (C.c_int, [_P]),
+    "ob_panel_n_y": (C.c_int, [_P]),
     "ob_point_estimate": (C.c_int, [_P, C.c_int, _D, _D]),
     "ob_boot_run": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, _D, _U8]),
     "ob_boot_run_device": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, _P, _P, _P]),
@@ -111,6 +114,7 @@ _SIGS = {
     "ob_builder_prepare": (C.c_int, [_P, C.POINTER(ob_column), C.c_int32, C.c_int64,
                                      C.POINTER(ob_builder_config), C.POINTER(_P)]),
     "ob_prepared_row_len": (C.c_int, [_P]),
+    "ob_prepared_n_y": (C.c_int, [_P]),
     "ob_prepared_seed": (C.c_uint64, [_P]),
     "ob_prepared_panel": (_P, [_P]),
     "ob_prepared_boot": (C.c_int, [_P, C.c_uint64, C.c_uint64, _D, _U8]),
@@ -121,6 +125,8 @@ _SIGS = {
                                  C.POINTER(ob_builder_config), C.POINTER(_P)]),
     "ob_builder_decompose_quantile": (C.c_int, [_P, C.POINTER(ob_column), C.c_int32, C.c_int64,
                                                 C.POINTER(ob_builder_config), C.c_double, C.POINTER(_P)]),
+    "ob_builder_decompose_quantiles": (C.c_int, [_P, C.POINTER(ob_column), C.c_int32, C.c_int64,
+                                                 C.POINTER(ob_builder_config), _D, C.c_int32, C.POINTER(_P)]),
     "ob_builder_data_matrices": (C.c_int, [C.POINTER(ob_column), C.c_int32, C.c_int64,
                                            C.POINTER(ob_builder_config), C.POINTER(_P)]),
     "ob_results_total_gap": (C.c_double, [_P]),

@@ -353,6 +353,22 @@ class OaxacaBuilder:
                                                   float(quantile), C.byref(h)))
         return _results_from_c(h)
 
+    def decompose_quantiles(self, quantiles) -> list:
+        """RIF decompositions at several quantiles in one run: one panel
+        whose outcomes are the RIF columns, so every replicate's resample and Gram pass serve all
+        quantiles. Element t equals ``decompose_quantile(quantiles[t])`` bitwise (same seed)."""
+        lib = N.lib()
+        taus = np.ascontiguousarray(quantiles, dtype=np.float64)
+        if taus.ndim != 1 or taus.size == 0:
+            raise ValueError("quantiles must be a non-empty 1-D sequence")
+        cols, ncol, nrow = self._frame.as_c()
+        cfg, keep = self._config()
+        hs = (C.c_void_p * taus.size)()
+        N.check(lib.ob_builder_decompose_quantiles(N.context(self._device), cols, ncol, nrow, C.byref(cfg),
+                                                   taus.ctypes.data_as(C.POINTER(C.c_double)), int(taus.size),
+                                                   C.cast(hs, C.POINTER(C.c_void_p))))
+        return [_results_from_c(C.c_void_p(h)) for h in hs]
+
     def prepare(self) -> "PreparedRun":
         """clean/dummies/split/upload/point estimate once; replicate ranges run separately
         (the multi-GPU path in ``distributed.py``)."""
@@ -447,6 +463,10 @@ class OaxacaBlinder:
 
     def fit_quantile(self, quantile: float) -> OaxacaResults:
         return self._create_builder().decompose_quantile(quantile)
+
+    def fit_quantiles(self, quantiles) -> list:
+        """Several RIF quantiles sharing one bootstrap (``OaxacaBuilder.decompose_quantiles``)."""
+        return self._create_builder().decompose_quantiles(quantiles)
 
     def optimize_budget(self, budget: float, target_gap: float):
         b = self._create_builder()

@@ -49,6 +49,7 @@ struct Frame {
 
 struct Config {
   std::string outcome, group, reference_group;
+  std::vector<std::string> outcomes;  // RIF multi-tau: y columns of one panel (empty: {outcome})
   std::vector<std::string> predictors, categorical, normalize;
   bool has_weights = false;
   std::string weights;
@@ -285,8 +286,13 @@ static int prepare_data(const Frame& f, const std::vector<int64_t>& rows, const 
   const size_t p = c.predictors.size() + dummy_names.size();
   d.n = n;
   d.x.assign((size_t)n * p, 0.0);
-  d.y.resize(n);
-  for (int64_t r = 0; r < n; ++r) d.y[r] = f.cols[yi].f[rows[r]];
+  const size_t ny = c.outcomes.empty() ? 1 : c.outcomes.size();
+  d.y.resize((size_t)n * ny);  // column-major n x ny
+  for (size_t t = 0; t < ny; ++t) {
+    const int ti = c.outcomes.empty() ? yi : f.find(c.outcomes[t]);
+    if (ti < 0 || f.cols[ti].kind != OB_COL_F64) return fail(OB_E_INVALID, "outcome column %zu missing", t);
+    for (int64_t r = 0; r < n; ++r) d.y[t * n + r] = f.cols[ti].f[rows[r]];
+  }
   size_t col = 0;
   for (const auto& name : c.predictors) {
     const int ci = f.find(name);
@@ -371,8 +377,9 @@ struct ob_prepared {
   int k = 0, n_base = 0, row_len = 0;
   std::vector<std::string> names;         // K final predictor names
   std::vector<std::string> detail_names;  // K + n_base (base categories appended)
-  std::vector<double> point_row, resid_b;
+  std::vector<double> point_row, resid_b;  // n_y x row_len, n_y x n_b
   int64_t n_a = 0, n_b = 0;
+  int n_y = 1;
 };
 
 struct ob_matrices {
@@ -449,6 +456,7 @@ static int prepare(ob_ctx* ctx, const Frame& input, const Config& c, ob_prepared
   pd.pooled_start = pstart.data();
   pd.pooled_idx = pidx.data();
   pd.has_base = has.data();
+  pd.n_y = c.outcomes.empty() ? 1 : (int32_t)c.outcomes.size();
   ob_prepared* pr = new ob_prepared();
   pr->ctx = ctx;
   pr->cfg = c;
@@ -467,8 +475,9 @@ static int prepare(ob_ctx* ctx, const Frame& input, const Config& c, ob_prepared
   pr->detail_names.insert(pr->detail_names.end(), base_names.begin(), base_names.end());
   pr->n_a = da.n;
   pr->n_b = db.n;
-  pr->point_row.assign(pr->row_len, 0.0);
-  pr->resid_b.assign(db.n, 0.0);
+  pr->n_y = pd.n_y;
+  pr->point_row.assign((size_t)pr->row_len * pr->n_y, 0.0);
+  pr->resid_b.assign((size_t)db.n * pr->n_y, 0.0);
   rc = ob_point_estimate(pr->panel, pr->ref, pr->point_row.data(), pr->resid_b.data());
   if (rc != OB_OK) {
     ob_panel_destroy(pr->panel);
@@ -479,9 +488,11 @@ static int prepare(ob_ctx* ctx, const Frame& input, const Config& c, ob_prepared
   return OB_OK;
 }
 
-// builder.rs:841-950 over successful rows in replicate order.
-static int finish(const ob_prepared* pr, const double* rows, const uint8_t* ok, uint64_t n_reps, ob_results** out) {
+// builder.rs:841-950 over successful rows in replicate order, for outcome t (rows/ok: its block).
+static int finish(const ob_prepared* pr, int t_out, const double* rows, const uint8_t* ok, uint64_t n_reps,
+                  ob_results** out) {
   const int k = pr->k, kd = k + pr->n_base, rl = pr->row_len;
+  const double* point_row = pr->point_row.data() + (size_t)t_out * rl;
   uint64_t ng = 0;
   for (uint64_t r = 0; r < n_reps; ++r) ng += ok[r] ? 1 : 0;
   if (ng < n_reps)
@@ -490,12 +501,12 @@ static int finish(const ob_prepared* pr, const double* rows, const uint8_t* ok, 
             "%llu successful replications.\n",
             (unsigned long long)(n_reps - ng), (unsigned long long)n_reps, (unsigned long long)ng);
   ob_results* res = new ob_results();
-  res->total_gap = pr->point_row[OB_ROW_TOTAL_GAP];
+  res->total_gap = point_row[OB_ROW_TOTAL_GAP];
   res->n_a = pr->n_a;
   res->n_b = pr->n_b;
   res->n_failed = (int64_t)(n_reps - ng);
-  res->residuals = pr->resid_b;
-  const double* tail = pr->point_row.data() + 6 + 2 * kd;
+  res->residuals.assign(pr->resid_b.begin() + (size_t)t_out * pr->n_b, pr->resid_b.begin() + (size_t)(t_out + 1) * pr->n_b);
+  const double* tail = point_row + 6 + 2 * kd;
   res->xa_mean.assign(tail + 2 * k, tail + 3 * k);
   res->xb_mean.assign(tail + 3 * k, tail + 4 * k);
   res->beta_star.assign(tail + 4 * k, tail + 5 * k);
@@ -509,14 +520,14 @@ static int finish(const ob_prepared* pr, const double* rows, const uint8_t* ok, 
   std::vector<Job> jobs;
   const char* two[2] = {"explained", "unexplained"};
   const char* three[3] = {"endowments", "coefficients", "interaction"};
-  for (int i = 0; i < 2; ++i) jobs.push_back({OB_TABLE_TWO_FOLD, two[i], pr->point_row[i], {i}});
-  for (int i = 0; i < 3; ++i) jobs.push_back({OB_TABLE_THREE_FOLD, three[i], pr->point_row[2 + i], {2 + i}});
+  for (int i = 0; i < 2; ++i) jobs.push_back({OB_TABLE_TWO_FOLD, two[i], point_row[i], {i}});
+  for (int i = 0; i < 3; ++i) jobs.push_back({OB_TABLE_THREE_FOLD, three[i], point_row[2 + i], {2 + i}});
   // process_detailed_components: estimates merged by variable name (builder.rs:963-971)
   for (int t = 0; t < 2; ++t) {
     const int base = 6 + t * kd;
     for (int i = 0; i < kd; ++i) {
       Job j{t == 0 ? OB_TABLE_DETAILED_EXPLAINED : OB_TABLE_DETAILED_UNEXPLAINED, pr->detail_names[i],
-            pr->point_row[base + i], {}};
+            point_row[base + i], {}};
       for (int q = 0; q < kd; ++q)
         if (pr->detail_names[q] == pr->detail_names[i]) j.cols.push_back(base + q);
       jobs.push_back(std::move(j));
@@ -537,14 +548,23 @@ static int finish(const ob_prepared* pr, const double* rows, const uint8_t* ok, 
   return OB_OK;
 }
 
+// prepare + every replicate + finish for each outcome: out[t] for t < n_y (OaxacaBuilder::run).
 static int run_all(ob_ctx* ctx, const Frame& f, const Config& c, ob_results** out) {
   ob_prepared* pr = nullptr;
   OB_TRY(prepare(ctx, f, c, &pr));
-  std::vector<double> rows((size_t)c.reps * pr->row_len);
-  std::vector<uint8_t> ok(c.reps, 0);
+  const size_t ny = (size_t)pr->n_y;
+  std::vector<double> rows((size_t)c.reps * pr->row_len * ny);
+  std::vector<uint8_t> ok(c.reps * ny, 0);
   int rc = OB_OK;
   if (c.reps > 0) rc = ob_boot_run(pr->panel, pr->seed, 0, c.reps, pr->ref, rows.data(), ok.data());
-  if (rc == OB_OK) rc = finish(pr, rows.data(), ok.data(), c.reps, out);
+  for (size_t t = 0; t < ny && rc == OB_OK; ++t) {
+    rc = finish(pr, (int)t, rows.data() + t * c.reps * pr->row_len, ok.data() + t * c.reps, c.reps, &out[t]);
+    if (rc != OB_OK)
+      for (size_t u = 0; u < t; ++u) {
+        delete out[u];
+        out[u] = nullptr;
+      }
+  }
   ob_panel_destroy(pr->panel);
   delete pr;
   return rc;
@@ -566,6 +586,7 @@ int ob_builder_prepare(ob_ctx* ctx, const ob_column* cols, int32_t n_cols, int64
 }
 
 int ob_prepared_row_len(const ob_prepared* p) { return p ? p->row_len : 0; }
+int ob_prepared_n_y(const ob_prepared* p) { return p ? p->n_y : 0; }
 uint64_t ob_prepared_seed(const ob_prepared* p) { return p ? p->seed : 0; }
 ob_panel* ob_prepared_panel(ob_prepared* p) { return p ? p->panel : nullptr; }
 
@@ -583,7 +604,7 @@ int ob_prepared_boot_device(ob_prepared* p, uint64_t first_rep, uint64_t n_reps,
 int ob_prepared_finish(ob_prepared* p, const double* rows, const uint8_t* ok, uint64_t n_reps, ob_results** out) {
   if (!p || !out || (n_reps && (!rows || !ok))) return ob::fail(OB_E_INVALID, "null pointer");
   *out = nullptr;
-  return ob::finish(p, rows, ok, n_reps, out);
+  return ob::finish(p, 0, rows, ok, n_reps, out);
 }
 
 void ob_prepared_destroy(ob_prepared* p) {
@@ -603,11 +624,13 @@ int ob_builder_run(ob_ctx* ctx, const ob_column* cols, int32_t n_cols, int64_t n
   return ob::run_all(ctx, f, c, out);
 }
 
-// builder.rs:711-757: RIF of each group's outcome on the cleaned data, then run() on vstack(A, B)
-int ob_builder_decompose_quantile(ob_ctx* ctx, const ob_column* cols, int32_t n_cols, int64_t n_rows,
-                                  const ob_builder_config* cfg, double quantile, ob_results** out) {
-  if (!ctx || !out) return ob::fail(OB_E_INVALID, "null pointer");
-  *out = nullptr;
+// builder.rs:711-757: RIF of each group's outcome on the cleaned data, then run() on vstack(A, B).
+// Several quantiles share one panel: the RIF columns are the panel's outcomes (n_y = n_taus), so
+// one Gram pass serves every tau; out[t] is bitwise the single-tau run.
+static int decompose_quantiles(ob_ctx* ctx, const ob_column* cols, int32_t n_cols, int64_t n_rows,
+                               const ob_builder_config* cfg, const double* taus, int32_t n_taus, ob_results** out) {
+  if (!ctx || !out || !taus || n_taus < 1) return ob::fail(OB_E_INVALID, "null pointer or no quantiles");
+  for (int32_t t = 0; t < n_taus; ++t) out[t] = nullptr;
   ob::Frame f, df;
   ob::Config c;
   OB_TRY(ob::config_from(cfg, c));
@@ -623,15 +646,38 @@ int ob_builder_decompose_quantile(ob_ctx* ctx, const ob_column* cols, int32_t n_
   order.insert(order.end(), sp.b.begin(), sp.b.end());
   ob::Frame mod = ob::take(df, order);
   const int mi = mod.find(c.outcome);
-  std::vector<double> ya(sp.a.size()), yb(sp.b.size()), ra(sp.a.size()), rb(sp.b.size());
-  for (size_t i = 0; i < sp.a.size(); ++i) ya[i] = mod.cols[mi].f[i];
-  for (size_t i = 0; i < sp.b.size(); ++i) yb[i] = mod.cols[mi].f[sp.a.size() + i];
-  ob::rif(ya.data(), (int64_t)ya.size(), quantile, ra.data());
-  ob::rif(yb.data(), (int64_t)yb.size(), quantile, rb.data());
-  for (size_t i = 0; i < sp.a.size(); ++i) mod.cols[mi].f[i] = ra[i];
-  for (size_t i = 0; i < sp.b.size(); ++i) mod.cols[mi].f[sp.a.size() + i] = rb[i];
+  const size_t na = sp.a.size(), nb = sp.b.size();
+  std::vector<double> ya(na), yb(nb), ra(na), rb(nb);
+  for (size_t i = 0; i < na; ++i) ya[i] = mod.cols[mi].f[i];
+  for (size_t i = 0; i < nb; ++i) yb[i] = mod.cols[mi].f[na + i];
+  for (int32_t t = 0; t < n_taus; ++t) {
+    ob::rif(ya.data(), (int64_t)na, taus[t], ra.data());
+    ob::rif(yb.data(), (int64_t)nb, taus[t], rb.data());
+    ob::Col rc = mod.cols[mi];
+    rc.name = "__ob_rif_" + std::to_string(t) + "__";
+    for (size_t i = 0; i < na; ++i) rc.f[i] = ra[i];
+    for (size_t i = 0; i < nb; ++i) rc.f[na + i] = rb[i];
+    if (n_taus == 1) {
+      mod.cols[mi] = std::move(rc);  // the reference's own layout: the outcome column replaced
+      mod.cols[mi].name = c.outcome;
+    } else {
+      c.outcomes.push_back(rc.name);
+      mod.cols.push_back(std::move(rc));
+    }
+  }
   c.has_selection = false;  // the new builder carries no Heckman settings (builder.rs:743-754)
   return ob::run_all(ctx, mod, c, out);
+}
+
+int ob_builder_decompose_quantile(ob_ctx* ctx, const ob_column* cols, int32_t n_cols, int64_t n_rows,
+                                  const ob_builder_config* cfg, double quantile, ob_results** out) {
+  return decompose_quantiles(ctx, cols, n_cols, n_rows, cfg, &quantile, 1, out);
+}
+
+int ob_builder_decompose_quantiles(ob_ctx* ctx, const ob_column* cols, int32_t n_cols, int64_t n_rows,
+                                   const ob_builder_config* cfg, const double* taus, int32_t n_taus,
+                                   ob_results** out) {
+  return decompose_quantiles(ctx, cols, n_cols, n_rows, cfg, taus, n_taus, out);
 }
 
 int ob_builder_data_matrices(const ob_column* cols, int32_t n_cols, int64_t n_rows, const ob_builder_config* cfg,

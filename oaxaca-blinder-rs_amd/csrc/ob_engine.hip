@@ -489,6 +489,7 @@ __global__ __launch_bounds__(kBlock) void ob_reduce_kernel(const double* partial
 struct SolveArgs {
   const double* gram;  // [rep][2][e_pad]
   int e_pad, k1, k, pool_pos, ref_mode, weighted;
+  int yc;  // the outcome's column in the extended Gram (p + 1 + t)
   double rows_a, rows_b;
   int n_norm, n_base;
   const int32_t* norm;  // start[n_norm+1] | idx | m[n_norm] | pstart[n_norm+1] | pidx | has_base[n_norm]
@@ -592,7 +593,7 @@ __global__ __launch_bounds__(64) void ob_solve_kernel(const SolveArgs a) {
       const int r = i % k, c = i / k;
       M[r + c * k] = gpair(G, r, c, k1);
     }
-    for (int i = lane; i < k; i += 64) rhs[i] = gpair(G, i, k1 - 1, k1);
+    for (int i = lane; i < k; i += 64) rhs[i] = gpair(G, i, a.yc, k1);
     __syncthreads();
     if (!wave_cholesky(M, k, lane)) {
       status = 0;
@@ -661,10 +662,10 @@ __global__ __launch_bounds__(64) void ob_solve_kernel(const SolveArgs a) {
       }
       for (int u = lane; u < kp; u += 64) {
         if (u == ip) {
-          rhs[u] = gpair(GA, 0, k1 - 1, k1);
+          rhs[u] = gpair(GA, 0, a.yc, k1);
         } else {
           const int o = u < ip ? u : u - 1;
-          rhs[u] = gpair(GA, o, k1 - 1, k1) + gpair(GB, o, k1 - 1, k1);
+          rhs[u] = gpair(GA, o, a.yc, k1) + gpair(GB, o, a.yc, k1);
         }
       }
       __syncthreads();
@@ -724,7 +725,7 @@ __global__ __launch_bounds__(64) void ob_solve_kernel(const SolveArgs a) {
       row[2] = endow;
       row[3] = coef;
       row[4] = inter;
-      row[5] = gpair(GA, 0, k1 - 1, k1) / GA[0] - gpair(GB, 0, k1 - 1, k1) / GB[0];  // builder.rs:676-684
+      row[5] = gpair(GA, 0, a.yc, k1) / GA[0] - gpair(GB, 0, a.yc, k1) / GB[0];  // builder.rs:676-684
       double* tail = row + 6 + 2 * kd;
       for (int j = 0; j < k; ++j) {
         tail[j] = beta_a[j];
@@ -740,12 +741,12 @@ __global__ __launch_bounds__(64) void ob_solve_kernel(const SolveArgs a) {
 
 // y_B - X_B beta_B on the unresampled group B (ols.rs:118-119; OaxacaResults::residuals).
 __global__ __launch_bounds__(kBlock) void ob_residual_kernel(const double* cols, int64_t ld, uint32_t n, int p,
-                                                             const double* beta, double* out) {
+                                                             int ycol, const double* beta, double* out) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   double yh = beta[0];
   for (int c = 0; c < p; ++c) yh += cols[(size_t)c * ld + i] * beta[1 + c];
-  out[i] = cols[(size_t)p * ld + i] - yh;
+  out[i] = cols[(size_t)ycol * ld + i] - yh;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -826,13 +827,14 @@ hipError_t launch_gram(const ob_panel* p, int cb, bool unit, const GramArgs& ga,
   return unit ? launch_gram_u<true>(p, cb, ga, blocks, s) : launch_gram_u<false>(p, cb, ga, blocks, s);
 }
 
-// Gram panel of a weighted design: [sqrt(w), sqrt(w) x_1..x_p, sqrt(w) y] (ols.rs:68-78).
-__global__ __launch_bounds__(kBlock) void ob_scale_kernel(const double* cols, int64_t ld, int p, double* gcols) {
+// Gram panel of a weighted design: [sqrt(w), sqrt(w) x_1..x_p, sqrt(w) y_1..] (ols.rs:68-78).
+// cols: nxy = p + n_y columns, then w.
+__global__ __launch_bounds__(kBlock) void ob_scale_kernel(const double* cols, int64_t ld, int nxy, double* gcols) {
   const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
   if (i >= (size_t)ld) return;
-  const double sw = sqrt(cols[(size_t)(p + 1) * ld + i]);
+  const double sw = sqrt(cols[(size_t)nxy * ld + i]);
   gcols[i] = sw;
-  for (int c = 0; c <= p; ++c) gcols[(size_t)(c + 1) * ld + i] = sw * cols[(size_t)c * ld + i];
+  for (int c = 0; c < nxy; ++c) gcols[(size_t)(c + 1) * ld + i] = sw * cols[(size_t)c * ld + i];
 }
 
 template <typename T>
@@ -854,6 +856,7 @@ SolveArgs solve_args(const ob_panel* p, int ref_mode) {
   sa.pool_pos = 1 + p->n_num;
   sa.ref_mode = ref_mode;
   sa.weighted = p->weighted;
+  sa.yc = p->p + 1;
   sa.rows_a = (double)p->n[0];
   sa.rows_b = (double)p->n[1];
   sa.n_norm = p->norm.n_norm;
@@ -926,10 +929,10 @@ int engine_point_estimate(ob_panel* p, int ref_mode, double* row, double* resid_
   }
     PE_OK(hipMalloc(&d_partial, sizeof(double) * (size_t)nch * pl.rep_pad * p->e_pad));
     PE_OK(hipMalloc(&d_gram, sizeof(double) * 2 * (size_t)pl.rep_pad * p->e_pad));
-    PE_OK(hipMalloc(&d_row, sizeof(double) * p->row_len));
+    PE_OK(hipMalloc(&d_row, sizeof(double) * p->row_len * p->n_y));
     PE_OK(hipMalloc(&d_gout, sizeof(double) * 2 * p->e_pad));
     PE_OK(hipMalloc(&d_chunks, sizeof(uint32_t) * pl.chunks.size()));
-    PE_OK(hipMalloc(&d_ok, 1));
+    PE_OK(hipMalloc(&d_ok, p->n_y));
     PE_OK(hipMemcpyAsync(d_chunks, pl.chunks.data(), sizeof(uint32_t) * pl.chunks.size(), hipMemcpyHostToDevice, s));
     GramArgs ga = gram_args(p, pl);
     ga.chunks = d_chunks;
@@ -943,20 +946,23 @@ int engine_point_estimate(ob_panel* p, int ref_mode, double* row, double* resid_
     hipLaunchKernelGGL(ob_reduce_kernel, dim3((unsigned)((nred + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
                        (const double*)d_partial, (const uint32_t*)d_chunks, nch, pl.rep_pad, p->e_pad, 1u, d_gram);
     PE_OK(hipGetLastError());
-    SolveArgs sa = solve_args(p, ref_mode);
-    sa.gram = d_gram;
-    sa.rows = d_row;
-    sa.ok = d_ok;
-    sa.n_reps = 1;
-    sa.gram_out = d_gout;
-    sa.raw_status = 1;
-    PE_OK(hipMalloc(&d_beta, sizeof(double) * p->k));
-    sa.raw_beta_b = d_beta;
-    hipLaunchKernelGGL(ob_solve_kernel, dim3(1), dim3(64), solve_lds_bytes(p), s, sa);
-    PE_OK(hipGetLastError());
+    PE_OK(hipMalloc(&d_beta, sizeof(double) * p->k * p->n_y));
+    for (int t = 0; t < p->n_y; ++t) {
+      SolveArgs sa = solve_args(p, ref_mode);
+      sa.yc = p->p + 1 + t;
+      sa.gram = d_gram;
+      sa.rows = d_row + (size_t)t * p->row_len;
+      sa.ok = d_ok + t;
+      sa.n_reps = 1;
+      sa.gram_out = t == 0 ? d_gout : nullptr;
+      sa.raw_status = 1;
+      sa.raw_beta_b = d_beta + (size_t)t * p->k;
+      hipLaunchKernelGGL(ob_solve_kernel, dim3(1), dim3(64), solve_lds_bytes(p), s, sa);
+      PE_OK(hipGetLastError());
+    }
     uint8_t okh = 0;
     std::vector<double> gout(2 * p->e_pad);
-    PE_OK(hipMemcpyAsync(row, d_row, sizeof(double) * p->row_len, hipMemcpyDeviceToHost, s));
+    PE_OK(hipMemcpyAsync(row, d_row, sizeof(double) * p->row_len * p->n_y, hipMemcpyDeviceToHost, s));
     PE_OK(hipMemcpyAsync(&okh, d_ok, 1, hipMemcpyDeviceToHost, s));
     PE_OK(hipMemcpyAsync(gout.data(), d_gout, sizeof(double) * gout.size(), hipMemcpyDeviceToHost, s));
     PE_OK(hipStreamSynchronize(s));
@@ -973,11 +979,12 @@ int engine_point_estimate(ob_panel* p, int ref_mode, double* row, double* resid_
     }
     if (resid_b) {
       PE_OK(hipMalloc(&d_res, sizeof(double) * std::max<uint32_t>(p->n[1], 1)));
-      if (p->n[1] > 0) {
+      for (int t = 0; t < p->n_y && p->n[1] > 0; ++t) {  // the kernel-stream order serializes d_res reuse
         hipLaunchKernelGGL(ob_residual_kernel, dim3((p->n[1] + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
-                           (const double*)p->d_cols[1], p->ld[1], p->n[1], p->p, (const double*)d_beta, d_res);
+                           (const double*)p->d_cols[1], p->ld[1], p->n[1], p->p, p->p + t,
+                           (const double*)(d_beta + (size_t)t * p->k), d_res);
         PE_OK(hipGetLastError());
-        PE_OK(hipMemcpyAsync(resid_b, d_res, sizeof(double) * p->n[1], hipMemcpyDeviceToHost, s));
+        PE_OK(hipMemcpyAsync(resid_b + (size_t)t * p->n[1], d_res, sizeof(double) * p->n[1], hipMemcpyDeviceToHost, s));
       }
       PE_OK(hipStreamSynchronize(s));
     }
@@ -1061,16 +1068,19 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
                        p->d_gram);
     HIP_OK(hipGetLastError());
     if (timed) HIP_OK(hipEventRecord(ev[3], s));
-    SolveArgs sa = solve_args(p, ref_mode);
-    sa.gram = p->d_gram;
-    sa.rows = d_rows + (size_t)s0 * p->row_len;
-    sa.ok = d_ok + s0;
-    sa.n_reps = ns;
-    sa.gram_out = nullptr;
-    sa.raw_beta_b = nullptr;
-    sa.raw_status = 0;
-    hipLaunchKernelGGL(ob_solve_kernel, dim3(ns), dim3(64), solve_lds_bytes(p), s, sa);
-    HIP_OK(hipGetLastError());
+    for (int t = 0; t < p->n_y; ++t) {  // outcome-major row blocks
+      SolveArgs sa = solve_args(p, ref_mode);
+      sa.yc = p->p + 1 + t;
+      sa.gram = p->d_gram;
+      sa.rows = d_rows + ((size_t)t * n_reps + s0) * p->row_len;
+      sa.ok = d_ok + (size_t)t * n_reps + s0;
+      sa.n_reps = ns;
+      sa.gram_out = nullptr;
+      sa.raw_beta_b = nullptr;
+      sa.raw_status = 0;
+      hipLaunchKernelGGL(ob_solve_kernel, dim3(ns), dim3(64), solve_lds_bytes(p), s, sa);
+      HIP_OK(hipGetLastError());
+    }
     if (timed) HIP_OK(hipEventRecord(ev[4], s));
     p->timing.gram_launches += 1;
     p->pending_segments += 1;
@@ -1156,6 +1166,8 @@ int ob_panel_create(ob_ctx* ctx, const ob_panel_desc* d, ob_panel** out) {
   if (!ctx || !d || !out) return ob::fail(OB_E_INVALID, "null pointer");
   *out = nullptr;
   if (d->p < 0 || d->p > 120) return ob::fail(OB_E_UNSUPPORTED, "predictor columns must be in [0, 120], got %d", d->p);
+  if (d->n_y < 0 || d->p + std::max(1, (int)d->n_y) > 121)
+    return ob::fail(OB_E_UNSUPPORTED, "outcome columns must be in [1, %d], got %d", 121 - d->p, d->n_y);
   if (d->n_num < 0 || d->n_num > d->p) return ob::fail(OB_E_INVALID, "n_num out of range");
   const ob_group_desc* gd[2] = {&d->a, &d->b};
   for (int g = 0; g < 2; ++g) {
@@ -1173,7 +1185,8 @@ int ob_panel_create(ob_ctx* ctx, const ob_panel_desc* d, ob_panel** out) {
   p->ctx = ctx;
   p->p = d->p;
   p->k = d->p + 1;
-  p->k1 = d->p + 2;
+  p->n_y = std::max(1, (int)d->n_y);
+  p->k1 = d->p + 1 + p->n_y;
   p->e = p->k1 * (p->k1 + 1) / 2;
   p->ncb = (p->e + 15) / 16;
   p->e_pad = p->ncb * 16;
@@ -1202,7 +1215,7 @@ int ob_panel_create(ob_ctx* ctx, const ob_panel_desc* d, ob_panel** out) {
     p->n[g] = (uint32_t)gd[g]->n;
     p->ntiles[g] = (p->n[g] + OB_TILE_ROWS - 1) / OB_TILE_ROWS;
     p->ld[g] = (int64_t)std::max<uint32_t>(p->ntiles[g], 1) * OB_TILE_ROWS;
-    const int ncols = p->p + 1 + p->weighted;
+    const int ncols = p->p + p->n_y + p->weighted;
     const size_t bytes = sizeof(double) * (size_t)ncols * p->ld[g];
     hipError_t e = hipMalloc(&p->d_cols[g], bytes);
     if (e != hipSuccess) { bad(e, __LINE__); break; }
@@ -1215,10 +1228,11 @@ int ob_panel_create(ob_ctx* ctx, const ob_panel_desc* d, ob_panel** out) {
                         sizeof(double) * n, p->p, hipMemcpyHostToDevice);
         if (e != hipSuccess) { bad(e, __LINE__); break; }
       }
-      e = hipMemcpy(p->d_cols[g] + (size_t)p->p * p->ld[g], gd[g]->y, sizeof(double) * n, hipMemcpyHostToDevice);
+      e = hipMemcpy2D(p->d_cols[g] + (size_t)p->p * p->ld[g], sizeof(double) * p->ld[g], gd[g]->y,
+                      sizeof(double) * gd[g]->ldx, sizeof(double) * n, p->n_y, hipMemcpyHostToDevice);
       if (e != hipSuccess) { bad(e, __LINE__); break; }
       if (p->weighted) {
-        e = hipMemcpy(p->d_cols[g] + (size_t)(p->p + 1) * p->ld[g], gd[g]->w, sizeof(double) * n,
+        e = hipMemcpy(p->d_cols[g] + (size_t)(p->p + p->n_y) * p->ld[g], gd[g]->w, sizeof(double) * n,
                       hipMemcpyHostToDevice);
         if (e != hipSuccess) { bad(e, __LINE__); break; }
       }
@@ -1228,7 +1242,7 @@ int ob_panel_create(ob_ctx* ctx, const ob_panel_desc* d, ob_panel** out) {
     hipError_t e = hipMalloc(&p->d_gcols[g], sizeof(double) * (size_t)p->k1 * p->ld[g]);
     if (e == hipSuccess) {
       hipLaunchKernelGGL(ob_scale_kernel, dim3((unsigned)((p->ld[g] + kBlock - 1) / kBlock)), dim3(kBlock), 0, 0,
-                         (const double*)p->d_cols[g], p->ld[g], p->p, p->d_gcols[g]);
+                         (const double*)p->d_cols[g], p->ld[g], p->p + p->n_y, p->d_gcols[g]);
       e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -1279,6 +1293,7 @@ void ob_panel_destroy(ob_panel* p) {
 int ob_panel_row_len(const ob_panel* p) { return p ? p->row_len : 0; }
 int ob_panel_k(const ob_panel* p) { return p ? p->k : 0; }
 int ob_panel_n_base(const ob_panel* p) { return p ? p->norm.n_base : 0; }
+int ob_panel_n_y(const ob_panel* p) { return p ? p->n_y : 0; }
 
 static bool valid_ref(int m) { return m >= OB_REF_GROUP_A && m <= OB_REF_NEUMARK; }
 
@@ -1324,14 +1339,14 @@ int ob_boot_run(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     p->d_rows_tmp = nullptr;
     p->d_ok_tmp = nullptr;
     p->tmp_reps = 0;
-    HIP_OK(hipMalloc(&p->d_rows_tmp, sizeof(double) * n_reps * p->row_len));
-    HIP_OK(hipMalloc(&p->d_ok_tmp, n_reps));
+    HIP_OK(hipMalloc(&p->d_rows_tmp, sizeof(double) * n_reps * p->row_len * p->n_y));
+    HIP_OK(hipMalloc(&p->d_ok_tmp, n_reps * p->n_y));
     p->tmp_reps = n_reps;
   }
   OB_TRY(ob_boot_run_device(p, seed, first_rep, n_reps, ref_mode, p->d_rows_tmp, p->d_ok_tmp, nullptr));
   OB_TRY(ob::engine_collect(p));
-  HIP_OK(hipMemcpy(rows, p->d_rows_tmp, sizeof(double) * n_reps * p->row_len, hipMemcpyDeviceToHost));
-  HIP_OK(hipMemcpy(ok, p->d_ok_tmp, n_reps, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(rows, p->d_rows_tmp, sizeof(double) * n_reps * p->row_len * p->n_y, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(ok, p->d_ok_tmp, n_reps * p->n_y, hipMemcpyDeviceToHost));
   return OB_OK;
 }
 

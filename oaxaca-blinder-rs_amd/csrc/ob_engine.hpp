@@ -24,7 +24,8 @@ struct ob_panel {
   ob_ctx* ctx = nullptr;
   int p = 0;        // predictor columns
   int k = 0;        // p + 1 (intercept)
-  int k1 = 0;       // p + 2: v = [1, x, y]
+  int n_y = 1;     // outcome columns (RIF multi-tau: one per quantile)
+  int k1 = 0;       // p + 1 + n_y: v = [1, x, y_1..y_n_y]
   int e = 0;        // extended-Gram pairs
   int e_pad = 0;    // multiple of 16
   int ncb = 0;      // 16-wide column blocks
@@ -33,7 +34,7 @@ struct ob_panel {
   uint32_t n[2] = {0, 0};
   int64_t ld[2] = {0, 0};      // padded rows (multiple of OB_TILE_ROWS)
   uint32_t ntiles[2] = {0, 0};
-  double* d_cols[2] = {nullptr, nullptr};   // [col][ld]: x_1..x_p, y, (w)
+  double* d_cols[2] = {nullptr, nullptr};   // [col][ld]: x_1..x_p, y_1..y_n_y, (w)
   double* d_gcols[2] = {nullptr, nullptr};  // weighted: [k1][ld] = sqrt(w) * [1, x, y]
   ob_norm_cfg norm;
   int32_t* d_norm = nullptr;               // packed norm lists

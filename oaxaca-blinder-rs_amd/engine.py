@@ -36,7 +36,9 @@ class Panel:
 
     ``xa``/``xb``: (n_g, p) arrays; ``n_num`` numeric predictors precede dummy columns (the
     pooled group indicator is inserted after them); ``norm`` optionally carries the
-    normalization lists (dict with start, idx, m, pstart, pidx, has_base).
+    normalization lists (dict with start, idx, m, pstart, pidx, has_base). ``ya``/``yb`` may be
+    (n_g, n_y) blocks of several outcomes (RIF multi-tau): every replicate then yields n_y rows
+    from one Gram pass, and ``point_estimate``/``boot`` return an outcome axis first.
     """
 
     def __init__(self, xa, ya, xb, yb, wa=None, wb=None, n_num=None, norm=None, device=None):
@@ -47,8 +49,13 @@ class Panel:
         self.p = xa.shape[1]
         self._xa = np.asfortranarray(xa)
         self._xb = np.asfortranarray(xb)
-        self._ya = np.ascontiguousarray(ya, dtype=np.float64)
-        self._yb = np.ascontiguousarray(yb, dtype=np.float64)
+        ya = np.asarray(ya, dtype=np.float64)
+        yb = np.asarray(yb, dtype=np.float64)
+        self.n_y = 1 if ya.ndim == 1 else ya.shape[1]
+        if (yb.ndim == 1 and self.n_y != 1) or (yb.ndim == 2 and yb.shape[1] != self.n_y):
+            raise ValueError("ya/yb must carry the same number of outcomes")
+        self._ya = np.asfortranarray(ya.reshape(ya.shape[0], self.n_y))  # ld = n_g, as x
+        self._yb = np.asfortranarray(yb.reshape(yb.shape[0], self.n_y))
         if len(self._ya) != xa.shape[0] or len(self._yb) != xb.shape[0]:
             raise ValueError("y length mismatch")
         weighted = wa is not None
@@ -60,6 +67,7 @@ class Panel:
         d.p = self.p
         d.n_num = self.p if n_num is None else int(n_num)
         d.weighted = 1 if weighted else 0
+        d.n_y = self.n_y
         d.a = N.ob_group_desc(xa.shape[0], _dp(self._xa), max(xa.shape[0], 1), _dp(self._ya), _dp(self._wa))
         d.b = N.ob_group_desc(xb.shape[0], _dp(self._xb), max(xb.shape[0], 1), _dp(self._yb), _dp(self._wb))
         self._norm_keep = []
@@ -78,18 +86,21 @@ class Panel:
         self.n_a, self.n_b = xa.shape[0], xb.shape[0]
 
     def point_estimate(self, ref=ReferenceCoefficients.GroupA, residuals=False):
-        row = np.empty(self.row_len)
-        res = np.empty(self.n_b) if residuals else None
+        row = np.empty((self.n_y, self.row_len))
+        res = np.empty((self.n_y, self.n_b)) if residuals else None
         N.check(N.lib().ob_point_estimate(self._h, int(ref), _dp(row), _dp(res)))
+        if self.n_y == 1:
+            row = row[0]
+            res = None if res is None else res[0]
         return (row, res) if residuals else row
 
     def boot(self, seed: int, first_rep: int, n_reps: int, ref=ReferenceCoefficients.GroupA):
-        rows = np.empty((n_reps, self.row_len))
-        ok = np.zeros(n_reps, dtype=np.uint8)
+        rows = np.empty((self.n_y, n_reps, self.row_len))
+        ok = np.zeros((self.n_y, n_reps), dtype=np.uint8)
         if n_reps:
             N.check(N.lib().ob_boot_run(self._h, seed & ((1 << 64) - 1), first_rep, n_reps, int(ref), _dp(rows),
                                         ok.ctypes.data_as(C.POINTER(C.c_uint8))))
-        return rows, ok
+        return (rows[0], ok[0]) if self.n_y == 1 else (rows, ok)
 
     def boot_device(self, seed: int, first_rep: int, n_reps: int, rows_ptr: int, ok_ptr: int,
                     ref=ReferenceCoefficients.GroupA, stream: int | None = None):

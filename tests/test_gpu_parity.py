@@ -217,6 +217,49 @@ def test_decompose_quantile_matches_oracle(ob, O):
         compare_results(b.decompose_quantile(q), o.decompose_quantile(q))
 
 
+@pytest.mark.parametrize("weighted,ref", [(False, 1), (True, 2), (True, 0)])
+def test_decompose_quantiles_multi_tau(ob, O, weighted, ref):
+    """one run serves several quantiles; each equals the single-quantile
+    run bitwise (same OBRS-1 stream, same per-pair MFMA columns) and the oracle within tolerance."""
+    f = synthetic_frame(4000, seed=21, weighted=weighted)
+    taus = (0.1, 0.5, 0.9)
+
+    def builder():
+        b = (ob.OaxacaBuilder(f, "wage", "gender", "F").predictors(["education", "experience"])
+             .categorical_predictors(["sector"]).bootstrap_reps(150).reference_coefficients(ref).seed(SEED))
+        return b.weights("w") if weighted else b
+
+    multi = builder().decompose_quantiles(taus)
+    assert len(multi) == len(taus)
+    for t, q in enumerate(taus):
+        single = builder().decompose_quantile(q)
+        assert multi[t].total_gap == single.total_gap
+        for tab in ("two_fold", "three_fold"):
+            for cm, cs in zip(getattr(multi[t], tab).aggregate, getattr(single, tab).aggregate):
+                assert (cm.name, cm.estimate, cm.std_err, cm.ci_lower, cm.ci_upper) == \
+                       (cs.name, cs.estimate, cs.std_err, cs.ci_lower, cs.ci_upper)
+        o = (O.OracleBuilder(f, "wage", "gender", "F")
+             .set(["education", "experience"], ["sector"], [], 150, ref, "w" if weighted else None, SEED))
+        compare_results(multi[t], o.decompose_quantile(q))
+
+
+def test_multi_outcome_panel_rows_bitwise(ob, O):
+    """Panel with an (n, 3) outcome block: each outcome's rows equal a one-outcome panel's."""
+    d = O.synthetic_panel(6000, 6, True, seed=5)
+    rng = np.random.default_rng(3)
+    ya = np.column_stack([d["ya"], d["ya"] ** 2 / 10, rng.normal(size=d["ya"].size)])
+    yb = np.column_stack([d["yb"], d["yb"] ** 2 / 10, rng.normal(size=d["yb"].size)])
+    multi = ob.Panel(d["xa"], ya, d["xb"], yb, d["wa"], d["wb"])
+    assert multi.n_y == 3
+    rows, ok = multi.boot(SEED, 40, 300, 2)
+    pe = multi.point_estimate(2)
+    for t in range(3):
+        one = ob.Panel(d["xa"], ya[:, t], d["xb"], yb[:, t], d["wa"], d["wb"])
+        r1, ok1 = one.boot(SEED, 40, 300, 2)
+        assert np.array_equal(rows[t], r1, equal_nan=True) and np.array_equal(ok[t], ok1)
+        assert np.array_equal(pe[t], one.point_estimate(2))
+
+
 @pytest.mark.parametrize("mode", ["GroupB", "GroupA", "Pooled", "Weighted"])
 def test_reference_integration_runs(ob, mode):  # tests/integration_test.rs:105-144
     k = KAT["integration_frame"]
