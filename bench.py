@@ -99,7 +99,11 @@ def main():
     ap.add_argument("--unweighted", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="0 disables the CPU baseline leg")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--taus", type=str, default="",
+                    help="configs[3]: comma-separated RIF quantiles sharing one bootstrap (e.g. 0.1,0.5,0.9); "
+                         "reports replicate-quantiles/s instead of the headline metric")
     args = ap.parse_args()
+    taus = [float(t) for t in args.taus.split(",") if t.strip()]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -117,13 +121,17 @@ def main():
     ob = importlib.import_module("oaxaca-blinder-rs_amd")
     weighted = not args.unweighted
     d = synthetic(args.rows, args.preds, weighted)
-    panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"], d["wa"], d["wb"], device=local)
-    B, rl = args.reps, panel.row_len
+    ya, yb = d["ya"], d["yb"]
+    if taus:  # builder.rs:711-757: each group's outcome replaced by its RIF, one column per tau
+        ya = np.column_stack([ob.rif(d["ya"], t) for t in taus])
+        yb = np.column_stack([ob.rif(d["yb"], t) for t in taus])
+    panel = ob.Panel(d["xa"], ya, d["xb"], yb, d["wa"], d["wb"], device=local)
+    B, rl, ny = args.reps, panel.row_len, panel.n_y
     dev = torch.device("cuda", local)
-    rows = torch.empty((B, rl), dtype=torch.float64, device=dev)
-    ok = torch.empty(B, dtype=torch.uint8, device=dev)
-    all_rows = torch.empty((world * B, rl), dtype=torch.float64, device=dev) if world > 1 else rows
-    all_ok = torch.empty(world * B, dtype=torch.uint8, device=dev) if world > 1 else ok
+    rows = torch.empty((ny * B, rl), dtype=torch.float64, device=dev)
+    ok = torch.empty(ny * B, dtype=torch.uint8, device=dev)
+    all_rows = torch.empty((world * ny * B, rl), dtype=torch.float64, device=dev) if world > 1 else rows
+    all_ok = torch.empty(world * ny * B, dtype=torch.uint8, device=dev) if world > 1 else ok
     kd = panel.k + panel.n_base
     stat_cols = np.arange(6 + 2 * kd, dtype=np.int32)  # every reported component (+ total_gap)
     seed = 0x0B5EED
@@ -135,10 +143,11 @@ def main():
         if world > 1:
             dist.all_gather_into_tensor(all_rows, rows)
             dist.all_gather_into_tensor(all_ok, ok)
-        if rank == 0:
-            h_rows = all_rows.cpu().numpy()
-            h_ok = all_ok.cpu().numpy()
-            stats = ob.aggregate(h_rows, h_ok, stat_cols)
+        if rank == 0:  # per outcome: that outcome's block of every rank, in replicate order
+            h_rows = all_rows.cpu().numpy().reshape(world, ny, B, rl)
+            h_ok = all_ok.cpu().numpy().reshape(world, ny, B)
+            stats = [ob.aggregate(np.ascontiguousarray(h_rows[:, t].reshape(-1, rl)),
+                                  np.ascontiguousarray(h_ok[:, t].reshape(-1)), stat_cols) for t in range(ny)][0]
         else:
             torch.cuda.current_stream(dev).synchronize()
             stats = None
@@ -171,15 +180,16 @@ def main():
         total_reps = world * B * args.steps
         value = total_reps / elapsed
         k = args.preds + 1
-        flops_rep = 2.0 * args.rows * (k * (k + 1) / 2 + k)
+        flops_rep = 2.0 * args.rows * (k * (k + 1) / 2 + ny * k)  # SURVEY.md §8d (X^T W X + one X^T W y per outcome)
         bytes_rep = args.rows * (args.preds + (2 if weighted else 1)) * 8.0
         reps_per_launch = B / max(launches / args.steps, 1)
         achieved = flops_rep * reps_per_launch / (gram_launch_ms * 1e-3) / 1e12
-        traffic = load_traffic(args.rows, args.preds, B)
+        traffic = load_traffic(args.rows, args.preds, B) if not taus else None
         out = {
-            "metric": "bootstrap replicates/sec on 1M-row×20-pred panel at 1/2/4/8 MI355X",
-            "value": value,
-            "unit": "replicates/s",
+            "metric": "bootstrap replicates/sec on 1M-row×20-pred panel at 1/2/4/8 MI355X" if not taus else
+                      "RIF bootstrap replicate-quantiles/sec (configs[3], quantiles share each resample)",
+            "value": value * ny,
+            "unit": "replicates/s" if not taus else "replicate-quantiles/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -189,7 +199,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (SURVEY.md §8d wage panel, numpy seed 20260424; OBRS-1 bootstrap seed 0x0B5EED)",
-            "config": {"workload": "configs[1]: two-fold WLS bootstrap, GroupA reference coefficients",
+            "config": {"workload": "configs[1]: two-fold WLS bootstrap, GroupA reference coefficients" if not taus
+                       else f"configs[3]: RIF decomposition at tau={taus}, two-fold WLS, GroupA",
                        "rows": args.rows, "predictors": args.preds, "weighted": weighted,
                        "replicates_per_gpu_per_step": B, "parallelism": f"replicates sharded x{world}, RCCL all-gather"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": F64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
@@ -200,12 +211,12 @@ def main():
                                   "GBps": bytes_rep * value / world / 1e9,
                                   "frac_of_hbm_peak": bytes_rep * value / world / 1e9 / HBM_PEAK_GBPS},
         }
-        if world == 1 and args.cpu_seconds > 0:
+        if world == 1 and args.cpu_seconds > 0 and not taus:
             out["cpu_baseline"] = cpu_baseline(d, args.preds, weighted, args.ref, args.cpu_seconds, args.cpu_threads)
         else:
             out["cpu_baseline"] = None
         out["check"] = {"explained_se": float(stats[0][0]), "unexplained_se": float(stats[1][0]),
-                        "ok_replicates": int(all_ok.sum().item())}
+                        "ok_replicates": int(all_ok.sum().item()), "quantiles": taus or None}
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
