@@ -132,12 +132,13 @@ int ob_boot_run_device(ob_panel* panel, uint64_t seed, uint64_t first_rep, uint6
 /* HIP-event timings of the last boot run (ms summed over its launches; 0 if not run). */
 typedef struct {
   double level1_ms; /* level-1 tile counts */
-  double gram_ms;   /* resample + X^T diag(c w) X MFMA kernel (the dominant kernel) */
+  double gram_ms;   /* X^T diag(c w) X MFMA kernel over the count images (the dominant kernel) */
   double reduce_ms;
   double solve_ms;  /* Cholesky solves + OB algebra */
   int32_t gram_launches;
   int32_t chunks;
   int32_t blocks;
+  double counts_ms; /* level-2 count images (ob_count_kernel) */
 } ob_timing;
 int ob_panel_last_timing(const ob_panel* panel, ob_timing* out);
 /* Synchronize the stream used by the last *_device call and collect its timings. */

@@ -63,7 +63,7 @@ class ob_panel_desc(C.Structure):
 class ob_timing(C.Structure):
     _fields_ = [("level1_ms", C.c_double), ("gram_ms", C.c_double), ("reduce_ms", C.c_double),
                 ("solve_ms", C.c_double), ("gram_launches", C.c_int32), ("chunks", C.c_int32),
-                ("blocks", C.c_int32)]
+                ("blocks", C.c_int32), ("counts_ms", C.c_double)]
 
 
 class ob_column(C.Structure):

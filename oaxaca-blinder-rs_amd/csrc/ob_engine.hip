@@ -34,8 +34,9 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kCntStride = OB_TILE_ROWS / 4 + 1;  // u32 words per replicate row of the u8 count image (+1 pad)
-constexpr int kCntBytes = 64 * kCntStride * 4;
 constexpr uint64_t kSegReps = 16384;
+constexpr uint64_t kCountBudget = 24ull << 30;  // bytes of level-2 count images per segment
+constexpr size_t kSegEvents = 6;
 constexpr int kColStride = 65;  // doubles per staged column (64 rows + 1: odd stride)
 
 #define HIP_OK(expr)                                                                     \
@@ -63,8 +64,9 @@ struct GramArgs {
   double* partial;  // [chunk][rep_pad][e_pad]
   int e_pad;
   uint32_t* flags;
-  int diag;  // ablation bits (OB_GRAM_DIAG, tools/gram_ablate.py): 1 no level-2 draws, 2 no MFMAs,
-            // 4 no sub-tile DMA
+  const uint32_t* counts;  // level-2 count images [tile (A then B)][batch][sub-tile][kCimgWords]
+  uint32_t tiles_total;
+  int diag;  // ablation bits (OB_GRAM_DIAG, tools/gram_ablate.py): 2 no MFMAs, 4 no sub-tile DMA
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -317,55 +319,90 @@ __device__ __forceinline__ void store_partials(const GramArgs& a, const Work& w,
 }
 
 // ---------------------------------------------------------------------------------------------
-// Gram: 4 waves (one per SIMD) per block, two blocks per CU, CB column blocks per wave; the
-// two blocks on a CU drift apart, so one block's barrier never drains a SIMD's MFMA pipe. One
-// 64-row sub-tile per step and one LDS barrier per step; A fragments are the count bytes of the
-// current tile (ds_read_b32 + convert), prefetched one k-step ahead. Per tile t the side work
-// rides between k-groups of its steps:
-//   step 0      recycle tile t-1's count image (exact overflow check + zeroing, all threads),
-//               publish tile t+1's level-1 counts (loaded at tile t-1's first step), load t+2's
-//   steps 1..ns-2  the level-2 draws of tile t+1 into the recycled image, in slices
-//   every step  LDS-DMA of the next sub-tile, first thing, so it has the whole step to land
+// Level-2 counts: one block per (64-replicate batch, run of tiles). Per tile: the batch's level-1
+// counts and call prefix, the level-2 draws into an LDS u8 image, the exact overflow check, then
+// the image written to HBM in the Gram kernel's sub-tile layout: per 64-row sub-tile, replicate
+// r's 16 count words at r * 17 (+1 pad word: odd stride, conflict-free A-fragment reads), so the
+// Gram kernel fetches a sub-tile with a plain LDS-DMA copy. Counts are drawn once per replicate
+// batch, whatever the number of column groups.
 // ---------------------------------------------------------------------------------------------
-constexpr int kAux = 3 * 129 * 4 + 4;  // mcnt[3][64] + cum[3][65], 16-byte aligned end
-constexpr int kXtOff = 2 * kCntBytes + kAux;
+constexpr int kCimgStride = 17;               // u32 words per replicate row of a sub-tile image
+constexpr int kCimgWords = 64 * kCimgStride;  // one sub-tile: 64 replicates x 64 rows (u8)
+constexpr int kCntTilesPerBlock = 8;
+
+__global__ __launch_bounds__(kBlock) void ob_count_kernel(const GramArgs a) {
+  __shared__ uint32_t img[64 * kCntStride];
+  __shared__ uint32_t mc[64], cum[65];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  Work w{};
+  w.rb = blockIdx.y;
+  w.rep0 = w.rb * 64;
+  const uint32_t tt0 = blockIdx.x * kCntTilesPerBlock;
+  const uint32_t tt1 = min(a.tiles_total, tt0 + kCntTilesPerBlock);
+  for (uint32_t tt = tt0; tt < tt1; ++tt) {
+    w.g = tt >= a.tiles0 ? 1u : 0u;
+    w.n = w.g ? a.n1 : a.n0;
+    const uint32_t tile = tt - (w.g ? a.tiles0 : 0u);
+    for (int i = tid; i < 64 * kCntStride; i += kBlock) img[i] = 0u;
+    if (wave == 0) tile_counts(a, w, tile, mc, cum, lane);
+    __syncthreads();
+    level2_draws(a, w, tile, img, mc, cum, 0, 1, wave, 4, lane);
+    __syncthreads();
+    check_counts(a, img, mc, tid);
+    const uint32_t ns = (min(OB_TILE_ROWS, w.n - tile * OB_TILE_ROWS) + 63) >> 6;
+    uint32_t* out = const_cast<uint32_t*>(a.counts) + ((size_t)tt * a.nb_rep + w.rb) * 4 * kCimgWords;
+    for (uint32_t i = tid; i < ns * kCimgWords; i += kBlock) {
+      const uint32_t s = i / kCimgWords, rem = i - s * kCimgWords, r = rem / kCimgStride, wd = rem - r * kCimgStride;
+      out[i] = wd < 16 ? img[r * kCntStride + s * 16 + wd] : 0u;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Gram: 4 waves (one per SIMD) per block, two blocks per CU, CB column blocks per wave; the two
+// blocks on a CU drift apart, so one block's barrier never drains a SIMD's MFMA pipe. One 64-row
+// sub-tile per step, one LDS barrier per step. The next sub-tile's staged rows and its count
+// image arrive by LDS-DMA issued at the start of the step; A fragments are count bytes
+// (ds_read_b32 + convert) and B fragments pair products of staged values, both read one k-step
+// ahead of their MFMAs (register double buffer). No draws here: ob_count_kernel made the counts.
+// ---------------------------------------------------------------------------------------------
+constexpr int kXtOff = 2 * kCimgWords * 4;
 static_assert(kXtOff % 16 == 0, "staged sub-tiles must stay 16-byte aligned");
 
 template <int CB, bool UNIT>
 __global__ __launch_bounds__(kBlock, 2) void ob_gram_kernel(const GramArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint32_t* cntb = reinterpret_cast<uint32_t*>(smem);                    // [2][64][kCntStride]
-  uint32_t* mcntb = reinterpret_cast<uint32_t*>(smem + 2 * kCntBytes);   // [3][64]
-  uint32_t* cumb = mcntb + 3 * 64;                                        // [3][65]
-  double* xt = reinterpret_cast<double*>(smem + kXtOff);               // [2][k1][kColStride]
+  uint32_t* cimg = reinterpret_cast<uint32_t*>(smem);      // [2][kCimgWords]
+  double* xt = reinterpret_cast<double*>(smem + kXtOff);  // [2][k1][kColStride]
   __attribute__((address_space(3))) unsigned char* lds3 = (__attribute__((address_space(3))) unsigned char*)smem;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const Work w = map_work(a);
   const int cb0 = ((int)w.cg * 4 + wave) * CB;
   const bool mma = cb0 < a.ncb && !(a.diag & 2);
-  const bool draws = !UNIT && !(a.diag & 1);
   const bool dma = !(a.diag & 4);
   const int buf_dbl = a.k1 * kColStride;
-  auto cnt_img = [&](uint32_t t) { return cntb + (t & 1) * 64 * kCntStride; };
-  auto mc_of = [&](uint32_t t) { return mcntb + (t % 3) * 64; };
-  auto cum_of = [&](uint32_t t) { return cumb + (t % 3) * 65; };
+  const uint32_t tg0 = w.g ? a.tiles0 : 0u;
   auto tile_rows = [&](uint32_t t) { return min(OB_TILE_ROWS, w.n - t * OB_TILE_ROWS); };
+  // LDS-DMA of one sub-tile's count image (17 dword-wave-instructions, round-robin over waves)
+  auto stage_counts = [&](int buf, uint32_t tile, uint32_t s) {
+    if (UNIT) return;
+    const uint32_t* src = a.counts + (((size_t)(tg0 + tile) * a.nb_rep + w.rb) * 4 + s) * kCimgWords;
+    for (int t = wave; t < kCimgStride; t += 4)
+      __builtin_amdgcn_global_load_lds(src + t * 64 + lane,
+                                       (__attribute__((address_space(3))) void*)(lds3 + (buf * kCimgWords + t * 64) * 4),
+                                       4, 0, 0);
+  };
 
   if (w.t0 < w.t1) {
-    if (draws) {
-      for (int i = tid; i < 2 * 64 * kCntStride; i += kBlock) cntb[i] = 0u;
-      if (wave == 0) tile_counts(a, w, w.t0, mc_of(w.t0), cum_of(w.t0), lane);
-      if (wave == 1 && w.t0 + 1 < w.t1) tile_counts(a, w, w.t0 + 1, mc_of(w.t0 + 1), cum_of(w.t0 + 1), lane);
-    }
     if (a.c_first == 1)
       for (int i = tid; i < 64; i += kBlock) {
         xt[i] = 1.0;
         xt[buf_dbl + i] = 1.0;
       }
     stage_dma(a, w, kXtOff, (size_t)w.t0 * OB_TILE_ROWS, wave, 0, 4, lane, lds3);
-    __syncthreads();
-    if (draws) level2_draws(a, w, w.t0, cnt_img(w.t0), mc_of(w.t0), cum_of(w.t0), 0, 1, wave, 4, lane);
+    stage_counts(0, w.t0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -385,42 +422,14 @@ __global__ __launch_bounds__(kBlock, 2) void ob_gram_kernel(const GramArgs a) {
   auto read_k = [&](const uint32_t* cw, const double* xb, int ks, uint32_t (&w4)[4], double (&va)[CB],
                     double (&vb)[CB]) {
 #pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4) w4[q4] = UNIT ? 0u : cw[q4 * 16 * kCntStride + ks];
+    for (int q4 = 0; q4 < 4; ++q4) w4[q4] = UNIT ? 0u : cw[q4 * 16 * kCimgStride + ks];
 #pragma unroll
     for (int c = 0; c < CB; ++c) {
       va[c] = xb[offa[c] + ks];
       vb[c] = xb[offb[c] + ks];
     }
   };
-  auto mma4 = [&](const uint32_t* cw, const double* xb, int g) {
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) {
-      const int ks = g * 4 + kk;
-      uint32_t an[4];
-      double na[CB], nb[CB];
-      if (ks < 15) read_k(cw, xb, ks + 1, an, na, nb);
-      __builtin_amdgcn_sched_barrier(0);
-      double af[4];
-#pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4)
-        af[q4] = UNIT ? ((gbase + ks * 4 + (lane >> 4) < w.n) ? 1.0 : 0.0) : (double)((aw[q4] >> sh) & 0xFFu);
-#pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4)
-#pragma unroll
-        for (int c = 0; c < CB; ++c)
-          acc[q4][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[q4], bf[c], acc[q4][c], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (ks < 15) {
-#pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4) aw[q4] = an[q4];
-#pragma unroll
-        for (int c = 0; c < CB; ++c) bf[c] = na[c] * nb[c];
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
 
-  uint32_t m_next = 0;  // wave 0: level-1 count of a later tile for replicate `lane`
   int j = 0;
   for (uint32_t tile = w.t0; tile < w.t1; ++tile) {
     const uint32_t ns = (tile_rows(tile) + 63) >> 6;
@@ -428,38 +437,51 @@ __global__ __launch_bounds__(kBlock, 2) void ob_gram_kernel(const GramArgs a) {
       const int cur = j & 1;
       const bool last_sub = s + 1 == ns;
       const bool has_next = !last_sub || tile + 1 < w.t1;
-      const size_t ngbase = last_sub ? (size_t)(tile + 1) * OB_TILE_ROWS : (size_t)tile * OB_TILE_ROWS + (s + 1) * 64;
+      const uint32_t ntile = last_sub ? tile + 1 : tile, nsub = last_sub ? 0u : s + 1;
       gbase = (size_t)tile * OB_TILE_ROWS + s * 64;
-      const uint32_t* cw = cnt_img(tile) + (lane & 15) * kCntStride + s * 16;
-      const double* xb = xt + cur * buf_dbl;
-      if (has_next && dma) stage_dma(a, w, kXtOff + (cur ^ 1) * buf_dbl * 8, ngbase, wave, 0, 4, lane, lds3);
-      if (mma) {
-        double va[CB], vb[CB];
-        read_k(cw, xb, 0, aw, va, vb);
-#pragma unroll
-        for (int c = 0; c < CB; ++c) bf[c] = va[c] * vb[c];
+      if (has_next && dma) {
+        stage_dma(a, w, kXtOff + (cur ^ 1) * buf_dbl * 8, (size_t)ntile * OB_TILE_ROWS + nsub * 64, wave, 0, 4, lane,
+                  lds3);
+        stage_counts(cur ^ 1, ntile, nsub);
       }
+      const uint32_t* cw = cimg + cur * kCimgWords + (lane & 15) * kCimgStride;
+      const double* xb = xt + cur * buf_dbl;
+      if (mma) {
+        {
+          double va[CB], vb[CB];
+          read_k(cw, xb, 0, aw, va, vb);
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        if (mma) mma4(cw, xb, g);
-        if (g == 0 && draws) {
-          if (s == 0) {
-            if (tile > w.t0) check_counts(a, cnt_img(tile - 1), mc_of(tile - 1), tid, true);
-          } else if (s + 1 < ns && tile + 1 < w.t1) {
-            level2_draws(a, w, tile + 1, cnt_img(tile + 1), mc_of(tile + 1), cum_of(tile + 1), (int)s - 1,
-                         (int)ns - 2, wave, 4, lane);
-          }
+          for (int c = 0; c < CB; ++c) bf[c] = va[c] * vb[c];
         }
-        if (g == 1 && draws && s == 0 && wave == 0) {
-          if (tile > w.t0 && tile + 1 < w.t1) publish_counts(w, tile + 1, m_next, mc_of(tile + 1), cum_of(tile + 1), lane);
-          if (tile + 2 < w.t1) m_next = level1_count(a, w, tile + 2, lane);
+#pragma unroll
+        for (int ks = 0; ks < 16; ++ks) {
+          uint32_t an[4];
+          double na[CB], nb[CB];
+          if (ks < 15) read_k(cw, xb, ks + 1, an, na, nb);
+          __builtin_amdgcn_sched_barrier(0);
+          double af[4];
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4)
+            af[q4] = UNIT ? ((gbase + ks * 4 + (lane >> 4) < w.n) ? 1.0 : 0.0) : (double)((aw[q4] >> sh) & 0xFFu);
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4)
+#pragma unroll
+            for (int c = 0; c < CB; ++c)
+              acc[q4][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[q4], bf[c], acc[q4][c], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          if (ks < 15) {
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) aw[q4] = an[q4];
+#pragma unroll
+            for (int c = 0; c < CB; ++c) bf[c] = na[c] * nb[c];
+          }
+          __builtin_amdgcn_sched_barrier(0);
         }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next sub-tile has landed
       lds_barrier();
     }
   }
-  if (draws && w.t0 < w.t1) check_counts(a, cnt_img(w.t1 - 1), mc_of(w.t1 - 1), tid);
   if (mma) store_partials<CB>(a, w, cb0, lane, acc);
 }
 
@@ -1002,14 +1024,18 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   if (first_rep + n_reps > 0x100000000ull)
     return ob::fail(OB_E_INVALID, "replicate ids must stay below 2^32 (OBRS-1 counter word)");
   hipStream_t s = stream ? stream : ctx->stream;
-  const uint64_t seg = std::min<uint64_t>(n_reps, kSegReps);
+  const uint32_t tiles = p->ntiles[0] + p->ntiles[1];
+  // segment: at most kSegReps replicates, and a count-image buffer within kCountBudget
+  const uint64_t batch_bytes = (uint64_t)std::max(tiles, 1u) * 4 * kCimgWords * sizeof(uint32_t);
+  const uint64_t seg_cap = std::max<uint64_t>(64, (kCountBudget / batch_bytes) * 64);
+  const uint64_t seg = std::min<uint64_t>(n_reps, std::min<uint64_t>(kSegReps, seg_cap));
   Plan pl = make_plan(p, seg, false);
   const uint64_t tail = n_reps % seg;
   Plan pl_tail = tail ? make_plan(p, tail, false) : pl;  // same chunks, fewer replicate batches
   const int nch = pl.n_chunks();
-  const uint32_t tiles = p->ntiles[0] + p->ntiles[1];
   const size_t need_partial = std::max((size_t)nch * pl.rep_pad, (size_t)pl_tail.n_chunks() * pl_tail.rep_pad);
   OB_TRY(ensure_buf(&p->d_m1, p->cap_m1, (size_t)tiles * pl.rep_pad));
+  OB_TRY(ensure_buf(&p->d_counts, p->cap_counts, (size_t)tiles * pl.nb_rep * 4 * kCimgWords));
   OB_TRY(ensure_buf(&p->d_partial, p->cap_partial, need_partial * p->e_pad));
   OB_TRY(ensure_buf(&p->d_gram, p->cap_gram, (size_t)2 * pl.rep_pad * p->e_pad));
   OB_TRY(ensure_buf(&p->d_chunks, p->cap_chunks, std::max(pl.chunks.size(), pl_tail.chunks.size())));
@@ -1027,7 +1053,7 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   p->pending_segments = 0;
   const uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
   const size_t nseg = (size_t)((n_reps + seg - 1) / seg);
-  while (p->seg_events.size() < 5 * nseg) {
+  while (p->seg_events.size() < kSegEvents * nseg) {
     hipEvent_t e;
     HIP_OK(hipEventCreate(&e));
     p->seg_events.push_back(e);
@@ -1043,7 +1069,7 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     }
     const int nchx = plx.n_chunks();
     const uint32_t frep = (uint32_t)(first_rep + s0);
-    hipEvent_t* ev = p->seg_events.data() + 5 * (size_t)p->pending_segments;
+    hipEvent_t* ev = p->seg_events.data() + kSegEvents * (size_t)p->pending_segments;
     const bool timed = true;
     if (timed) HIP_OK(hipEventRecord(ev[0], s));
     hipLaunchKernelGGL(ob_level1_kernel, dim3(ns, 2), dim3(kBlock), lds_l1, s, p->n[0], p->n[1], p->ntiles[0], frep,
@@ -1058,16 +1084,22 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     ga.key0 = key0;
     ga.key1 = key1;
     ga.partial = p->d_partial;
+    ga.counts = p->d_counts;
+    ga.tiles_total = tiles;
     ga.diag = diag_mode();
+    hipLaunchKernelGGL(ob_count_kernel, dim3((tiles + kCntTilesPerBlock - 1) / kCntTilesPerBlock, plx.nb_rep),
+                       dim3(kBlock), 0, s, ga);
+    HIP_OK(hipGetLastError());
+    if (timed) HIP_OK(hipEventRecord(ev[2], s));
     const uint32_t blocks = plx.nb_rep * plx.n_cg * (uint32_t)nchx;
     HIP_OK(launch_gram(p, plx.cb, false, ga, blocks, s));
-    if (timed) HIP_OK(hipEventRecord(ev[2], s));
+    if (timed) HIP_OK(hipEventRecord(ev[3], s));
     const size_t nred = (size_t)ns * p->e_pad;
     hipLaunchKernelGGL(ob_reduce_kernel, dim3((unsigned)((nred + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
                        (const double*)p->d_partial, (const uint32_t*)p->d_chunks, nchx, plx.rep_pad, p->e_pad, ns,
                        p->d_gram);
     HIP_OK(hipGetLastError());
-    if (timed) HIP_OK(hipEventRecord(ev[3], s));
+    if (timed) HIP_OK(hipEventRecord(ev[4], s));
     for (int t = 0; t < p->n_y; ++t) {  // outcome-major row blocks
       SolveArgs sa = solve_args(p, ref_mode);
       sa.yc = p->p + 1 + t;
@@ -1081,7 +1113,7 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
       hipLaunchKernelGGL(ob_solve_kernel, dim3(ns), dim3(64), solve_lds_bytes(p), s, sa);
       HIP_OK(hipGetLastError());
     }
-    if (timed) HIP_OK(hipEventRecord(ev[4], s));
+    if (timed) HIP_OK(hipEventRecord(ev[5], s));
     p->timing.gram_launches += 1;
     p->pending_segments += 1;
   }
@@ -1097,10 +1129,11 @@ int engine_collect(ob_panel* p) {
   HIP_OK(hipSetDevice(p->ctx->device));
   HIP_OK(hipStreamSynchronize(p->last_stream));
   p->timing_pending = false;
-  double* dst[4] = {&p->timing.level1_ms, &p->timing.gram_ms, &p->timing.reduce_ms, &p->timing.solve_ms};
+  double* dst[kSegEvents - 1] = {&p->timing.level1_ms, &p->timing.counts_ms, &p->timing.gram_ms,
+                                 &p->timing.reduce_ms, &p->timing.solve_ms};
   for (int sg = 0; sg < p->pending_segments; ++sg) {
-    hipEvent_t* ev = p->seg_events.data() + 5 * (size_t)sg;
-    for (int i = 0; i < 4; ++i) {
+    hipEvent_t* ev = p->seg_events.data() + kSegEvents * (size_t)sg;
+    for (size_t i = 0; i + 1 < kSegEvents; ++i) {
       float t = 0.f;
       HIP_OK(hipEventElapsedTime(&t, ev[i], ev[i + 1]));
       *dst[i] += t;
@@ -1280,6 +1313,7 @@ void ob_panel_destroy(ob_panel* p) {
   }
   (void)hipFree(p->d_norm);
   (void)hipFree(p->d_m1);
+  (void)hipFree(p->d_counts);
   (void)hipFree(p->d_partial);
   (void)hipFree(p->d_gram);
   (void)hipFree(p->d_chunks);

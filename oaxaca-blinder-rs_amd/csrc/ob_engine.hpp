@@ -42,6 +42,7 @@ struct ob_panel {
 
   // workspace, sized for `cap_reps` replicates per segment
   uint32_t* d_m1 = nullptr;      // [tile][rep_pad]
+  uint32_t* d_counts = nullptr;  // level-2 count images [tile][batch][sub-tile][17 x 64]
   double* d_partial = nullptr;   // [chunk][rep_pad][e_pad]
   double* d_gram = nullptr;      // [rep_pad][2][e_pad]
   uint32_t* d_chunks = nullptr;  // [chunk][3] = (g, t0, t1)
@@ -50,8 +51,8 @@ struct ob_panel {
   uint8_t* d_ok_tmp = nullptr;
   uint64_t tmp_reps = 0;
 
-  size_t cap_m1 = 0, cap_partial = 0, cap_gram = 0, cap_chunks = 0;
-  std::vector<hipEvent_t> seg_events;  // 5 per segment of the last boot run
+  size_t cap_m1 = 0, cap_partial = 0, cap_gram = 0, cap_chunks = 0, cap_counts = 0;
+  std::vector<hipEvent_t> seg_events;  // 6 per segment of the last boot run
   ob_timing timing = {};
   bool timing_pending = false;
   hipStream_t last_stream = nullptr;
