@@ -802,7 +802,12 @@ Plan make_plan(const ob_panel* p, uint64_t n_reps, bool unit) {
   Plan pl;
   pl.nb_rep = (uint32_t)((n_reps + 63) / 64);
   pl.rep_pad = pl.nb_rep * 64;
-  pl.cb = (p->ncb > 8 && !unit) ? 4 : (p->ncb > 4 ? 2 : 1);  // the unit variant stays at CB <= 2
+  if (unit) {  // the unit (point-estimate) variant stays at CB <= 2
+    pl.cb = p->ncb > 4 ? 2 : 1;
+  } else {      // fewest column groups (each re-reads the rows), then the smallest CB that covers
+    const int groups = (p->ncb + 19) / 20;
+    pl.cb = std::max(1, (p->ncb + 4 * groups - 1) / (4 * groups));
+  }
   pl.n_cg = (uint32_t)((p->ncb + 4 * pl.cb - 1) / (4 * pl.cb));
   const uint32_t tT = p->ntiles[0] + p->ntiles[1];
   for (uint32_t g = 0; g < 2; ++g) {
@@ -837,6 +842,9 @@ template <bool U>
 hipError_t launch_gram_u(const ob_panel* p, int cb, const GramArgs& ga, uint32_t blocks, hipStream_t s) {
   const size_t lds = gram_lds_bytes(p);
   switch (cb) {
+    case 5:
+      if constexpr (!U) return launch_gram_t<5, U>(ga, blocks, lds, s);
+      [[fallthrough]];
     case 4:
       if constexpr (!U) return launch_gram_t<4, U>(ga, blocks, lds, s);
       [[fallthrough]];
