@@ -37,7 +37,7 @@ constexpr int kCntStride = OB_TILE_ROWS / 4 + 1;  // u32 words per replicate row
 constexpr uint64_t kSegReps = 16384;
 constexpr uint64_t kCountBudget = 24ull << 30;  // bytes of level-2 count images per segment
 constexpr size_t kSegEvents = 6;
-constexpr int kColStride = 65;  // doubles per staged column (64 rows + 1: odd stride)
+constexpr int kColStride = 96;  // doubles per staged column: 64 rows rotated by (c mod 32), wrap duplicated
 
 #define HIP_OK(expr)                                                                     \
   do {                                                                                   \
@@ -48,7 +48,7 @@ constexpr int kColStride = 65;  // doubles per staged column (64 rows + 1: odd s
   } while (0)
 
 struct GramArgs {
-  const double* gcols0;  // Gram panel of group A: column c (c_first <= c < k1) at gcols0 + (c - c_first) * ld0
+  const double* gcols0;  // Gram panel of group A (ob_panel_kernel layout: [sub-tile][c_first..k1-1][96])
   const double* gcols1;
   int64_t ld0, ld1;
   uint32_t n0, n1;
@@ -111,10 +111,14 @@ __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t
 //
 // v = [1, x_1..x_p, y] scaled by sqrt(w) when weighted (the reference's own WLS formulation,
 // ols.rs:68-78), so G[r][e] = sum_i c[r][i] v_i[a(e)] v_i[b(e)] with A = counts only.
-// Staged sub-tile image: column-major [col][kColStride] doubles; row r of the 64-row sub-tile
-// sits at position (r & 3) * 16 + (r >> 2): the 4 rows of a k-step are 16 doubles (32 banks)
-// apart, and the 16 consecutive pair columns a 16-lane group reads fall on distinct banks.
-// Column 0 is the intercept: ones (unweighted, filled once) or sqrt(w) (weighted, staged).
+// Staged sub-tile image: column-major [col][kColStride = 96] doubles. Row r of the 64-row
+// sub-tile has slot q = (r & 3) * 16 + (r >> 2) (the 4 rows of a k-step 16 slots = 32 banks
+// apart), and column c stores slot q at position q + (c mod 32), positions past 63 + (c mod 32)
+// wrapping (duplicated), so the B read of (column c, k-step ks, row group g) is at
+// c * 96 + g * 16 + (c mod 32) + ks: an immediate offset, and the 16 pair columns a 16-lane
+// group reads fall on distinct banks. The Gram panel in HBM holds exactly this image per
+// sub-tile ([sub-tile][column][96], ob_panel_kernel), so staging is one contiguous LDS-DMA copy.
+// Column 0 is the intercept: ones (unweighted, filled once in LDS) or sqrt(w) (weighted).
 // ---------------------------------------------------------------------------------------------
 struct Work {
   uint32_t rb, cg, chunk, g, t0, t1, n, rep0;
@@ -163,26 +167,25 @@ __device__ __forceinline__ void pair_offsets(const GramArgs& a, int cb0, int lan
       }
       pb = pa + rem;
     }
-    offa[c] = pa * kColStride + (lane >> 4) * 16;
-    offb[c] = pb * kColStride + (lane >> 4) * 16;
+    offa[c] = pa * kColStride + (lane >> 4) * 16 + (pa & 31);
+    offb[c] = pb * kColStride + (lane >> 4) * 16 + (pb & 31);
   }
 }
 
-// LDS-DMA (global_load_lds_dword) of one 64-row sub-tile: no staging registers. Lane i of a
-// wave-instruction writes dword i of a 256-byte half column; waves [w_lo, w_lo+nw) take the
-// 2 x (k1 - c_first) instructions round-robin.
+// LDS-DMA of one 64-row sub-tile: the Gram panel holds each sub-tile's staged image
+// contiguously ([column][96] from column c_first), so it is one copy of (k1 - c_first) x 768 B in
+// 1 KiB wave-instructions (16 B per lane), waves [w_lo, w_lo + nw) round-robin.
 __device__ __forceinline__ void stage_dma(const GramArgs& a, const Work& w, uint32_t xt_byte_off, size_t gbase,
                                           int wave, int w_lo, int nw, int lane,
                                           __attribute__((address_space(3))) unsigned char* lds3) {
   const int ncl = a.k1 - a.c_first;
-  for (int t = wave - w_lo; t < 2 * ncl; t += nw) {
-    const int cc = t >> 1, half = t & 1;
-    const int p2 = half * 32 + (lane >> 1);
-    const int row = ((p2 & 15) << 2) | (p2 >> 4);  // inverse of the row interleave
-    const char* src = reinterpret_cast<const char*>(w.X + (size_t)cc * w.ld + gbase + row) + (lane & 1) * 4;
-    const uint32_t dst = xt_byte_off + (uint32_t)((cc + a.c_first) * kColStride + half * 32) * 8u;
-    __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)(lds3 + dst), 4, 0, 0);
-  }
+  const uint32_t bytes = (uint32_t)ncl * kColStride * 8;
+  const char* src = reinterpret_cast<const char*>(w.X + (gbase >> 6) * (size_t)ncl * kColStride);
+  const uint32_t dst = xt_byte_off + (uint32_t)a.c_first * kColStride * 8;
+  for (uint32_t t = wave - w_lo; t * 1024 < bytes; t += nw)
+    if (t * 1024 + lane * 16 < bytes)
+      __builtin_amdgcn_global_load_lds(src + t * 1024 + lane * 16,
+                                       (__attribute__((address_space(3))) void*)(lds3 + dst + t * 1024), 16, 0, 0);
 }
 
 // Level-2 draws of `tile` into a u8 count image (OBRS-1, ob_spec.h: full tiles take sixteen
@@ -385,19 +388,21 @@ __global__ __launch_bounds__(kBlock, 2) void ob_gram_kernel(const GramArgs a) {
   const int buf_dbl = a.k1 * kColStride;
   const uint32_t tg0 = w.g ? a.tiles0 : 0u;
   auto tile_rows = [&](uint32_t t) { return min(OB_TILE_ROWS, w.n - t * OB_TILE_ROWS); };
-  // LDS-DMA of one sub-tile's count image (17 dword-wave-instructions, round-robin over waves)
+  // LDS-DMA of one sub-tile's count image: 16 bytes per lane, 1 KiB per wave-instruction
+  // (kCimgWords = 4.25 KiB: waves 0..3 one piece each, wave 0 the quarter piece too)
   auto stage_counts = [&](int buf, uint32_t tile, uint32_t s) {
     if (UNIT) return;
     const uint32_t* src = a.counts + (((size_t)(tg0 + tile) * a.nb_rep + w.rb) * 4 + s) * kCimgWords;
-    for (int t = wave; t < kCimgStride; t += 4)
-      __builtin_amdgcn_global_load_lds(src + t * 64 + lane,
-                                       (__attribute__((address_space(3))) void*)(lds3 + (buf * kCimgWords + t * 64) * 4),
-                                       4, 0, 0);
+    for (int t = wave; t * 256 < kCimgWords; t += 4)
+      if (t * 256 + lane * 4 < kCimgWords)
+        __builtin_amdgcn_global_load_lds(src + t * 256 + lane * 4,
+                                         (__attribute__((address_space(3))) void*)(lds3 + (buf * kCimgWords + t * 256) * 4),
+                                         16, 0, 0);
   };
 
   if (w.t0 < w.t1) {
     if (a.c_first == 1)
-      for (int i = tid; i < 64; i += kBlock) {
+      for (int i = tid; i < kColStride; i += kBlock) {
         xt[i] = 1.0;
         xt[buf_dbl + i] = 1.0;
       }
@@ -857,14 +862,28 @@ hipError_t launch_gram(const ob_panel* p, int cb, bool unit, const GramArgs& ga,
   return unit ? launch_gram_u<true>(p, cb, ga, blocks, s) : launch_gram_u<false>(p, cb, ga, blocks, s);
 }
 
-// Gram panel of a weighted design: [sqrt(w), sqrt(w) x_1..x_p, sqrt(w) y_1..] (ols.rs:68-78).
-// cols: nxy = p + n_y columns, then w.
-__global__ __launch_bounds__(kBlock) void ob_scale_kernel(const double* cols, int64_t ld, int nxy, double* gcols) {
+// Gram panel (the staged-image layout of stage_dma): [sub-tile][column c_first..k1-1][96].
+// Columns: weighted sqrt(w) * [1, x_1..x_p, y_1..] (ols.rs:68-78), else [x, y] (the intercept's
+// ones are LDS-resident). cols: [x_1..x_p, y_1..y_n_y, (w)] x ld, zero rows past n.
+__global__ __launch_bounds__(kBlock) void ob_panel_kernel(const double* cols, int64_t ld, int nxy, int weighted,
+                                                          double* gp) {
+  const int ncl = weighted ? nxy + 1 : nxy, c_first = weighted ? 0 : 1;
   const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
-  if (i >= (size_t)ld) return;
-  const double sw = sqrt(cols[(size_t)nxy * ld + i]);
-  gcols[i] = sw;
-  for (int c = 0; c < nxy; ++c) gcols[(size_t)(c + 1) * ld + i] = sw * cols[(size_t)c * ld + i];
+  const size_t per_sub = (size_t)ncl * kColStride;
+  if (i >= (size_t)(ld >> 6) * per_sub) return;
+  const size_t sub = i / per_sub;
+  const int cc = (int)((i % per_sub) / kColStride), pos = (int)(i % kColStride);
+  const int c = cc + c_first;
+  const int q = (pos - (c & 31)) & 63;
+  const size_t row = sub * 64 + (size_t)(((q & 15) << 2) | (q >> 4));
+  double v;
+  if (weighted) {
+    const double sw = sqrt(cols[(size_t)nxy * ld + row]);
+    v = c == 0 ? sw : sw * cols[(size_t)(c - 1) * ld + row];
+  } else {
+    v = cols[(size_t)(c - 1) * ld + row];
+  }
+  gp[i] = v;
 }
 
 template <typename T>
@@ -904,8 +923,8 @@ SolveArgs solve_args(const ob_panel* p, int ref_mode) {
 
 GramArgs gram_args(const ob_panel* p, const Plan& pl) {
   GramArgs ga{};
-  ga.gcols0 = p->weighted ? p->d_gcols[0] : p->d_cols[0];
-  ga.gcols1 = p->weighted ? p->d_gcols[1] : p->d_cols[1];
+  ga.gcols0 = p->d_gpanel[0];
+  ga.gcols1 = p->d_gpanel[1];
   ga.c_first = p->weighted ? 0 : 1;
   ga.ld0 = p->ld[0];
   ga.ld1 = p->ld[1];
@@ -1279,11 +1298,13 @@ int ob_panel_create(ob_ctx* ctx, const ob_panel_desc* d, ob_panel** out) {
       }
     }
   }
-  for (int g = 0; g < 2 && rc == OB_OK && p->weighted; ++g) {
-    hipError_t e = hipMalloc(&p->d_gcols[g], sizeof(double) * (size_t)p->k1 * p->ld[g]);
-    if (e == hipSuccess) {
-      hipLaunchKernelGGL(ob_scale_kernel, dim3((unsigned)((p->ld[g] + kBlock - 1) / kBlock)), dim3(kBlock), 0, 0,
-                         (const double*)p->d_cols[g], p->ld[g], p->p + p->n_y, p->d_gcols[g]);
+  for (int g = 0; g < 2 && rc == OB_OK; ++g) {
+    const int ncl = p->k1 - (p->weighted ? 0 : 1);
+    const size_t elems = (size_t)(p->ld[g] >> 6) * ncl * kColStride;
+    hipError_t e = hipMalloc(&p->d_gpanel[g], sizeof(double) * std::max<size_t>(elems, 1));
+    if (e == hipSuccess && elems) {
+      hipLaunchKernelGGL(ob_panel_kernel, dim3((unsigned)((elems + kBlock - 1) / kBlock)), dim3(kBlock), 0, 0,
+                         (const double*)p->d_cols[g], p->ld[g], p->p + p->n_y, p->weighted, p->d_gpanel[g]);
       e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -1317,7 +1338,7 @@ void ob_panel_destroy(ob_panel* p) {
   if (p->timing_pending) (void)hipStreamSynchronize(p->last_stream);
   for (int g = 0; g < 2; ++g) {
     (void)hipFree(p->d_cols[g]);
-    (void)hipFree(p->d_gcols[g]);
+    (void)hipFree(p->d_gpanel[g]);
   }
   (void)hipFree(p->d_norm);
   (void)hipFree(p->d_m1);

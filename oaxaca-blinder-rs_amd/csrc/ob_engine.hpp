@@ -35,7 +35,7 @@ struct ob_panel {
   int64_t ld[2] = {0, 0};      // padded rows (multiple of OB_TILE_ROWS)
   uint32_t ntiles[2] = {0, 0};
   double* d_cols[2] = {nullptr, nullptr};   // [col][ld]: x_1..x_p, y_1..y_n_y, (w)
-  double* d_gcols[2] = {nullptr, nullptr};  // weighted: [k1][ld] = sqrt(w) * [1, x, y]
+  double* d_gpanel[2] = {nullptr, nullptr};  // Gram panel: [ld/64][k1 - c_first][96] staged images
   ob_norm_cfg norm;
   int32_t* d_norm = nullptr;               // packed norm lists
   int row_len = 0;
