@@ -169,6 +169,15 @@ typedef struct {
   const uint8_t* valid;    /* numeric kinds: 1 = valid, 0 = null; NULL = all valid */
 } ob_column;
 
+/* ---- CSV front end (the reference CLI's LazyCsvReader, main.rs:161-165) ------------------
+ * Header row; dtypes from the first 100 rows (i64, else f64, else str); empty field = null;
+ * RFC 4180 quotes. ob_csv_column views stay valid until ob_csv_free. */
+typedef struct ob_csv ob_csv;
+int ob_csv_read(const char* path, ob_csv** out);
+int ob_csv_dims(const ob_csv* csv, int64_t* nrows, int32_t* ncols);
+int ob_csv_column(const ob_csv* csv, int32_t i, ob_column* out);
+void ob_csv_free(ob_csv* csv);
+
 typedef struct {
   const char* outcome;
   const char* group;

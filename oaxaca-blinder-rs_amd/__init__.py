@@ -9,10 +9,10 @@ from ._native import OaxacaError
 from .api import (BudgetAdjustment, ComponentResult, DecompositionDetail, OaxacaBlinder, OaxacaBuilder,
                   OaxacaResults, PreparedRun, ReferenceCoefficients, TwoFoldResults, parse_formula)
 from .engine import Panel, aggregate, bootstrap_stats, rif, row_layout
-from .frame import Frame
+from .frame import Frame, read_csv
 
 __all__ = [
     "OaxacaBuilder", "OaxacaBlinder", "OaxacaResults", "TwoFoldResults", "DecompositionDetail",
     "ComponentResult", "BudgetAdjustment", "ReferenceCoefficients", "OaxacaError", "PreparedRun",
-    "Panel", "Frame", "aggregate", "bootstrap_stats", "rif", "row_layout", "parse_formula",
+    "Panel", "Frame", "read_csv", "aggregate", "bootstrap_stats", "rif", "row_layout", "parse_formula",
 ]

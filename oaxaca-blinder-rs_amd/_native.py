@@ -31,7 +31,7 @@ EXPORTED = (
     "ob_builder_prepare", "ob_prepared_row_len", "ob_prepared_n_y", "ob_prepared_seed", "ob_prepared_panel",
     "ob_prepared_boot", "ob_prepared_boot_device", "ob_prepared_finish", "ob_prepared_destroy",
     "ob_builder_run", "ob_builder_decompose_quantile", "ob_builder_decompose_quantiles",
-    "ob_builder_data_matrices",
+    "ob_builder_data_matrices", "ob_csv_read", "ob_csv_dims", "ob_csv_column", "ob_csv_free",
     "ob_results_total_gap", "ob_results_n_a", "ob_results_n_b", "ob_results_n_failed",
     "ob_results_count", "ob_results_component", "ob_results_vector", "ob_results_free",
     "ob_matrices_dims", "ob_matrices_get", "ob_matrices_name", "ob_matrices_free",
@@ -129,6 +129,10 @@ _SIGS = {
                                                  C.POINTER(ob_builder_config), _D, C.c_int32, C.POINTER(_P)]),
     "ob_builder_data_matrices": (C.c_int, [C.POINTER(ob_column), C.c_int32, C.c_int64,
                                            C.POINTER(ob_builder_config), C.POINTER(_P)]),
+    "ob_csv_read": (C.c_int, [C.c_char_p, C.POINTER(_P)]),
+    "ob_csv_dims": (C.c_int, [_P, C.POINTER(C.c_int64), C.POINTER(C.c_int32)]),
+    "ob_csv_column": (C.c_int, [_P, C.c_int32, C.POINTER(ob_column)]),
+    "ob_csv_free": (None, [_P]),
     "ob_results_total_gap": (C.c_double, [_P]),
     "ob_results_n_a": (C.c_int64, [_P]),
     "ob_results_n_b": (C.c_int64, [_P]),

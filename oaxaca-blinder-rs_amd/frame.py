@@ -130,3 +130,31 @@ def _convert(col):
 
 def _strings(vals):
     return N.OB_COL_STR, [None if v is None else v.encode("utf-8") for v in vals], None
+
+
+def read_csv(path) -> dict:
+    """The reference CLI's CSV front end (main.rs:161-165, polars ``LazyCsvReader`` with a header)
+    through the native reader: dtypes from the first 100 rows (i64, else f64, else str), empty
+    fields are nulls (masked numeric entries / ``None`` strings). Returns a dict frame."""
+    lib = N.lib()
+    h = C.c_void_p()
+    N.check(lib.ob_csv_read(str(path).encode(), C.byref(h)))
+    try:
+        nrows, ncols = C.c_int64(), C.c_int32()
+        N.check(lib.ob_csv_dims(h, C.byref(nrows), C.byref(ncols)))
+        n = nrows.value
+        out = {}
+        for j in range(ncols.value):
+            col = N.ob_column()
+            N.check(lib.ob_csv_column(h, j, C.byref(col)))
+            valid = np.ctypeslib.as_array(col.valid, shape=(n,)).astype(bool) if n else np.zeros(0, bool)
+            if col.kind == N.OB_COL_STR:
+                vals = [col.str[i].decode() if valid[i] else None for i in range(n)]
+            else:
+                ptr = col.f64 if col.kind == N.OB_COL_F64 else col.i64
+                arr = np.ctypeslib.as_array(ptr, shape=(n,)).copy() if n else np.zeros(0)
+                vals = arr if valid.all() else np.ma.MaskedArray(arr, mask=~valid)
+            out[col.name.decode()] = vals
+        return out
+    finally:
+        lib.ob_csv_free(h)

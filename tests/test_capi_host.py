@@ -138,3 +138,66 @@ def test_row_layout(ob):
     lay = ob.row_layout(21, 2)
     assert lay["len"] == 6 + 2 * 23 + 5 * 21
     assert lay["beta_star"].stop == lay["len"]
+
+
+def _write(tmp_path, name, text):
+    p = tmp_path / name
+    p.write_text(text)
+    return str(p)
+
+
+def test_read_csv_reference_wage_file(ob, tmp_path):
+    """tests/data/wage.csv of the reference (golden transcription), read as the CLI's
+    LazyCsvReader would: floats for wage/education, strings for gender/sector."""
+    k = KAT["wage_csv"]
+    cols = ["wage", "education", "gender", "sector"]
+    lines = [",".join(cols)] + [",".join(f"{k[c][i]:.1f}" if c in ("wage", "education") else str(k[c][i])
+                                        for c in cols) for i in range(len(k["wage"]))]
+    f = ob.read_csv(_write(tmp_path, "wage.csv", "\n".join(lines) + "\n"))
+    assert list(f) == cols
+    assert f["wage"].dtype == np.float64 and np.allclose(f["wage"], k["wage"])
+    assert f["gender"] == list(k["gender"]) and f["sector"] == list(k["sector"])
+    # the frame feeds the builder's host path (get_data_matrices needs no GPU)
+    xa, ya, xb, yb, names = (ob.OaxacaBuilder(f, "wage", "gender", "F").predictors(["education"])
+                             .categorical_predictors(["sector"]).get_data_matrices())
+    assert names == ["__ob_intercept__", "education", "sector_B"]
+    assert len(ya) + len(yb) == len(k["wage"])
+
+
+def test_read_csv_inference_nulls_quotes(ob, tmp_path):
+    text = ('a,b,c,d,e\n'
+            '1,2.5,x,,"q,1"\n'
+            '2,,y,,"say ""hi"""\r\n'
+            '3,4,,,z\n')
+    f = ob.read_csv(_write(tmp_path, "t.csv", text))
+    assert f["a"].dtype == np.int64 and list(f["a"]) == [1, 2, 3]
+    assert f["b"].dtype == np.float64 and isinstance(f["b"], np.ma.MaskedArray)
+    assert list(np.ma.getmaskarray(f["b"])) == [False, True, False] and f["b"][2] == 4.0
+    assert f["c"] == ["x", "y", None]
+    assert f["d"] == [None, None, None]          # all-null inference window -> str column
+    assert f["e"] == ["q,1", 'say "hi"', "z"]
+
+
+def test_read_csv_errors(ob, N, tmp_path):
+    with pytest.raises(N.OaxacaError) as e:
+        ob.read_csv(str(tmp_path / "missing.csv"))
+    assert e.value.code == 1
+    rows = "\n".join(["v"] + [str(i) for i in range(150)] + ["1.5"]) + "\n"  # i64 inferred from 100 rows
+    with pytest.raises(N.OaxacaError) as e:
+        ob.read_csv(_write(tmp_path, "late.csv", rows))
+    assert "could not parse" in str(e.value)
+    with pytest.raises(N.OaxacaError):
+        ob.read_csv(_write(tmp_path, "ragged.csv", "a,b\n1,2\n3\n"))
+
+
+def test_read_csv_large_parallel(ob, tmp_path):
+    rng = np.random.default_rng(1)
+    n = 120_000
+    x = rng.normal(size=n)
+    g = rng.integers(0, 2, n)
+    p = tmp_path / "big.csv"
+    with open(p, "w") as fh:
+        fh.write("x,g\n")
+        fh.writelines(f"{v!r},{gg}\n" for v, gg in zip(x.tolist(), g.tolist()))
+    f = ob.read_csv(str(p))
+    assert np.array_equal(f["x"], x) and np.array_equal(f["g"], g)
