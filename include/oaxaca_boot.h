@@ -98,6 +98,19 @@ typedef struct {
      y is an n x n_y column-major block with leading dimension ldx, and every replicate yields
      n_y rows (one per outcome) from one Gram pass. */
   int32_t n_y;
+  /* Heckman two-step (builder .heckman_selection; estimation.rs:114-260, heckman.rs:38-108):
+     heckman = 1 runs a probit of s on [1, z] (math/probit.rs:25-170) and the outcome OLS on the
+     rows with s = 1 augmented by the inverse Mills ratio. z: n x n_zsel column-major with
+     leading dimension ldx (intercept implicit, n_zsel <= 7); s: the 0/1 selection outcome.
+     With heckman = 1 the group w (if weighted) only feeds the total gap and the Cotton weights
+     (the Heckman OLS is unweighted), n_norm must be 0, n_y 1, and rows carry K' = K + 1
+     coefficients (IMR last) then 1 + n_zsel selection components (OB_ROW_* with K'). */
+  int32_t heckman;
+  int32_t n_zsel;
+  const double* za;
+  const double* zb;
+  const double* sa;
+  const double* sb;
 } ob_panel_desc;
 
 typedef struct ob_panel ob_panel;

@@ -57,7 +57,9 @@ class ob_panel_desc(C.Structure):
                 ("norm_start", C.POINTER(C.c_int32)), ("norm_idx", C.POINTER(C.c_int32)),
                 ("norm_m", C.POINTER(C.c_int32)), ("pooled_start", C.POINTER(C.c_int32)),
                 ("pooled_idx", C.POINTER(C.c_int32)), ("has_base", C.POINTER(C.c_int32)),
-                ("n_y", C.c_int32)]
+                ("n_y", C.c_int32), ("heckman", C.c_int32), ("n_zsel", C.c_int32),
+                ("za", C.POINTER(C.c_double)), ("zb", C.POINTER(C.c_double)),
+                ("sa", C.POINTER(C.c_double)), ("sb", C.POINTER(C.c_double))]
 
 
 class ob_timing(C.Structure):

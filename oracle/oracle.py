@@ -223,6 +223,11 @@ class OracleBuilder:
         self.outcome, self.group, self.reference_group = outcome, group, reference_group
         self.predictors, self.categorical, self.normalize_vars = [], [], []
         self.reps, self.ref_mode, self.weights, self.seed = 20, 0, None, 0x0B5EED
+        self.selection, self.selection_predictors = None, []
+
+    def heckman(self, outcome, predictors):  # builder.rs:238-246
+        self.selection, self.selection_predictors = outcome, list(predictors)
+        return self
 
     # setters mirror builder.rs:165-246
     def set(self, predictors=(), categorical=(), normalize=(), reps=20, ref_mode=0, weights=None, seed=0x0B5EED):
@@ -232,6 +237,8 @@ class OracleBuilder:
 
     def clean_dataframe(self, frame):  # builder.rs:760-784
         cols = [self.outcome, self.group] + self.predictors + self.categorical + ([self.weights] if self.weights else [])
+        if self.selection:
+            cols += [self.selection] + self.selection_predictors
         for c in cols:
             _col(frame, c)
         n = len(next(iter(frame.values()))) if frame else 0
@@ -358,7 +365,70 @@ class OracleBuilder:
             xa_mean=point_row[tail + 2 * k: tail + 3 * k], xb_mean=point_row[tail + 3 * k: tail + 4 * k],
             beta_star=point_row[tail + 4 * k: tail + 5 * k], n_failed=int(len(ok) - ok.sum()))
 
+    def _heckman_groups(self, df, rows, dummy_names):  # estimation.rs:177-260 for one group
+        x, y, w, names = self.prepare_data(df, rows, dummy_names)
+        sel = df[self.selection]
+        if _kind(sel) != "f64":
+            raise OracleError("PolarsError", "invalid series dtype: expected `Float64`")
+        zsel = np.ones((len(rows), 1 + len(self.selection_predictors)))
+        for j, nm in enumerate(self.selection_predictors, start=1):
+            zsel[:, j] = [float(df[nm][i]) for i in rows]
+        return dict(x=x, y=y, w=w, zsel=zsel, s=np.array([float(sel[i]) for i in rows])), names
+
+    def run_heckman(self):
+        """run() with .heckman_selection(): every pass through heckman_single_pass, replicates
+        gathered by the OBRS-1 index stream."""
+        df, dummy_names, _, _ = self._stage()
+        ia, ib, _ = self.split_groups(df)
+        if not ia or not ib:
+            raise OracleError("InvalidGroupVariable", "Invalid group variable: One group has no data")
+        ga, names = self._heckman_groups(df, ia, dummy_names)
+        gb, _ = self._heckman_groups(df, ib, dummy_names)
+        weighted = self.weights is not None
+        point = heckman_single_pass(ga, gb, self.ref_mode, weighted)
+        k1, ks = len(names) + 1, ga["zsel"].shape[1]
+        rows, ok = np.full((self.reps, len(point)), np.nan), np.zeros(self.reps, dtype=np.uint8)
+        for r in range(self.reps):
+            take = []
+            for gi, g in enumerate((ga, gb)):
+                idx = resample_indices(self.seed, r, gi, len(g["y"]))
+                take.append({kk: (None if v is None else v[idx]) for kk, v in g.items()})
+            try:
+                rows[r] = heckman_single_pass(take[0], take[1], self.ref_mode, weighted)
+                ok[r] = 1
+            except OracleError:
+                pass
+        good = rows[ok.astype(bool)]
+
+        def comp(name, pt, vals):
+            se, p, (lo, hi) = bootstrap_stats(vals)
+            return dict(name=name, estimate=pt, std_err=se, t_stat=pt / se if abs(se) > 1e-9 else 0.0, p_value=p,
+                        ci_lower=lo, ci_upper=hi)
+
+        dnames = names + ["IMR"]
+        snames = ["__ob_intercept__"] + self.selection_predictors
+        base_sel = 6 + 2 * k1 + 5 * k1
+        det = lambda base: [comp(dnames[i], point[base + i], good[:, base + i] if len(good) else np.zeros(0))
+                            for i in range(k1)]
+        n_b_sel = int((gb["s"] == 1.0).sum())
+        tail = 6 + 2 * k1
+        return dict(
+            total_gap=point[5],
+            two_fold=dict(aggregate=[comp("explained", point[0], good[:, 0]),
+                                     comp("unexplained", point[1], good[:, 1])],
+                          detailed_explained=det(6), detailed_unexplained=det(6 + k1),
+                          detailed_selection=[comp(snames[i], point[base_sel + i], good[:, base_sel + i])
+                                              for i in range(ks)]),
+            three_fold=dict(aggregate=[comp(nm, point[2 + i], good[:, 2 + i])
+                                       for i, nm in enumerate(("endowments", "coefficients", "interaction"))],
+                            detailed=[]),
+            n_a=len(ga["y"]), n_b=len(gb["y"]), residuals=np.zeros(n_b_sel),
+            xa_mean=point[tail + 2 * k1: tail + 3 * k1], xb_mean=point[tail + 3 * k1: tail + 4 * k1],
+            beta_star=point[tail + 4 * k1: tail + 5 * k1], n_failed=int(len(ok) - ok.sum()), rows=rows, ok=ok)
+
     def run(self, threads=None):
+        if self.selection:
+            return self.run_heckman()
         prep = self.prepared()
         point_row, resid = self.point(prep)
         rows, ok = self.boot_rows(prep, 0, self.reps, threads=threads)
@@ -387,6 +457,128 @@ class OracleBuilder:
         finally:
             self.weights = saved
         return xa, ya, xb, yb, names
+
+
+# ---------------------------------------------------------------------------------------------
+# Heckman two-step (estimation.rs:114-260, heckman.rs:38-108, math/probit.rs:25-170) and the
+# selection terms of run_single_pass (builder.rs:477-534). statrs Normal(0, 1): cdf(z) =
+# 0.5 erfc(-z / sqrt 2), pdf(z) = exp(-z^2 / 2) / sqrt(2 pi).
+# ---------------------------------------------------------------------------------------------
+def _ncdf(z):
+    from scipy.special import erfc
+
+    return 0.5 * erfc(-np.asarray(z, dtype=float) / math.sqrt(2.0))
+
+
+def _npdf(z):
+    z = np.asarray(z, dtype=float)
+    return np.exp(-0.5 * z * z) / math.sqrt(2.0 * math.pi)
+
+
+def _chol_solve_nalgebra(m, b):
+    """nalgebra Cholesky (fails iff a pivot is 0, negative or NaN) + solve; None on failure."""
+    k = m.shape[0]
+    a = np.array(m, dtype=float, order="F")
+    for j in range(k):
+        for c in range(j):
+            a[j:, j] += -a[j, c] * a[j:, c]
+        d = a[j, j]
+        if not (d != 0.0 and d >= 0.0):
+            return None
+        a[j, j] = math.sqrt(d)
+        a[j + 1:, j] /= a[j, j]
+    x = np.array(b, dtype=float)
+    for i in range(k):
+        x[i] = x[i] / a[i, i]
+        x[i + 1:] -= x[i] * a[i + 1:, i]
+    for i in range(k - 1, -1, -1):
+        x[i] = (x[i] - a[i + 1:, i] @ x[i + 1:]) / a[i, i]
+    return x
+
+
+def probit(y, x, max_iter=100, tol=1e-6, full=False):  # math/probit.rs:25-170 (Fisher scoring from 0)
+    k = x.shape[1]
+    beta = np.zeros(k)
+    converged, it = False, 0
+    for it in range(1, max_iter + 1):
+        z = x @ beta
+        phi = _npdf(z)
+        big = np.clip(_ncdf(z), 1e-10, 1.0 - 1e-10)
+        lam = np.where(y > 0.5, phi / big, -phi / (1.0 - big))
+        w = np.sqrt(phi * phi / (big * (1.0 - big))) ** 2  # sqrt_w squared, as the reference
+        g = x.T @ lam
+        h = -(x.T * w) @ x - 1e-9 * np.eye(k)
+        step = _chol_solve_nalgebra(-h, g)
+        if step is None:  # LU fallback (probit.rs:124-137)
+            step = -np.linalg.solve(h, g)
+        beta = beta + step
+        if np.linalg.norm(step) < tol:
+            converged = True
+            break
+    return dict(coefficients=beta, converged=converged, iterations=it) if full else beta
+
+
+def heckman_two_step(y_sel, x_sel, y_out, x_out, x_sel_sub):  # heckman.rs:38-108
+    gamma = probit(y_sel, x_sel)
+    zg = x_sel_sub @ gamma
+    phi, big = _npdf(zg), _ncdf(zg)
+    imr = np.where(big < 1e-10, 0.0, phi / np.where(big < 1e-10, 1.0, big))
+    x_aug = np.column_stack([x_out, imr])
+    rc, coef, _ = ols(y_out, x_aug)
+    if rc != ORC_OK:
+        raise OracleError({1: "InsufficientData", 2: "NalgebraError"}[rc], f"heckman ols failed ({rc})")
+    delta = float(np.mean(-imr * (imr + zg)))
+    return dict(gamma=gamma, beta=coef[:-1], theta=coef[-1], imr=imr, imr_mean=float(imr.mean()), delta=delta)
+
+
+def heckman_single_pass(ga, gb, ref_mode, weighted):
+    """One Heckman decomposition pass. ga/gb: dict(x (n x K with intercept), y, w, zsel (n x Ks with
+    intercept), s). Returns the row [aggregates | detailed K+1 | detailed K+1 | beta_a, beta_b,
+    xa_mean, xb_mean, beta_star (K+1 each) | selection components (Ks)]."""
+    res, means, zmean = [], [], []
+    for g in (ga, gb):
+        sel = g["s"] == 1.0
+        if not sel.any():
+            raise OracleError("InvalidGroupVariable", "No observed outcomes in group")
+        r = heckman_two_step(g["s"], g["zsel"], g["y"][sel], g["x"][sel], g["zsel"][sel])
+        res.append(r)
+        means.append(np.append(g["x"][sel].mean(axis=0), r["imr_mean"]))
+        zmean.append(g["zsel"].mean(axis=0))
+    ba = np.append(res[0]["beta"], res[0]["theta"])
+    bb = np.append(res[1]["beta"], res[1]["theta"])
+    if ref_mode == 0:
+        bs = ba
+    elif ref_mode == 1:
+        bs = bb
+    elif ref_mode in (3, 4):
+        na = ga["w"].sum() if weighted else len(ga["y"])
+        nb = gb["w"].sum() if weighted else len(gb["y"])
+        if na + nb == 0.0:
+            raise OracleError("InvalidGroupVariable", "No data in groups for weighted coefficients.")
+        wa_ = na / (na + nb)
+        bs = ba * wa_ + bb * (1.0 - wa_)
+    else:
+        raise OracleError("Unsupported", "Heckman with pooled coefficients (the reference panics)")
+    xa, xb = means
+    dx, db = xa - xb, ba - bb
+    expl = float(dx @ bs)
+    unexpl = float((xa @ ba - xb @ bb) - expl)
+    row = [expl, unexpl, float(dx @ bb), float(xb @ db), float(dx @ db)]
+    if weighted:
+        gap = ga["y"] @ ga["w"] / ga["w"].sum() - gb["y"] @ gb["w"] / gb["w"].sum()
+    else:
+        gap = ga["y"].mean() - gb["y"].mean()
+    row.append(float(gap))
+    row += list(dx * bs) + list(xa * (ba - bs) + xb * (bs - bb))
+    row += list(ba) + list(bb) + list(xa) + list(xb) + list(bs)
+    th, de, gm = (res[0]["theta"], res[0]["delta"], res[0]["gamma"]) if ref_mode == 0 else \
+        (res[1]["theta"], res[1]["delta"], res[1]["gamma"])
+    row += list(th * de * gm * (zmean[0] - zmean[1]))
+    return np.array(row)
+
+
+def heckman_row_len(k, ks):
+    return 6 + 2 * (k + 1) + 5 * (k + 1) + ks
 
 
 # ---------------------------------------------------------------------------------------------

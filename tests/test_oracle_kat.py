@@ -214,3 +214,90 @@ def test_resample_is_multinomial(O):
     assert abs(chi2 - (n - 1)) < 6 * np.sqrt(2 * (n - 1))
     m = O.level1_counts(0xABC, 7, 0, 100_000)
     assert m.sum() == 100_000 and len(m) == (100_000 + 255) // 256
+
+
+# --- Heckman two-step (heckman.rs, estimation.rs:114-260, math/probit.rs) ---------------------
+def test_probit_basic_convergence_kat(O):  # math/probit.rs:179-213
+    y = np.array([0.0, 1.0, 0.0, 1.0, 0.0, 1.0])
+    x = np.column_stack([np.ones(6), [-1.5, -0.5, 0.0, 0.5, 1.0, 1.5]])
+    r = O.probit(y, x, 100, 1e-6, full=True)
+    assert r["converged"] and r["iterations"] > 0 and len(r["coefficients"]) == 2
+    assert r["coefficients"][1] > 0.0
+
+
+def test_probit_non_convergence_kat(O):  # math/probit.rs:215-228
+    y = np.array([0.0, 0.0, 1.0, 1.0])
+    x = np.column_stack([np.ones(4), [-1.0, -0.5, 0.5, 1.0]])
+    r = O.probit(y, x, 1, 1e-15, full=True)
+    assert not r["converged"] and r["iterations"] == 1
+
+
+def test_probit_recovers_latent_index(O):
+    """A well-posed probit (n = 20000, index 0.3 + 0.8 z): Fisher scoring recovers it."""
+    rng = np.random.default_rng(5)
+    z = rng.normal(size=20000)
+    s = (0.3 + 0.8 * z + rng.normal(size=z.size) > 0).astype(float)
+    r = O.probit(s, np.column_stack([np.ones_like(z), z]), full=True)
+    assert r["converged"] and np.allclose(r["coefficients"], [0.3, 0.8], atol=0.05)
+
+
+def heckman_frame(n=2000, seed=42, null_unselected=True):
+    """tests/heckman_test.rs's recipe (z, x = z + 0.5 e, corr(u, e) = 0.8, s = [0.5 z + u > 0],
+    y = 1 + 2x + e, group A/B at random) with numpy draws in place of rand's StdRng."""
+    rng = np.random.default_rng(seed)
+    z = rng.normal(size=n)
+    x = z + 0.5 * rng.normal(size=n)
+    u, e0 = rng.normal(size=n), rng.normal(size=n)
+    e = 0.8 * u + np.sqrt(1 - 0.64) * e0
+    s = (0.5 * z + u > 0).astype(float)
+    y = 1.0 + 2.0 * x + e
+    grp = np.where(rng.random(n) < 0.5, "A", "B")
+    out = [float(v) if (si == 1.0 or not null_unselected) else None for v, si in zip(y, s)]
+    return {"outcome": out, "x": x.tolist(), "z": z.tolist(), "selection": s.tolist(), "group": grp.tolist()}
+
+
+def test_heckman_imr_in_detailed_kat(O):  # tests/heckman_test.rs:55-66
+    ob = O.OracleBuilder(heckman_frame(), "outcome", "group", "B").set(predictors=["x"], reps=0)
+    r = ob.heckman("selection", ["z"]).run()
+    assert any(c["name"] == "IMR" for c in r["two_fold"]["detailed_explained"])
+    # the reference drops null outcomes before the probit (builder.rs:760-784): every s is 1
+    assert len(r["residuals"]) == r["n_b"]
+
+
+def _two_step_by_hand(O, fr, grp):
+    """heckman.rs:38-108 written out with numpy lstsq for one group of a frame."""
+    g = np.array(fr["group"]) == grp
+    s, x, y, z = (np.array(fr[c]) for c in ("selection", "x", "outcome", "z"))
+    gam = O.probit(s[g], np.column_stack([np.ones(g.sum()), z[g]]))
+    sel = g & (s == 1)
+    zg = gam[0] + gam[1] * z[sel]
+    imr = O._npdf(zg) / O._ncdf(zg)
+    coef = np.linalg.lstsq(np.column_stack([np.ones(sel.sum()), x[sel], imr]), y[sel], rcond=None)[0]
+    return gam, coef, np.array([1.0, x[sel].mean(), imr.mean()])
+
+
+@pytest.mark.parametrize("ref_mode", [0, 1, 3])
+def test_heckman_two_step_consistency(O, ref_mode):
+    """Outcomes present on unselected rows: the builder's means equal the two steps written out
+    by hand, explained + unexplained = xa.ba - xb.bb, and the intercept's selection term is 0
+    (builder.rs:510-530)."""
+    fr = heckman_frame(null_unselected=False)
+    ob = O.OracleBuilder(fr, "outcome", "group", "B").set(predictors=["x"], reps=8, ref_mode=ref_mode)
+    r = ob.heckman("selection", ["z"]).run()
+    assert r["n_failed"] == 0 and r["rows"].shape == (8, O.heckman_row_len(2, 2))
+    gam_a, ba, xa = _two_step_by_hand(O, fr, "A")
+    _, bb, xb = _two_step_by_hand(O, fr, "B")
+    assert gam_a[1] > 0.2
+    assert np.allclose(r["xa_mean"], xa, rtol=1e-12) and np.allclose(r["xb_mean"], xb, rtol=1e-12)
+    est = {c["name"]: c["estimate"] for c in r["two_fold"]["aggregate"]}
+    assert abs(est["explained"] + est["unexplained"] - (xa @ ba - xb @ bb)) < 1e-8
+    assert {c["name"] for c in r["two_fold"]["detailed_explained"]} == {"__ob_intercept__", "x", "IMR"}
+    sel = r["two_fold"]["detailed_selection"]
+    assert [c["name"] for c in sel] == ["__ob_intercept__", "z"] and sel[0]["estimate"] == 0.0
+
+
+def test_heckman_pooled_unsupported(O):  # builder.rs:500-507 panics: beta_star lacks the IMR entry
+    ob = O.OracleBuilder(heckman_frame(null_unselected=False), "outcome", "group", "B").set(predictors=["x"], reps=0,
+                                                                                             ref_mode=2)
+    with pytest.raises(O.OracleError):
+        ob.heckman("selection", ["z"]).run()
