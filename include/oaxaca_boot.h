@@ -152,6 +152,8 @@ typedef struct {
   int32_t chunks;
   int32_t blocks;
   double counts_ms; /* level-2 count images (ob_count_kernel) */
+  double heckman_ms; /* Heckman panels: probit iterations + IMR sums + two-step solve (in solve_ms too) */
+  int32_t probit_iterations; /* Heckman panels: probit iterations of the last segment */
 } ob_timing;
 int ob_panel_last_timing(const ob_panel* panel, ob_timing* out);
 /* Synchronize the stream used by the last *_device call and collect its timings. */
@@ -202,11 +204,13 @@ typedef struct {
   const char* const* normalize;
   int32_t n_normalize;
   const char* weights;           /* NULL: unweighted */
-  const char* selection_outcome; /* Heckman: not supported (OB_E_UNSUPPORTED) */
+  const char* selection_outcome; /* Heckman two-step (builder .heckman_selection): the 0/1 outcome */
   uint64_t bootstrap_reps;       /* builder default 20 (builder.rs:122) */
   int32_t reference_coeffs;      /* builder default OB_REF_GROUP_A (builder.rs:123) */
   int32_t has_seed;              /* 0: fresh entropy per run, like the unseeded reference */
   uint64_t seed;
+  const char* const* selection_predictors; /* Heckman: z (intercept implicit), at most 7 */
+  int32_t n_selection_predictors;
 } ob_builder_config;
 
 typedef struct ob_prepared ob_prepared;
@@ -249,7 +253,7 @@ int ob_builder_data_matrices(const ob_column* cols, int32_t n_cols, int64_t n_ro
 #define OB_TABLE_TWO_FOLD 0            /* two_fold.aggregate: explained, unexplained */
 #define OB_TABLE_DETAILED_EXPLAINED 1
 #define OB_TABLE_DETAILED_UNEXPLAINED 2
-#define OB_TABLE_DETAILED_SELECTION 3  /* always empty (Heckman only) */
+#define OB_TABLE_DETAILED_SELECTION 3  /* Heckman only: intercept + selection predictors */
 #define OB_TABLE_THREE_FOLD 4          /* endowments, coefficients, interaction */
 
 typedef struct {

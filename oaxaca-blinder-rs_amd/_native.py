@@ -65,7 +65,8 @@ class ob_panel_desc(C.Structure):
 class ob_timing(C.Structure):
     _fields_ = [("level1_ms", C.c_double), ("gram_ms", C.c_double), ("reduce_ms", C.c_double),
                 ("solve_ms", C.c_double), ("gram_launches", C.c_int32), ("chunks", C.c_int32),
-                ("blocks", C.c_int32), ("counts_ms", C.c_double)]
+                ("blocks", C.c_int32), ("counts_ms", C.c_double),
+                ("heckman_ms", C.c_double), ("probit_iterations", C.c_int32)]
 
 
 class ob_column(C.Structure):
@@ -81,7 +82,8 @@ class ob_builder_config(C.Structure):
                 ("normalize", C.POINTER(C.c_char_p)), ("n_normalize", C.c_int32),
                 ("weights", C.c_char_p), ("selection_outcome", C.c_char_p),
                 ("bootstrap_reps", C.c_uint64), ("reference_coeffs", C.c_int32),
-                ("has_seed", C.c_int32), ("seed", C.c_uint64)]
+                ("has_seed", C.c_int32), ("seed", C.c_uint64),
+                ("selection_predictors", C.POINTER(C.c_char_p)), ("n_selection_predictors", C.c_int32)]
 
 
 class ob_component(C.Structure):

@@ -302,6 +302,10 @@ class OaxacaBuilder:
         cfg.n_normalize = len(self._normalize)
         cfg.weights = self._weights.encode() if self._weights else None
         cfg.selection_outcome = self._selection.encode() if self._selection else None
+        ptr, arr = _strs(self._selection_predictors)
+        keep.append(arr)
+        cfg.selection_predictors = ptr
+        cfg.n_selection_predictors = len(self._selection_predictors)
         cfg.bootstrap_reps = self._bootstrap_reps
         cfg.reference_coeffs = int(self._ref)
         cfg.has_seed = 0 if self._seed is None else 1

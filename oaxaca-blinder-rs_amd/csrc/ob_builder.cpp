@@ -55,6 +55,7 @@ struct Config {
   std::string weights;
   bool has_selection = false;
   std::string selection;
+  std::vector<std::string> selection_predictors;
   uint64_t reps = 20;
   int ref = OB_REF_GROUP_A;
   bool has_seed = false;
@@ -156,6 +157,7 @@ static int config_from(const ob_builder_config* c, Config& out) {
   if (c->weights) out.weights = c->weights;
   out.has_selection = c->selection_outcome != nullptr;
   if (c->selection_outcome) out.selection = c->selection_outcome;
+  OB_TRY(names(c->selection_predictors, c->n_selection_predictors, out.selection_predictors));
   out.reps = c->bootstrap_reps;
   out.ref = c->reference_coeffs;
   if (out.ref < OB_REF_GROUP_A || out.ref > OB_REF_NEUMARK)
@@ -172,6 +174,7 @@ static int clean_dataframe(const Frame& f, const Config& c, Frame& out) {
   cols.insert(cols.end(), c.categorical.begin(), c.categorical.end());
   if (c.has_weights) cols.push_back(c.weights);
   if (c.has_selection) cols.push_back(c.selection);
+  cols.insert(cols.end(), c.selection_predictors.begin(), c.selection_predictors.end());
   std::vector<int> idx;
   for (const auto& name : cols) {
     const int i = f.find(name);
@@ -380,6 +383,8 @@ struct ob_prepared {
   std::vector<double> point_row, resid_b;  // n_y x row_len, n_y x n_b
   int64_t n_a = 0, n_b = 0;
   int n_y = 1;
+  int64_t n_resid = 0;                     // residuals per outcome: n_b, or B's selected rows (Heckman)
+  std::vector<std::string> selection_names;  // Heckman: intercept + selection predictors
 };
 
 struct ob_matrices {
@@ -397,9 +402,15 @@ static uint64_t fresh_seed() {
 }
 
 static int prepare(ob_ctx* ctx, const Frame& input, const Config& c, ob_prepared** out) {
-  if (c.has_selection)
+  const bool heck = c.has_selection;
+  if (heck && (c.ref == OB_REF_POOLED || c.ref == OB_REF_NEUMARK))
     return fail(OB_E_UNSUPPORTED,
-                "Heckman selection (heckman_selection) is outside the MI355X bootstrap engine's scope");
+                "Heckman selection with pooled reference coefficients: the reference's pooled beta* has no IMR "
+                "entry and its decomposition panics on the dimension mismatch (builder.rs:547-589)");
+  if (heck && !c.normalize.empty())
+    return fail(OB_E_UNSUPPORTED, "Heckman selection with normalized categoricals is outside the engine's scope");
+  if (heck && !c.outcomes.empty())
+    return fail(OB_E_UNSUPPORTED, "Heckman selection takes one outcome");
   Staged st;
   OB_TRY(stage(input, c, st));
   if (st.split.a.empty() || st.split.b.empty())  // builder.rs:431-435
@@ -411,6 +422,7 @@ static int prepare(ob_ctx* ctx, const Frame& input, const Config& c, ob_prepared
   const int k = p + 1;
   // ols() check order for A then B (ols.rs:60-66 negative weights, ols.rs:98-105 n <= k)
   for (const Design* d : {&da, &db}) {
+    if (heck) break;  // the Heckman OLS is unweighted and its row count varies: checked on the GPU
     if (c.has_weights)
       for (double w : d->w)
         if (w < 0.0) return fail(OB_E_GROUP, "%sWeights cannot be negative", error_prefix(OB_E_GROUP));
@@ -457,6 +469,38 @@ static int prepare(ob_ctx* ctx, const Frame& input, const Config& c, ob_prepared
   pd.pooled_idx = pidx.data();
   pd.has_base = has.data();
   pd.n_y = c.outcomes.empty() ? 1 : (int32_t)c.outcomes.size();
+  // Heckman: selection outcome s (f64, prepare_selection_data's `.f64()?`) and z per group
+  std::vector<double> hs[2], hz[2];
+  int64_t n_b_sel = 0;
+  if (heck) {
+    const int si = st.df.find(c.selection);
+    if (si < 0) return fail(OB_E_COLUMN, "%s%s", error_prefix(OB_E_COLUMN), c.selection.c_str());
+    if (st.df.cols[si].kind != OB_COL_F64)
+      return fail(OB_E_POLARS, "%sinvalid series dtype: expected `Float64`, got `%s` for `%s`", error_prefix(OB_E_POLARS),
+                  dtype_name(st.df.cols[si].kind), c.selection.c_str());
+    const std::vector<int64_t>* grows[2] = {&st.split.a, &st.split.b};
+    const size_t nz = c.selection_predictors.size();
+    for (int g = 0; g < 2; ++g) {
+      const auto& rows = *grows[g];
+      const size_t n = rows.size();
+      hs[g].resize(n);
+      for (size_t r = 0; r < n; ++r) hs[g][r] = st.df.cols[si].f[rows[r]];
+      hz[g].assign(n * nz, 0.0);
+      for (size_t j = 0; j < nz; ++j) {
+        const int ci = st.df.find(c.selection_predictors[j]);
+        if (ci < 0) return fail(OB_E_COLUMN, "%s%s", error_prefix(OB_E_COLUMN), c.selection_predictors[j].c_str());
+        for (size_t r = 0; r < n; ++r) OB_TRY(numeric_value(st.df.cols[ci], rows[r], hz[g][j * n + r]));
+      }
+    }
+    for (double v : hs[1]) n_b_sel += v == 1.0 ? 1 : 0;
+    pd.heckman = 1;
+    pd.n_zsel = (int32_t)nz;
+    pd.sa = hs[0].data();
+    pd.sb = hs[1].data();
+    pd.za = hz[0].data();
+    pd.zb = hz[1].data();
+    names.push_back("IMR");  // estimation.rs:148-149
+  }
   ob_prepared* pr = new ob_prepared();
   pr->ctx = ctx;
   pr->cfg = c;
@@ -467,7 +511,7 @@ static int prepare(ob_ctx* ctx, const Frame& input, const Config& c, ob_prepared
     delete pr;
     return rc;
   }
-  pr->k = k;
+  pr->k = heck ? k + 1 : k;
   pr->n_base = ob_panel_n_base(pr->panel);
   pr->row_len = ob_panel_row_len(pr->panel);
   pr->names = names;
@@ -476,9 +520,15 @@ static int prepare(ob_ctx* ctx, const Frame& input, const Config& c, ob_prepared
   pr->n_a = da.n;
   pr->n_b = db.n;
   pr->n_y = pd.n_y;
+  pr->n_resid = heck ? n_b_sel : db.n;
+  if (heck) {
+    pr->selection_names = {"__ob_intercept__"};
+    pr->selection_names.insert(pr->selection_names.end(), c.selection_predictors.begin(),
+                               c.selection_predictors.end());
+  }
   pr->point_row.assign((size_t)pr->row_len * pr->n_y, 0.0);
-  pr->resid_b.assign((size_t)db.n * pr->n_y, 0.0);
-  rc = ob_point_estimate(pr->panel, pr->ref, pr->point_row.data(), pr->resid_b.data());
+  pr->resid_b.assign((size_t)pr->n_resid * pr->n_y, 0.0);  // Heckman: zeros (estimation.rs:152-153)
+  rc = ob_point_estimate(pr->panel, pr->ref, pr->point_row.data(), heck ? nullptr : pr->resid_b.data());
   if (rc != OB_OK) {
     ob_panel_destroy(pr->panel);
     delete pr;
@@ -505,7 +555,8 @@ static int finish(const ob_prepared* pr, int t_out, const double* rows, const ui
   res->n_a = pr->n_a;
   res->n_b = pr->n_b;
   res->n_failed = (int64_t)(n_reps - ng);
-  res->residuals.assign(pr->resid_b.begin() + (size_t)t_out * pr->n_b, pr->resid_b.begin() + (size_t)(t_out + 1) * pr->n_b);
+  res->residuals.assign(pr->resid_b.begin() + (size_t)t_out * pr->n_resid,
+                        pr->resid_b.begin() + (size_t)(t_out + 1) * pr->n_resid);
   const double* tail = point_row + 6 + 2 * kd;
   res->xa_mean.assign(tail + 2 * k, tail + 3 * k);
   res->xb_mean.assign(tail + 3 * k, tail + 4 * k);
@@ -533,6 +584,10 @@ static int finish(const ob_prepared* pr, int t_out, const double* rows, const ui
       jobs.push_back(std::move(j));
     }
   }
+  // Heckman: detailed_selection (builder.rs:510-530), after the 5K' coefficient/mean tail
+  const int sel0 = 6 + 2 * kd + 5 * k;
+  for (size_t i = 0; i < pr->selection_names.size(); ++i)
+    jobs.push_back({OB_TABLE_DETAILED_SELECTION, pr->selection_names[i], point_row[sel0 + i], {sel0 + (int)i}});
   std::vector<std::vector<int>> groups;
   for (const Job& j : jobs) groups.push_back(j.cols);
   std::vector<double> st(4 * jobs.size());
@@ -666,6 +721,7 @@ static int decompose_quantiles(ob_ctx* ctx, const ob_column* cols, int32_t n_col
     }
   }
   c.has_selection = false;  // the new builder carries no Heckman settings (builder.rs:743-754)
+  c.selection_predictors.clear();
   return ob::run_all(ctx, mod, c, out);
 }
 

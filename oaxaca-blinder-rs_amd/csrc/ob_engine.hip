@@ -25,7 +25,9 @@
 #include <cstring>
 #include <vector>
 
+#include "ob_device.hpp"
 #include "ob_engine.hpp"
+#include "ob_heckman.hpp"
 #include "ob_spec.h"
 
 typedef double ob_d4 __attribute__((ext_vector_type(4)));
@@ -66,7 +68,7 @@ struct GramArgs {
   uint32_t* flags;
   const uint32_t* counts;  // level-2 count images [tile (A then B)][batch][sub-tile][kCimgWords]
   uint32_t tiles_total;
-  int diag;  // ablation bits (OB_GRAM_DIAG, tools/gram_ablate.py): 2 no MFMAs, 4 no sub-tile DMA
+  int diag;  // OB_GRAM_DIAG bits: 2 no MFMAs, 4 no sub-tile DMA (tools/gram_ablate.py), 8 raw Heckman statuses
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -329,8 +331,6 @@ __device__ __forceinline__ void store_partials(const GramArgs& a, const Work& w,
 // Gram kernel fetches a sub-tile with a plain LDS-DMA copy. Counts are drawn once per replicate
 // batch, whatever the number of column groups.
 // ---------------------------------------------------------------------------------------------
-constexpr int kCimgStride = 17;               // u32 words per replicate row of a sub-tile image
-constexpr int kCimgWords = 64 * kCimgStride;  // one sub-tile: 64 replicates x 64 rows (u8)
 constexpr int kCntTilesPerBlock = 8;
 
 __global__ __launch_bounds__(kBlock) void ob_count_kernel(const GramArgs a) {
@@ -529,48 +529,6 @@ struct SolveArgs {
   double* raw_beta_b;  // optional: replicate-0 beta_B before normalization (ols.rs residuals)
   int raw_status;      // 1: ok[] receives the status code (1 ok, 0 Cholesky, 2 zero weight)
 };
-
-__device__ __forceinline__ double gpair(const double* g, int a, int b, int k1) {
-  return a <= b ? g[ob_pair_index(a, b, k1)] : g[ob_pair_index(b, a, k1)];
-}
-
-// nalgebra Cholesky::new order (left-looking, per-element updates in column order).
-// Fails iff a pivot is zero, negative or NaN (!is_zero && try_sqrt). m: n x n col-major.
-__device__ bool wave_cholesky(double* m, int n, int lane) {
-  for (int j = 0; j < n; ++j) {
-    for (int i = j + lane; i < n; i += 64) {
-      double v = m[i + j * n];
-      for (int c = 0; c < j; ++c) v = -m[j + c * n] * m[i + c * n] + v;
-      m[i + j * n] = v;
-    }
-    __syncthreads();
-    const double diag = m[j + j * n];
-    if (!(diag != 0.0 && diag >= 0.0)) return false;
-    const double den = sqrt(diag);
-    __syncthreads();
-    for (int i = j + lane; i < n; i += 64) m[i + j * n] = (i == j) ? den : m[i + j * n] / den;
-    __syncthreads();
-  }
-  return true;
-}
-
-__device__ void wave_chol_solve(const double* l, int n, double* b, int lane) {
-  for (int i = 0; i < n; ++i) {
-    const double coeff = b[i] / l[i + i * n];
-    __syncthreads();
-    for (int r = i + 1 + lane; r < n; r += 64) b[r] -= coeff * l[r + i * n];
-    if (lane == 0) b[i] = coeff;
-    __syncthreads();
-  }
-  for (int i = n - 1; i >= 0; --i) {
-    double part = 0.0;
-    for (int r = i + 1 + lane; r < n; r += 64) part += l[r + i * n] * b[r];
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off);
-    if (lane == 0) b[i] = (b[i] - part) / l[i + i * n];
-    __syncthreads();
-  }
-}
 
 // normalization.rs:5-51
 __device__ void normalize_coeffs(double* beta, const SolveArgs& a, const int32_t* starts,
@@ -942,6 +900,44 @@ GramArgs gram_args(const ob_panel* p, const Plan& pl) {
   return ga;
 }
 
+int ensure_heck(ob_panel* p, const Plan& pl) {
+  const int vals = std::max(ob::heck_probit_len(p->ks), ob::heck_sums_len(p->k));
+  OB_TRY(ensure_buf(&p->d_hgamma, p->cap_hgamma, (size_t)2 * pl.rep_pad * p->ks));
+  OB_TRY(ensure_buf(&p->d_hflags, p->cap_hflags, (size_t)2 * pl.rep_pad));
+  OB_TRY(ensure_buf(&p->d_hpartial, p->cap_hpartial, (size_t)pl.n_chunks() * pl.rep_pad * vals));
+  if (!p->d_hactive) HIP_OK(hipMalloc(&p->d_hactive, sizeof(uint32_t)));
+  return OB_OK;
+}
+
+ob_heck_seg heck_seg(const ob_panel* p, const Plan& pl, const uint32_t* d_chunks, const double* d_gram,
+                     int ref_mode) {
+  ob_heck_seg h{};
+  for (int g = 0; g < 2; ++g) {
+    h.cols[g] = p->d_cols[g];
+    h.ld[g] = p->ld[g];
+    h.n[g] = p->n[g];
+  }
+  h.tiles0 = p->ntiles[0];
+  h.p = p->p;
+  h.ks = p->ks;
+  h.weighted = p->h_weighted;
+  h.nb_rep = pl.nb_rep;
+  h.chunks = d_chunks;
+  h.n_chunks = pl.n_chunks();
+  h.rep_pad = pl.rep_pad;
+  h.gram = d_gram;
+  h.e_pad = p->e_pad;
+  h.k1 = p->k1;
+  h.gamma = p->d_hgamma;
+  h.hflags = p->d_hflags;
+  h.partial = p->d_hpartial;
+  h.active = p->d_hactive;
+  h.ref_mode = ref_mode;
+  h.row_len = p->row_len;
+  h.max_iter = 100;  // heckman.rs:46
+  return h;
+}
+
 }  // namespace
 
 namespace ob {
@@ -995,6 +991,46 @@ int engine_point_estimate(ob_panel* p, int ref_mode, double* row, double* resid_
     hipLaunchKernelGGL(ob_reduce_kernel, dim3((unsigned)((nred + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
                        (const double*)d_partial, (const uint32_t*)d_chunks, nch, pl.rep_pad, p->e_pad, 1u, d_gram);
     PE_OK(hipGetLastError());
+    if (p->heckman) {  // estimation.rs:114-172 on the whole groups (every row once)
+      rc = ensure_heck(p, pl);
+      if (rc != OB_OK) break;
+      ob_heck_seg hs = heck_seg(p, pl, d_chunks, d_gram, ref_mode);
+      hs.counts = nullptr;
+      hs.n_reps = 1;
+      hs.rows = d_row;
+      hs.ok = d_ok;
+      hs.raw_status = 1;
+      int it = 0;
+      rc = ob::heckman_segment(hs, s, &it);
+      if (rc != OB_OK) break;
+      uint8_t okh = 0;
+      PE_OK(hipMemcpyAsync(row, d_row, sizeof(double) * p->row_len, hipMemcpyDeviceToHost, s));
+      PE_OK(hipMemcpyAsync(&okh, d_ok, 1, hipMemcpyDeviceToHost, s));
+      PE_OK(hipStreamSynchronize(s));
+      p->timing.probit_iterations = it;
+      switch (okh) {
+        case OB_HS_OK: break;
+        case OB_HS_NO_OUTCOMES:
+          rc = ob::fail(OB_E_GROUP, "%sNo observed outcomes in group", error_prefix(OB_E_GROUP));
+          break;
+        case OB_HS_PROBIT:
+          rc = ob::fail(OB_E_LINALG, "%sFailed to solve Hessian system in Probit", error_prefix(OB_E_LINALG));
+          break;
+        case OB_HS_INSUFFICIENT:
+          rc = ob::fail(OB_E_INSUFFICIENT, "%sInsufficient data for OLS calculation: n_obs must be strictly greater than k",
+                        error_prefix(OB_E_INSUFFICIENT));
+          break;
+        case OB_HS_ZERO_WEIGHT:
+          rc = ob::fail(OB_E_GROUP, "%sNo data in groups for weighted coefficients.", error_prefix(OB_E_GROUP));
+          break;
+        default:
+          rc = ob::fail(OB_E_LINALG,
+                        "%sFailed to perform Cholesky decomposition. Matrix may be singular or not positive "
+                        "definite due to multicollinearity.",
+                        error_prefix(OB_E_LINALG));
+      }
+      break;  // residuals: zeros over the selected rows of B (estimation.rs:152-153), filled by the caller
+    }
     PE_OK(hipMalloc(&d_beta, sizeof(double) * p->k * p->n_y));
     for (int t = 0; t < p->n_y; ++t) {
       SolveArgs sa = solve_args(p, ref_mode);
@@ -1066,6 +1102,7 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   OB_TRY(ensure_buf(&p->d_partial, p->cap_partial, need_partial * p->e_pad));
   OB_TRY(ensure_buf(&p->d_gram, p->cap_gram, (size_t)2 * pl.rep_pad * p->e_pad));
   OB_TRY(ensure_buf(&p->d_chunks, p->cap_chunks, std::max(pl.chunks.size(), pl_tail.chunks.size())));
+  if (p->heckman) OB_TRY(ensure_heck(p, pl));
   HIP_OK(hipMemcpyAsync(p->d_chunks, pl.chunks.data(), sizeof(uint32_t) * pl.chunks.size(), hipMemcpyHostToDevice, s));
   HIP_OK(hipStreamSynchronize(s));  // the host vector dies with this call
   HIP_OK(hipMemsetAsync(p->d_flags, 0, sizeof(uint32_t), s));
@@ -1127,7 +1164,18 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
                        p->d_gram);
     HIP_OK(hipGetLastError());
     if (timed) HIP_OK(hipEventRecord(ev[4], s));
-    for (int t = 0; t < p->n_y; ++t) {  // outcome-major row blocks
+    if (p->heckman) {  // probit iterations + IMR sums + two-step solve (synchronizes the stream)
+      ob_heck_seg hs = heck_seg(p, plx, p->d_chunks, p->d_gram, ref_mode);
+      hs.counts = p->d_counts;
+      hs.n_reps = ns;
+      hs.rows = d_rows + s0 * p->row_len;
+      hs.ok = d_ok + s0;
+      hs.raw_status = (diag_mode() & 8) ? 1 : 0;  // OB_GRAM_DIAG bit 8: ok[] = ob_heck_status codes
+      int it = 0;
+      OB_TRY(ob::heckman_segment(hs, s, &it));
+      p->timing.probit_iterations = std::max(p->timing.probit_iterations, it);
+    }
+    for (int t = 0; t < p->n_y && !p->heckman; ++t) {  // outcome-major row blocks
       SolveArgs sa = solve_args(p, ref_mode);
       sa.yc = p->p + 1 + t;
       sa.gram = p->d_gram;
@@ -1166,6 +1214,7 @@ int engine_collect(ob_panel* p) {
       *dst[i] += t;
     }
   }
+  if (p->heckman) p->timing.heckman_ms = p->timing.solve_ms;
   uint32_t flag = 0;
   HIP_OK(hipMemcpy(&flag, p->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost));
   if (flag) return ob::fail(OB_E_OVERFLOW, "a resampled row was drawn more than 255 times in one replicate");
@@ -1230,12 +1279,27 @@ int ob_panel_create(ob_ctx* ctx, const ob_panel_desc* d, ob_panel** out) {
     return ob::fail(OB_E_UNSUPPORTED, "outcome columns must be in [1, %d], got %d", 121 - d->p, d->n_y);
   if (d->n_num < 0 || d->n_num > d->p) return ob::fail(OB_E_INVALID, "n_num out of range");
   const ob_group_desc* gd[2] = {&d->a, &d->b};
+  const bool heck = d->heckman != 0;
+  if (heck) {
+    if (d->n_zsel < 0 || d->n_zsel > ob::kHeckMaxKs - 1)
+      return ob::fail(OB_E_UNSUPPORTED, "Heckman selection predictors must be in [0, %d], got %d", ob::kHeckMaxKs - 1,
+                      d->n_zsel);
+    if (d->p > ob::kHeckMaxP)
+      return ob::fail(OB_E_UNSUPPORTED, "Heckman panels take at most %d predictor columns, got %d", ob::kHeckMaxP, d->p);
+    if (d->n_y > 1 || d->n_norm > 0)
+      return ob::fail(OB_E_UNSUPPORTED, "Heckman panels take one outcome and no normalization");
+    const double* sp[2] = {d->sa, d->sb};
+    const double* zp[2] = {d->za, d->zb};
+    for (int g = 0; g < 2; ++g)
+      if (gd[g]->n > 0 && (!sp[g] || (d->n_zsel > 0 && !zp[g])))
+        return ob::fail(OB_E_INVALID, "missing selection column pointer");
+  }
   for (int g = 0; g < 2; ++g) {
     if (gd[g]->n < 0 || gd[g]->n > 16000000) return ob::fail(OB_E_UNSUPPORTED, "group rows must be in [0, 16e6]");
     if (gd[g]->n > 0 && ((d->p > 0 && !gd[g]->x) || !gd[g]->y || (d->weighted && !gd[g]->w)))
       return ob::fail(OB_E_INVALID, "missing column pointer");
     if (gd[g]->ldx < gd[g]->n) return ob::fail(OB_E_INVALID, "ldx < n");
-    if (d->weighted)
+    if (d->weighted && !heck)  // the Heckman OLS is unweighted: weights only scale the gap / Cotton
       for (int64_t i = 0; i < gd[g]->n; ++i)
         if (gd[g]->w[i] < 0.0)
           return ob::fail(OB_E_GROUP, "%sWeights cannot be negative", ob::error_prefix(OB_E_GROUP));
@@ -1251,7 +1315,10 @@ int ob_panel_create(ob_ctx* ctx, const ob_panel_desc* d, ob_panel** out) {
   p->ncb = (p->e + 15) / 16;
   p->e_pad = p->ncb * 16;
   p->n_num = d->n_num;
-  p->weighted = d->weighted ? 1 : 0;
+  p->heckman = heck ? 1 : 0;
+  p->ks = heck ? 1 + d->n_zsel : 0;
+  p->h_weighted = heck && d->weighted ? 1 : 0;
+  p->weighted = (d->weighted || heck) ? 1 : 0;
   ob_norm_cfg& nc = p->norm;
   nc.n_norm = d->n_norm;
   if (d->n_norm > 0) {
@@ -1266,7 +1333,7 @@ int ob_panel_create(ob_ctx* ctx, const ob_panel_desc* d, ob_panel** out) {
     nc.start.assign(1, 0);
     nc.pstart.assign(1, 0);
   }
-  p->row_len = ob_row_len(p->k, nc.n_base);
+  p->row_len = heck ? ob::heck_row_len(p->k, p->ks) : ob_row_len(p->k, nc.n_base);
   int rc = OB_OK;
   auto bad = [&](hipError_t e, int line) {
     rc = ob::fail(OB_E_HIP, "HIP error %s at %s:%d", hipGetErrorString(e), __FILE__, line);
@@ -1275,7 +1342,7 @@ int ob_panel_create(ob_ctx* ctx, const ob_panel_desc* d, ob_panel** out) {
     p->n[g] = (uint32_t)gd[g]->n;
     p->ntiles[g] = (p->n[g] + OB_TILE_ROWS - 1) / OB_TILE_ROWS;
     p->ld[g] = (int64_t)std::max<uint32_t>(p->ntiles[g], 1) * OB_TILE_ROWS;
-    const int ncols = p->p + p->n_y + p->weighted;
+    const int ncols = heck ? p->p + 3 + (p->ks - 1) + p->h_weighted : p->p + p->n_y + p->weighted;
     const size_t bytes = sizeof(double) * (size_t)ncols * p->ld[g];
     hipError_t e = hipMalloc(&p->d_cols[g], bytes);
     if (e != hipSuccess) { bad(e, __LINE__); break; }
@@ -1291,7 +1358,21 @@ int ob_panel_create(ob_ctx* ctx, const ob_panel_desc* d, ob_panel** out) {
       e = hipMemcpy2D(p->d_cols[g] + (size_t)p->p * p->ld[g], sizeof(double) * p->ld[g], gd[g]->y,
                       sizeof(double) * gd[g]->ldx, sizeof(double) * n, p->n_y, hipMemcpyHostToDevice);
       if (e != hipSuccess) { bad(e, __LINE__); break; }
-      if (p->weighted) {
+      if (heck) {  // ob_heckman.hpp layout: x | y | [s == 1] | s | z | (w)
+        const double* sg = g ? d->sb : d->sa;
+        const double* zg = g ? d->zb : d->za;
+        std::vector<double> ind((size_t)n);
+        for (int64_t i = 0; i < n; ++i) ind[i] = sg[i] == 1.0 ? 1.0 : 0.0;  // estimation.rs:203-206 (== 1)
+        double* c0 = p->d_cols[g] + (size_t)(p->p + 1) * p->ld[g];
+        e = hipMemcpy(c0, ind.data(), sizeof(double) * n, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(c0 + p->ld[g], sg, sizeof(double) * n, hipMemcpyHostToDevice);
+        if (e == hipSuccess && p->ks > 1)
+          e = hipMemcpy2D(c0 + 2 * p->ld[g], sizeof(double) * p->ld[g], zg, sizeof(double) * gd[g]->ldx,
+                          sizeof(double) * n, p->ks - 1, hipMemcpyHostToDevice);
+        if (e == hipSuccess && p->h_weighted)
+          e = hipMemcpy(c0 + (size_t)(1 + p->ks) * p->ld[g], gd[g]->w, sizeof(double) * n, hipMemcpyHostToDevice);
+        if (e != hipSuccess) { bad(e, __LINE__); break; }
+      } else if (p->weighted) {
         e = hipMemcpy(p->d_cols[g] + (size_t)(p->p + p->n_y) * p->ld[g], gd[g]->w, sizeof(double) * n,
                       hipMemcpyHostToDevice);
         if (e != hipSuccess) { bad(e, __LINE__); break; }
@@ -1347,6 +1428,10 @@ void ob_panel_destroy(ob_panel* p) {
   (void)hipFree(p->d_gram);
   (void)hipFree(p->d_chunks);
   (void)hipFree(p->d_flags);
+  (void)hipFree(p->d_hgamma);
+  (void)hipFree(p->d_hflags);
+  (void)hipFree(p->d_hpartial);
+  (void)hipFree(p->d_hactive);
   (void)hipFree(p->d_rows_tmp);
   (void)hipFree(p->d_ok_tmp);
   for (hipEvent_t e : p->seg_events) (void)hipEventDestroy(e);

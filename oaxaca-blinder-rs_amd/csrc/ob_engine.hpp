@@ -7,6 +7,12 @@
 
 #include "ob_common.hpp"
 
+// Level-2 count images in HBM (ob_count_kernel): [tile (A then B)][replicate batch][sub-tile]
+// [kCimgWords]; replicate r's counts for the sub-tile's 64 rows are the 16 words at r * 17 (+1 pad
+// word), row i of the sub-tile in byte (i & 3) of word (i >> 2).
+constexpr int kCimgStride = 17;               // u32 words per replicate row of a sub-tile image
+constexpr int kCimgWords = 64 * kCimgStride;  // one sub-tile: 64 replicates x 64 rows (u8)
+
 struct ob_ctx {
   int device = 0;
   int cus = 0;
@@ -30,7 +36,9 @@ struct ob_panel {
   int e_pad = 0;    // multiple of 16
   int ncb = 0;      // 16-wide column blocks
   int n_num = 0;
-  int weighted = 0;
+  int weighted = 0;  // the Gram's weight column is present (Heckman panels: [s == 1])
+  // Heckman two-step panels (ob_heckman.hpp column layout): ks = 1 + selection predictors
+  int heckman = 0, ks = 0, h_weighted = 0;
   uint32_t n[2] = {0, 0};
   int64_t ld[2] = {0, 0};      // padded rows (multiple of OB_TILE_ROWS)
   uint32_t ntiles[2] = {0, 0};
@@ -51,6 +59,11 @@ struct ob_panel {
   uint8_t* d_ok_tmp = nullptr;
   uint64_t tmp_reps = 0;
 
+  double* d_hgamma = nullptr;     // Heckman: [2][rep_pad][ks] probit coefficients
+  uint32_t* d_hflags = nullptr;   // Heckman: [2][rep_pad] done / failed
+  double* d_hpartial = nullptr;   // Heckman: [chunk][rep_pad][values]
+  uint32_t* d_hactive = nullptr;  // Heckman: replicates still iterating
+  size_t cap_hgamma = 0, cap_hflags = 0, cap_hpartial = 0;
   size_t cap_m1 = 0, cap_partial = 0, cap_gram = 0, cap_chunks = 0, cap_counts = 0;
   std::vector<hipEvent_t> seg_events;  // 6 per segment of the last boot run
   ob_timing timing = {};

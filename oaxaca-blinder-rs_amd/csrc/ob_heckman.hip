@@ -1,0 +1,568 @@
+// ob_heckman.hip -- the Heckman two-step per replicate (builder .heckman_selection):
+//   probit of s on [1, z] by Fisher scoring from 0 (math/probit.rs:25-170),
+//   IMR lambda = phi/Phi on the selected rows, OLS of y on [1, x, lambda] over them
+//   (heckman.rs:38-108, estimation.rs:114-260), beta* and the decomposition over K + 1 terms,
+//   and the selection terms theta_ref delta_ref gamma_ref,j (zbar_A,j - zbar_B,j) (builder.rs:477-534).
+//
+// A replicate's resample enters through the same level-2 count images as the Gram kernel: every
+// sum below is sum_i c_i f(row i). The selected-row normal matrix [X'X | X'y] is the engine's
+// extended Gram with weights [s == 1]; only the IMR column needs per-replicate transcendental work.
+//
+// Kernels (one block per (row chunk, 64-replicate batch) unless noted; lane = replicate, wave =
+// 64-row sub-tile of each 256-row tile, so a wave's panel reads are uniform and count reads are
+// one word per 4 rows):
+//   ob_probit_kernel<KS>      per iteration: sum c w z z', sum c lambda z (w, lambda per probit.rs)
+//   ob_probit_step_kernel<KS> thread per (replicate, group): chunk sums in a fixed order, the
+//                             nalgebra Cholesky step (LU fallback), convergence flag
+//   ob_heck_sums_kernel<NB>   sum c lambda [1, x, y], c lambda^2, c lambda (lambda + z'gamma) over
+//                             selected rows; sum c z, c w y, c w over all rows
+//   ob_heck_solve_kernel      wave per replicate: [X'X, X'lambda; lambda'X, lambda'lambda] Cholesky,
+//                             beta*, decomposition, selection terms
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include "ob_device.hpp"
+#include "ob_engine.hpp"
+#include "ob_heckman.hpp"
+#include "ob_spec.h"
+
+namespace {
+
+constexpr int kHB = 256;
+constexpr uint32_t kDone = 1u, kFailed = 2u;
+
+#define HK_OK(expr)                                                                      \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return ob::fail(OB_E_HIP, "HIP error %s at %s:%d", hipGetErrorString(e_), __FILE__, \
+                      __LINE__);                                                         \
+  } while (0)
+
+// statrs Normal(0, 1): pdf = exp(-z^2 / 2) / sqrt(2 pi), cdf = erfc(-z / sqrt 2) / 2.
+__device__ __forceinline__ double npdf(double z) { return exp(-0.5 * z * z) / 2.5066282746310002; }
+__device__ __forceinline__ double ncdf(double z) { return 0.5 * erfc(-z / 1.4142135623730951); }
+
+// f64::clamp: NaN stays NaN.
+__device__ __forceinline__ double clamp_phi(double v) {
+  return v < 1e-10 ? 1e-10 : (v > 1.0 - 1e-10 ? 1.0 - 1e-10 : v);
+}
+
+struct Lanes {
+  uint32_t g, t0, t1, rep, rb;
+  int wave, lane;
+};
+
+__device__ __forceinline__ Lanes lanes(const ob_heck_seg& a) {
+  Lanes l;
+  l.lane = threadIdx.x & 63;
+  l.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t chunk = blockIdx.x;
+  l.rb = blockIdx.y;
+  l.g = a.chunks[3 * chunk];
+  l.t0 = a.chunks[3 * chunk + 1];
+  l.t1 = a.chunks[3 * chunk + 2];
+  l.rep = l.rb * 64 + l.lane;
+  return l;
+}
+
+// This lane's count words for the wave's sub-tile of a tile (NULL: every row once).
+__device__ __forceinline__ const uint32_t* count_row(const ob_heck_seg& a, const Lanes& l, uint32_t tile) {
+  if (!a.counts) return nullptr;
+  const size_t tt = (l.g ? a.tiles0 : 0u) + tile;
+  return a.counts + ((tt * a.nb_rep + l.rb) * 4 + l.wave) * kCimgWords + l.lane * kCimgStride;
+}
+
+// Fixed-order block sum of acc over the 4 waves into LDS row `lane` (wave 3 + 2 + 1, then + 0).
+template <int N>
+__device__ __forceinline__ void block_sum(double (&acc)[N], double* red, const Lanes& l) {
+#pragma unroll 1
+  for (int w = 3; w >= 1; --w) {
+    if (l.wave == w)
+#pragma unroll
+      for (int i = 0; i < N; ++i) red[l.lane * (N + 1) + i] = (w == 3 ? 0.0 : red[l.lane * (N + 1) + i]) + acc[i];
+    __syncthreads();
+  }
+  if (l.wave == 0)
+#pragma unroll
+    for (int i = 0; i < N; ++i) acc[i] = red[l.lane * (N + 1) + i] + acc[i];
+}
+
+template <int KS>
+__global__ __launch_bounds__(kHB) void ob_probit_kernel(const ob_heck_seg a) {
+  constexpr int NH = KS * (KS + 1) / 2, NP = NH + KS;
+  __shared__ double red[64 * (NP + 1)];
+  const Lanes l = lanes(a);
+  const size_t st = (size_t)l.g * a.rep_pad + l.rep;
+  const bool act = l.rep < a.n_reps && !(a.hflags[st] & kDone);
+  if (!__syncthreads_or(act)) return;
+  double gam[KS];
+#pragma unroll
+  for (int j = 0; j < KS; ++j) gam[j] = act ? a.gamma[st * KS + j] : 0.0;
+  double acc[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) acc[i] = 0.0;
+  const double* X = a.cols[l.g];
+  const int64_t ld = a.ld[l.g];
+  const uint32_t n = a.n[l.g];
+  const double* S = X + (size_t)(a.p + 2) * ld;
+  const double* Z = X + (size_t)(a.p + 3) * ld;
+  for (uint32_t tile = l.t0; tile < l.t1; ++tile) {
+    const uint32_t r0 = tile * OB_TILE_ROWS + l.wave * 64;
+    if (r0 >= n) break;
+    const uint32_t nr = min(64u, n - r0);
+    const uint32_t* cw = count_row(a, l, tile);
+    uint32_t word = 0;
+    for (uint32_t ri = 0; ri < nr; ++ri) {
+      if ((ri & 3) == 0) word = cw ? cw[ri >> 2] : 0x01010101u;
+      const uint32_t cu = (word >> ((ri & 3) * 8)) & 255u;
+      if (!act || cu == 0) continue;
+      const double c = (double)cu;
+      const size_t row = r0 + ri;
+      double z[KS];
+      z[0] = 1.0;
+#pragma unroll
+      for (int j = 1; j < KS; ++j) z[j] = Z[(size_t)(j - 1) * ld + row];
+      double zg = 0.0;
+#pragma unroll
+      for (int j = 0; j < KS; ++j) zg += z[j] * gam[j];
+      const double phi = npdf(zg);
+      const double bp = clamp_phi(ncdf(zg));
+      const double lam = S[row] > 0.5 ? phi / bp : -phi / (1.0 - bp);  // probit.rs:66-70
+      const double sw = sqrt(phi * phi / (bp * (1.0 - bp)));           // probit.rs:75-76
+      const double cwt = c * (sw * sw), cl = c * lam;
+      int e = 0;
+#pragma unroll
+      for (int j = 0; j < KS; ++j) {
+        const double t = cwt * z[j];
+#pragma unroll
+        for (int k = 0; k <= j; ++k) acc[e++] += t * z[k];
+      }
+#pragma unroll
+      for (int j = 0; j < KS; ++j) acc[NH + j] += cl * z[j];
+    }
+  }
+  block_sum(acc, red, l);
+  if (l.wave == 0 && l.rep < a.n_reps)
+#pragma unroll
+    for (int i = 0; i < NP; ++i) a.partial[((size_t)blockIdx.x * a.rep_pad + l.rep) * NP + i] = acc[i];
+}
+
+// nalgebra LU (partial pivoting on the first largest |pivot|) + solve; false if U is singular.
+template <int KS>
+__device__ bool lu_solve(double (&m)[KS * KS], double (&b)[KS]) {
+  int perm[KS];
+#pragma unroll
+  for (int i = 0; i < KS; ++i) perm[i] = i;
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < KS; ++i) {
+    int piv = i;
+    double best = fabs(m[i + i * KS]);
+#pragma unroll
+    for (int r = i + 1; r < KS; ++r)
+      if (fabs(m[r + i * KS]) > best) {
+        best = fabs(m[r + i * KS]);
+        piv = r;
+      }
+    // select-based swaps keep every index compile-time (registers, no scratch)
+#pragma unroll
+    for (int r = i + 1; r < KS; ++r)
+      if (r == piv) {
+#pragma unroll
+        for (int c = 0; c < KS; ++c) {
+          const double t = m[i + c * KS];
+          m[i + c * KS] = m[r + c * KS];
+          m[r + c * KS] = t;
+        }
+        const int t = perm[i];
+        perm[i] = perm[r];
+        perm[r] = t;
+      }
+    const double d = m[i + i * KS];
+    if (d == 0.0) {
+      ok = false;
+      continue;
+    }
+#pragma unroll
+    for (int r = i + 1; r < KS; ++r) m[r + i * KS] /= d;
+#pragma unroll
+    for (int c = i + 1; c < KS; ++c)
+#pragma unroll
+      for (int r = i + 1; r < KS; ++r) m[r + c * KS] += -m[i + c * KS] * m[r + i * KS];
+  }
+  if (!ok) return false;
+  double x[KS];
+#pragma unroll
+  for (int i = 0; i < KS; ++i) {
+    double v = 0.0;
+#pragma unroll
+    for (int r = 0; r < KS; ++r)
+      if (perm[i] == r) v = b[r];
+    x[i] = v;
+  }
+#pragma unroll
+  for (int i = 0; i < KS; ++i)
+#pragma unroll
+    for (int r = i + 1; r < KS; ++r) x[r] += -x[i] * m[r + i * KS];
+#pragma unroll
+  for (int i = KS - 1; i >= 0; --i) {
+    x[i] /= m[i + i * KS];
+#pragma unroll
+    for (int r = 0; r < i; ++r) x[r] += -x[i] * m[r + i * KS];
+  }
+#pragma unroll
+  for (int i = 0; i < KS; ++i) b[i] = x[i];
+  return true;
+}
+
+template <int KS>
+__global__ __launch_bounds__(64) void ob_probit_step_kernel(const ob_heck_seg a) {
+  constexpr int NH = KS * (KS + 1) / 2, NP = NH + KS;
+  const uint32_t rep = blockIdx.x * 64 + threadIdx.x, g = blockIdx.y;
+  if (rep >= a.n_reps) return;
+  const size_t st = (size_t)g * a.rep_pad + rep;
+  const uint32_t fl = a.hflags[st];
+  if (fl & kDone) return;
+  double sum[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) sum[i] = 0.0;
+  for (int c = 0; c < a.n_chunks; ++c) {
+    if (a.chunks[3 * c] != g) continue;
+    const double* pp = a.partial + ((size_t)c * a.rep_pad + rep) * NP;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) sum[i] += pp[i];
+  }
+  // -H = sum c w z z' + 1e-9 I (probit.rs:95-118), g = sum c lambda z
+  double m[KS * KS], l[KS * KS], b[KS];
+  int e = 0;
+#pragma unroll
+  for (int j = 0; j < KS; ++j)
+#pragma unroll
+    for (int k = 0; k <= j; ++k) {
+      m[j + k * KS] = sum[e];
+      m[k + j * KS] = sum[e];
+      ++e;
+    }
+#pragma unroll
+  for (int j = 0; j < KS; ++j) {
+    m[j + j * KS] += 1e-9;
+    b[j] = sum[NH + j];
+  }
+#pragma unroll
+  for (int i = 0; i < KS * KS; ++i) l[i] = m[i];
+  bool chol = true;
+#pragma unroll
+  for (int j = 0; j < KS; ++j) {  // nalgebra Cholesky::new order
+#pragma unroll
+    for (int i = j; i < KS; ++i) {
+      double v = l[i + j * KS];
+#pragma unroll
+      for (int c = 0; c < j; ++c) v = -l[j + c * KS] * l[i + c * KS] + v;
+      l[i + j * KS] = v;
+    }
+    const double diag = l[j + j * KS];
+    if (!(diag != 0.0 && diag >= 0.0)) chol = false;
+    const double den = sqrt(diag);
+#pragma unroll
+    for (int i = j + 1; i < KS; ++i) l[i + j * KS] /= den;
+    l[j + j * KS] = den;
+  }
+  double step[KS];
+#pragma unroll
+  for (int i = 0; i < KS; ++i) step[i] = b[i];
+  if (chol) {
+#pragma unroll
+    for (int i = 0; i < KS; ++i) {
+      const double coeff = step[i] / l[i + i * KS];
+#pragma unroll
+      for (int r = i + 1; r < KS; ++r) step[r] -= coeff * l[r + i * KS];
+      step[i] = coeff;
+    }
+#pragma unroll
+    for (int i = KS - 1; i >= 0; --i) {
+      double part = 0.0;
+#pragma unroll
+      for (int r = i + 1; r < KS; ++r) part += l[r + i * KS] * step[r];
+      step[i] = (step[i] - part) / l[i + i * KS];
+    }
+  } else if (!lu_solve<KS>(m, step)) {  // probit.rs:124-137: -(H^-1 g) = (-H)^-1 g
+    a.hflags[st] = kDone | kFailed;
+    return;
+  }
+  double nrm = 0.0;
+#pragma unroll
+  for (int i = 0; i < KS; ++i) {
+    a.gamma[st * KS + i] += step[i];
+    nrm += step[i] * step[i];
+  }
+  if (sqrt(nrm) < 1e-6)
+    a.hflags[st] = kDone;
+  else
+    atomicAdd(a.active, 1u);
+}
+
+template <int NB>
+__global__ __launch_bounds__(kHB) void ob_heck_sums_kernel(const ob_heck_seg a) {
+  __shared__ double red[64 * (NB + 1)];
+  const Lanes l = lanes(a);
+  const bool act = l.rep < a.n_reps;
+  if (!__syncthreads_or(act)) return;
+  const int K = a.p + 1, nhs = ob::heck_sums_len(K), ks = a.ks;
+  const size_t st = (size_t)l.g * a.rep_pad + l.rep;
+  double gam[ob::kHeckMaxKs];
+#pragma unroll
+  for (int j = 0; j < ob::kHeckMaxKs; ++j) gam[j] = (act && j < ks) ? a.gamma[st * ks + j] : 0.0;
+  double acc[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) acc[i] = 0.0;
+  const double* X = a.cols[l.g];
+  const int64_t ld = a.ld[l.g];
+  const uint32_t n = a.n[l.g];
+  const double* Y = X + (size_t)a.p * ld;
+  const double* IND = X + (size_t)(a.p + 1) * ld;
+  const double* Z = X + (size_t)(a.p + 3) * ld;
+  const double* W = a.weighted ? X + (size_t)(a.p + 2 + ks) * ld : nullptr;
+  for (uint32_t tile = l.t0; tile < l.t1; ++tile) {
+    const uint32_t r0 = tile * OB_TILE_ROWS + l.wave * 64;
+    if (r0 >= n) break;
+    const uint32_t nr = min(64u, n - r0);
+    const uint32_t* cw = count_row(a, l, tile);
+    uint32_t word = 0;
+    for (uint32_t ri = 0; ri < nr; ++ri) {
+      if ((ri & 3) == 0) word = cw ? cw[ri >> 2] : 0x01010101u;
+      const uint32_t cu = (word >> ((ri & 3) * 8)) & 255u;
+      if (!act || cu == 0) continue;
+      const double c = (double)cu;
+      const size_t row = r0 + ri;
+      double z[ob::kHeckMaxKs];
+      z[0] = 1.0;
+#pragma unroll
+      for (int j = 1; j < ob::kHeckMaxKs; ++j) z[j] = j < ks ? Z[(size_t)(j - 1) * ld + row] : 0.0;
+      double zg = 0.0;
+#pragma unroll
+      for (int j = 0; j < ob::kHeckMaxKs; ++j)
+        if (j < ks) zg += z[j] * gam[j];
+#pragma unroll
+      for (int j = 0; j < ob::kHeckMaxKs; ++j) acc[5 + j] += c * z[j];  // selection means (all rows)
+      const double y = Y[row], w = W ? W[row] : 1.0;
+      acc[3] += c * w * y;  // total gap (builder.rs:676-684, all rows)
+      acc[4] += c * w;
+      if (IND[row] == 1.0) {  // heckman.rs:56-69: lambda = phi / Phi, 0 when Phi < 1e-10
+        const double bp = ncdf(zg);
+        const double lam = bp < 1e-10 ? 0.0 : npdf(zg) / bp;
+        const double cl = c * lam;
+        acc[0] += cl * y;
+        acc[1] += cl * lam;
+        acc[2] += cl * (lam + zg);
+        acc[13] += cl;
+#pragma unroll
+        for (int j = 1; j < NB - 13; ++j)
+          if (j < K) acc[13 + j] += cl * X[(size_t)(j - 1) * ld + row];
+      }
+    }
+  }
+  block_sum(acc, red, l);
+  if (l.wave == 0 && act)
+#pragma unroll
+    for (int i = 0; i < NB; ++i)
+      if (i < nhs) a.partial[((size_t)blockIdx.x * a.rep_pad + l.rep) * nhs + i] = acc[i];
+}
+
+size_t heck_solve_lds(const ob_heck_seg& a) {
+  const int K = a.p + 1, kp = K + 1;
+  return sizeof(double) * ((size_t)kp * kp + 7 * (size_t)kp + 2 * (size_t)ob::heck_sums_len(K) + 4);
+}
+
+// Sums layout (per group): [0] c lam y, [1] c lam^2, [2] c lam (lam + z'g), [3] c w y, [4] c w,
+// [5..13) c z_j, [13..13+K) c lam x_j (x_0 = 1).
+__global__ __launch_bounds__(64) void ob_heck_solve_kernel(const ob_heck_seg a) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int lane = threadIdx.x;
+  const uint32_t rep = blockIdx.x;
+  if (rep >= a.n_reps) return;
+  const int K = a.p + 1, kp = K + 1, nhs = ob::heck_sums_len(K), ks = a.ks;
+  double* M = sm;
+  double* rhs = M + kp * kp;
+  double* beta_a = rhs + kp;
+  double* beta_b = beta_a + kp;
+  double* xam = beta_b + kp;
+  double* xbm = xam + kp;
+  double* bstar = xbm + kp;
+  double* S = bstar + kp;      // [2][nhs]
+  double* delta = S + 2 * nhs;  // [2]
+  for (int i = lane; i < 2 * nhs; i += 64) {
+    const uint32_t g = (uint32_t)(i / nhs);
+    const int j = i % nhs;
+    double v = 0.0;
+    for (int c = 0; c < a.n_chunks; ++c)
+      if (a.chunks[3 * c] == g) v += a.partial[((size_t)c * a.rep_pad + rep) * nhs + j];
+    S[i] = v;
+  }
+  __syncthreads();
+  const double* GA = a.gram + (size_t)rep * 2 * a.e_pad;
+  const double* GB = GA + a.e_pad;
+  double* row = a.rows + (size_t)rep * a.row_len;
+  uint8_t status = OB_HS_OK;
+  if (GA[0] == 0.0 || GB[0] == 0.0) status = OB_HS_NO_OUTCOMES;  // estimation.rs:124-125
+  for (int g = 0; g < 2 && status == OB_HS_OK; ++g) {
+    if (a.hflags[(size_t)g * a.rep_pad + rep] & kFailed) {
+      status = OB_HS_PROBIT;
+      break;
+    }
+    const double* G = g ? GB : GA;
+    const double* Sg = S + g * nhs;
+    const double nsel = G[0];
+    if (nsel <= (double)kp) {  // ols.rs:98-104
+      status = OB_HS_INSUFFICIENT;
+      break;
+    }
+    for (int i = lane; i < kp * kp; i += 64) {
+      const int r = i % kp, c = i / kp;
+      double v;
+      if (r < K && c < K)
+        v = gpair(G, r, c, a.k1);
+      else if (r == K && c == K)
+        v = Sg[1];
+      else
+        v = Sg[13 + (r == K ? c : r)];
+      M[r + c * kp] = v;
+    }
+    for (int i = lane; i < kp; i += 64) rhs[i] = i < K ? gpair(G, i, K, a.k1) : Sg[0];
+    __syncthreads();
+    if (!wave_cholesky(M, kp, lane)) {
+      status = OB_HS_CHOLESKY;
+      break;
+    }
+    wave_chol_solve(M, kp, rhs, lane);
+    double* beta = g ? beta_b : beta_a;
+    double* xm = g ? xbm : xam;
+    for (int i = lane; i < kp; i += 64) {
+      beta[i] = rhs[i];
+      xm[i] = i < K ? gpair(G, 0, i, a.k1) / nsel : Sg[13] / nsel;  // row means + IMR mean
+    }
+    if (lane == 0) delta[g] = -Sg[2] / nsel;  // heckman.rs:92-99
+    __syncthreads();
+  }
+  if (status == OB_HS_OK) {  // beta* (builder.rs:536-621; Pooled/Neumark are refused on the host)
+    if (a.ref_mode == OB_REF_GROUP_A || a.ref_mode == OB_REF_GROUP_B) {
+      const double* src = a.ref_mode == OB_REF_GROUP_A ? beta_a : beta_b;
+      for (int i = lane; i < kp; i += 64) bstar[i] = src[i];
+    } else {
+      const double sa = S[4], sb = S[nhs + 4];
+      const double tot = sa + sb;
+      if (tot == 0.0) {
+        status = OB_HS_ZERO_WEIGHT;
+      } else {
+        const double wA = sa / tot, wB = 1.0 - wA;
+        for (int i = lane; i < kp; i += 64) bstar[i] = beta_a[i] * wA + beta_b[i] * wB;
+      }
+    }
+  }
+  __syncthreads();
+  if (lane == 0) {
+    if (status != OB_HS_OK) {
+      for (int i = 0; i < a.row_len; ++i) row[i] = __builtin_nan("");
+    } else {
+      double* dex = row + 6;
+      double* dun = row + 6 + kp;
+      double expl = 0.0, ta = 0.0, tb = 0.0, endow = 0.0, coef = 0.0, inter = 0.0;
+      for (int j = 0; j < kp; ++j) {  // decomposition.rs:56-89
+        const double dx = xam[j] - xbm[j], db = beta_a[j] - beta_b[j];
+        expl += dx * bstar[j];
+        ta += xam[j] * beta_a[j];
+        tb += xbm[j] * beta_b[j];
+        endow += dx * beta_b[j];
+        coef += xbm[j] * db;
+        inter += dx * db;
+      }
+      for (int j = 0; j < kp; ++j) {  // decomposition.rs:92-122
+        dex[j] = (xam[j] - xbm[j]) * bstar[j];
+        dun[j] = xam[j] * (beta_a[j] - bstar[j]) + xbm[j] * (bstar[j] - beta_b[j]);
+      }
+      row[0] = expl;
+      row[1] = (ta - tb) - expl;
+      row[2] = endow;
+      row[3] = coef;
+      row[4] = inter;
+      row[5] = S[3] / S[4] - S[nhs + 3] / S[nhs + 4];
+      double* tail = row + 6 + 2 * kp;
+      for (int j = 0; j < kp; ++j) {
+        tail[j] = beta_a[j];
+        tail[kp + j] = beta_b[j];
+        tail[2 * kp + j] = xam[j];
+        tail[3 * kp + j] = xbm[j];
+        tail[4 * kp + j] = bstar[j];
+      }
+      // selection terms (builder.rs:510-530): A's (theta, delta, gamma) for GroupA, else B's
+      const int gr = a.ref_mode == OB_REF_GROUP_A ? 0 : 1;
+      const double theta = gr ? beta_b[K] : beta_a[K];
+      const double* gam = a.gamma + ((size_t)gr * a.rep_pad + rep) * ks;
+      double* sel = tail + 5 * kp;
+      for (int j = 0; j < ks; ++j) {
+        const double za = S[5 + j] / S[5], zb = S[nhs + 5 + j] / S[nhs + 5];
+        sel[j] = theta * delta[gr] * gam[j] * (za - zb);
+      }
+    }
+    a.ok[rep] = a.raw_status ? status : (uint8_t)(status == OB_HS_OK);
+  }
+}
+
+template <int KS>
+hipError_t launch_probit_iter(const ob_heck_seg& a, hipStream_t s) {
+  hipLaunchKernelGGL(ob_probit_kernel<KS>, dim3(a.n_chunks, a.rep_pad / 64), dim3(kHB), 0, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(ob_probit_step_kernel<KS>, dim3(a.rep_pad / 64, 2), dim3(64), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t probit_iter(const ob_heck_seg& a, hipStream_t s) {
+  switch (a.ks) {
+    case 1: return launch_probit_iter<1>(a, s);
+    case 2: return launch_probit_iter<2>(a, s);
+    case 3: return launch_probit_iter<3>(a, s);
+    case 4: return launch_probit_iter<4>(a, s);
+    case 5: return launch_probit_iter<5>(a, s);
+    case 6: return launch_probit_iter<6>(a, s);
+    case 7: return launch_probit_iter<7>(a, s);
+    default: return launch_probit_iter<8>(a, s);
+  }
+}
+
+}  // namespace
+
+namespace ob {
+
+int heckman_segment(const ob_heck_seg& a, hipStream_t s, int* iters) {
+  if (a.ks < 1 || a.ks > kHeckMaxKs || a.p > kHeckMaxP || a.rep_pad % 64 != 0)
+    return ob::fail(OB_E_INVALID, "heckman segment: bad shape");
+  HK_OK(hipMemsetAsync(a.gamma, 0, sizeof(double) * 2 * a.rep_pad * a.ks, s));
+  HK_OK(hipMemsetAsync(a.hflags, 0, sizeof(uint32_t) * 2 * a.rep_pad, s));
+  int it = 0;
+  while (it < a.max_iter) {  // probit.rs:48-147, each replicate stopping on its own
+    HK_OK(hipMemsetAsync(a.active, 0, sizeof(uint32_t), s));
+    HK_OK(probit_iter(a, s));
+    ++it;
+    uint32_t active = 0;
+    HK_OK(hipMemcpyAsync(&active, a.active, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    HK_OK(hipStreamSynchronize(s));
+    if (active == 0) break;
+  }
+  if (iters) *iters = it;
+  const dim3 grid(a.n_chunks, a.rep_pad / 64);
+  if (heck_sums_len(a.p + 1) <= 32)
+    hipLaunchKernelGGL(ob_heck_sums_kernel<32>, grid, dim3(kHB), 0, s, a);
+  else
+    hipLaunchKernelGGL(ob_heck_sums_kernel<64>, grid, dim3(kHB), 0, s, a);
+  HK_OK(hipGetLastError());
+  const size_t lds = heck_solve_lds(a);
+  HK_OK(hipFuncSetAttribute((const void*)ob_heck_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  hipLaunchKernelGGL(ob_heck_solve_kernel, dim3(a.n_reps), dim3(64), lds, s, a);
+  HK_OK(hipGetLastError());
+  return OB_OK;
+}
+
+}  // namespace ob

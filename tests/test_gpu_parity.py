@@ -365,7 +365,7 @@ def test_errors_on_gpu(ob, N):
     assert e.value.code == N.OB_E_GROUP and "One group has no data" in str(e.value)
     with pytest.raises(N.OaxacaError) as e:
         ob.OaxacaBuilder(base, "y", "g", "b").predictors(["x"]).heckman_selection("s", ["x"]).run()
-    assert e.value.code == N.OB_E_UNSUPPORTED
+    assert e.value.code == N.OB_E_COLUMN
 
 
 def test_sharded_fit_two_ranks_on_one_gpu(ob, O, tmp_path):
