@@ -282,6 +282,50 @@ int ob_matrices_get(const ob_matrices* m, const double** x_a, const double** y_a
 const char* ob_matrices_name(const ob_matrices* m, int32_t i);
 void ob_matrices_free(ob_matrices* m);
 
+/* ---- Machado-Mata (QuantileDecompositionBuilder, quantile_decomposition.rs:21-445) ---------
+ * A pass (run_single_pass, :173-279): `simulations` quantile regressions per group at the MM-1
+ * quantiles (csrc/ob_spec.h; the reference draws from an unseeded thread_rng), one MM-1 row pick
+ * per group per successful simulation, predictions x_A b_A, x_B b_B, x_A b_B, and empirical
+ * quantiles. Each QR (math/quantile_regression.rs:22-129, Clarabel LP) is solved on the GPU by an
+ * interior-point method on its dual LP; the replicates are OBRS-1 resamples. */
+
+/* Runs the point pass (every row once; with_point != 0) then one pass per replicate of
+   [first_rep, first_rep + n_reps). rows: (with_point + n_reps) x 3 n_quantiles host doubles,
+   [gap, characteristics, coefficients] per quantile; ok[r] = 0 where the pass failed (fewer than
+   simulations / 2 successful fits in a group, :231-236). panel: unweighted, one outcome, at most
+   15 predictor columns. Replaces run_single_pass + the bootstrap loop (:173-354). */
+int ob_mm_run(ob_panel* panel, uint64_t seed, int32_t simulations, const double* quantiles,
+              int32_t n_quantiles, uint64_t first_rep, uint64_t n_reps, int32_t with_point, double* rows,
+              uint8_t* ok);
+
+typedef struct {
+  const char* outcome;
+  const char* group;
+  const char* reference_group;
+  const char* const* predictors;
+  int32_t n_predictors;
+  const char* const* categorical;
+  int32_t n_categorical;
+  const double* quantiles; /* NULL: the builder default {0.1, 0.25, 0.5, 0.75, 0.9} */
+  int32_t n_quantiles;
+  int32_t simulations;     /* builder default 200 */
+  uint64_t bootstrap_reps; /* builder default 20 */
+  int32_t has_seed;        /* 0: fresh entropy per run, like the reference's thread_rng */
+  uint64_t seed;
+} ob_qd_config;
+
+typedef struct ob_qd_results ob_qd_results;
+/* QuantileDecompositionBuilder::run over a column frame (quantile_decomposition.rs:281-445). */
+int ob_quantile_decomposition_run(ob_ctx* ctx, const ob_column* cols, int32_t n_cols, int64_t n_rows,
+                                  const ob_qd_config* cfg, ob_qd_results** out);
+/* results_by_quantile: n entries keyed "q{floor(100 tau)}" (a repeated key keeps the later
+   quantile, as the reference's HashMap does), in first-appearance order of the keys. */
+int ob_qd_results_dims(const ob_qd_results* r, int32_t* n_entries, int64_t* n_a, int64_t* n_b);
+/* comps[0..2] = Total Gap, Characteristics, Coefficients (QuantileDecompositionDetail). */
+int ob_qd_results_get(const ob_qd_results* r, int32_t i, const char** key, ob_component* comps);
+int64_t ob_qd_results_n_failed(const ob_qd_results* r);
+void ob_qd_results_free(ob_qd_results* r);
+
 #ifdef __cplusplus
 }
 #endif

@@ -7,7 +7,8 @@ hyphen). See DESIGN.md for the kernels and INTEGRATION.md for the Rust/C binding
 from . import _native
 from ._native import OaxacaError
 from .api import (BudgetAdjustment, ComponentResult, DecompositionDetail, OaxacaBlinder, OaxacaBuilder,
-                  OaxacaResults, PreparedRun, ReferenceCoefficients, TwoFoldResults, parse_formula)
+                  OaxacaResults, PreparedRun, QuantileDecompositionBuilder, QuantileDecompositionDetail,
+                  QuantileDecompositionResults, ReferenceCoefficients, TwoFoldResults, parse_formula)
 from .engine import Panel, aggregate, bootstrap_stats, rif, row_layout
 from .frame import Frame, read_csv
 
@@ -15,4 +16,5 @@ __all__ = [
     "OaxacaBuilder", "OaxacaBlinder", "OaxacaResults", "TwoFoldResults", "DecompositionDetail",
     "ComponentResult", "BudgetAdjustment", "ReferenceCoefficients", "OaxacaError", "PreparedRun",
     "Panel", "Frame", "read_csv", "aggregate", "bootstrap_stats", "rif", "row_layout", "parse_formula",
+    "QuantileDecompositionBuilder", "QuantileDecompositionDetail", "QuantileDecompositionResults",
 ]

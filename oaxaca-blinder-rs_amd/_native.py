@@ -35,6 +35,8 @@ EXPORTED = (
     "ob_results_total_gap", "ob_results_n_a", "ob_results_n_b", "ob_results_n_failed",
     "ob_results_count", "ob_results_component", "ob_results_vector", "ob_results_free",
     "ob_matrices_dims", "ob_matrices_get", "ob_matrices_name", "ob_matrices_free",
+    "ob_mm_run", "ob_quantile_decomposition_run", "ob_qd_results_dims", "ob_qd_results_get",
+    "ob_qd_results_n_failed", "ob_qd_results_free",
 )
 
 
@@ -84,6 +86,15 @@ class ob_builder_config(C.Structure):
                 ("bootstrap_reps", C.c_uint64), ("reference_coeffs", C.c_int32),
                 ("has_seed", C.c_int32), ("seed", C.c_uint64),
                 ("selection_predictors", C.POINTER(C.c_char_p)), ("n_selection_predictors", C.c_int32)]
+
+
+class ob_qd_config(C.Structure):
+    _fields_ = [("outcome", C.c_char_p), ("group", C.c_char_p), ("reference_group", C.c_char_p),
+                ("predictors", C.POINTER(C.c_char_p)), ("n_predictors", C.c_int32),
+                ("categorical", C.POINTER(C.c_char_p)), ("n_categorical", C.c_int32),
+                ("quantiles", C.POINTER(C.c_double)), ("n_quantiles", C.c_int32),
+                ("simulations", C.c_int32), ("bootstrap_reps", C.c_uint64),
+                ("has_seed", C.c_int32), ("seed", C.c_uint64)]
 
 
 class ob_component(C.Structure):
@@ -149,6 +160,13 @@ _SIGS = {
     "ob_matrices_get": (C.c_int, [_P, C.POINTER(_D), C.POINTER(_D), C.POINTER(_D), C.POINTER(_D)]),
     "ob_matrices_name": (C.c_char_p, [_P, C.c_int32]),
     "ob_matrices_free": (None, [_P]),
+    "ob_mm_run": (C.c_int, [_P, C.c_uint64, C.c_int32, _D, C.c_int32, C.c_uint64, C.c_uint64, C.c_int32, _D, _U8]),
+    "ob_quantile_decomposition_run": (C.c_int, [_P, C.POINTER(ob_column), C.c_int32, C.c_int64,
+                                                C.POINTER(ob_qd_config), C.POINTER(_P)]),
+    "ob_qd_results_dims": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+    "ob_qd_results_get": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_char_p), C.POINTER(ob_component)]),
+    "ob_qd_results_n_failed": (C.c_int64, [_P]),
+    "ob_qd_results_free": (None, [_P]),
 }
 
 _lib = None

@@ -24,6 +24,7 @@
 #include "ob_common.hpp"
 #include "ob_engine.hpp"
 #include "ob_host.hpp"
+#include "ob_mm.hpp"
 #include "ob_spec.h"
 
 namespace ob {
@@ -626,6 +627,215 @@ static int run_all(ob_ctx* ctx, const Frame& f, const Config& c, ob_results** ou
 }
 
 }  // namespace ob
+
+// ---------------------------------------------------------------------------------------------
+// Machado-Mata: QuantileDecompositionBuilder::run (quantile_decomposition.rs:21-445)
+// ---------------------------------------------------------------------------------------------
+struct ob_qd_results {
+  int64_t n_a = 0, n_b = 0, n_failed = 0;
+  std::vector<std::string> keys;
+  std::vector<std::vector<ob_results::Comp>> comps;  // per key: Total Gap, Characteristics, Coefficients
+};
+
+namespace ob {
+
+struct QdConfig {
+  std::string outcome, group, reference_group;
+  std::vector<std::string> predictors, categorical;
+  std::vector<double> quantiles;
+  int sims = 200;
+  uint64_t reps = 20;
+  bool has_seed = false;
+  uint64_t seed = 0;
+};
+
+// prepare_data (quantile_decomposition.rs:96-141): y must be Float64 without nulls; X columns =
+// predictors then dummies (intercept implicit); a null predictor value reads as NaN (to_ndarray).
+static int qd_design(const Frame& f, const std::vector<int64_t>& rows, const QdConfig& c,
+                     const std::vector<std::string>& dummy_names, Design& d) {
+  const int yi = f.find(c.outcome);
+  if (f.cols[yi].kind != OB_COL_F64)
+    return fail(OB_E_POLARS, "%sinvalid series dtype: expected `Float64`, got `%s` for `%s`", error_prefix(OB_E_POLARS),
+                dtype_name(f.cols[yi].kind), c.outcome.c_str());
+  const int64_t n = (int64_t)rows.size();
+  d.n = n;
+  d.y.resize(n);
+  for (int64_t r = 0; r < n; ++r) {
+    if (!f.cols[yi].valid[rows[r]])
+      return fail(OB_E_GROUP, "%sNull outcome encountered", error_prefix(OB_E_GROUP));
+    d.y[r] = f.cols[yi].f[rows[r]];
+  }
+  std::vector<std::string> xs = c.predictors;
+  xs.insert(xs.end(), dummy_names.begin(), dummy_names.end());
+  d.x.assign((size_t)n * xs.size(), 0.0);
+  for (size_t j = 0; j < xs.size(); ++j) {
+    const int ci = f.find(xs[j]);
+    for (int64_t r = 0; r < n; ++r) {
+      if (!f.cols[ci].valid[rows[r]]) {
+        d.x[j * n + r] = NAN;
+        continue;
+      }
+      OB_TRY(numeric_value(f.cols[ci], rows[r], d.x[j * n + r]));
+    }
+  }
+  return OB_OK;
+}
+
+static int qd_run(ob_ctx* ctx, const Frame& f, const QdConfig& c, ob_qd_results** out) {
+  std::vector<std::string> need = {c.outcome, c.group};  // df.select (:284-287): no null cleaning
+  need.insert(need.end(), c.predictors.begin(), c.predictors.end());
+  need.insert(need.end(), c.categorical.begin(), c.categorical.end());
+  for (const auto& nm : need)
+    if (f.find(nm) < 0) return fail(OB_E_COLUMN, "%s%s", error_prefix(OB_E_COLUMN), nm.c_str());
+  if (c.quantiles.empty()) return fail(OB_E_INVALID, "no target quantiles");
+  Frame df = f;
+  std::vector<std::string> dummy_names;
+  for (const auto& cat : c.categorical) {  // create_dummies_manual (:143-161); a null level reads NaN
+    const int ci = df.find(cat);
+    Dummies dm;
+    OB_TRY(create_dummies(df.cols[ci], dm));
+    for (auto& col : dm.cols) {
+      if (df.find(col.name) >= 0)
+        return fail(OB_E_POLARS, "%sduplicate: column with name '%s' has more than one occurrence",
+                    error_prefix(OB_E_POLARS), col.name.c_str());
+      for (int64_t r = 0; r < df.nrows; ++r)
+        if (!df.cols[ci].valid[r]) col.f[r] = NAN;
+      dummy_names.push_back(col.name);
+      df.cols.push_back(std::move(col));
+    }
+  }
+  const Col& g = df.cols[df.find(c.group)];  // run_single_pass (:178-206)
+  OB_TRY(expect_str(g));
+  const auto levels = sorted_levels(g);
+  if (levels.size() < 2) return fail(OB_E_GROUP, "%sNot enough groups", error_prefix(OB_E_GROUP));
+  const std::string& name_b = c.reference_group;
+  const std::string name_a = levels[0] != name_b ? levels[0] : levels[1];
+  std::vector<int64_t> ra, rb;
+  for (int64_t r = 0; r < df.nrows; ++r) {
+    if (!g.valid[r]) continue;
+    if (g.s[r] == name_a) ra.push_back(r);
+    if (g.s[r] == name_b) rb.push_back(r);
+  }
+  if (ra.size() < 2 || rb.size() < 2)
+    return fail(OB_E_GROUP, "%sOne group has insufficient data", error_prefix(OB_E_GROUP));
+  Design da, db;
+  OB_TRY(qd_design(df, ra, c, dummy_names, da));
+  OB_TRY(qd_design(df, rb, c, dummy_names, db));
+  const int p = (int)(c.predictors.size() + dummy_names.size());
+  if (p + 1 > kMmMaxK)
+    return fail(OB_E_UNSUPPORTED, "Machado-Mata takes at most %d predictor columns (dummies included), got %d",
+                kMmMaxK - 1, p);
+  ob_panel_desc pd{};
+  pd.p = p;
+  pd.n_num = (int32_t)c.predictors.size();
+  pd.a = {da.n, da.x.data(), da.n, da.y.data(), nullptr};
+  pd.b = {db.n, db.x.data(), db.n, db.y.data(), nullptr};
+  pd.n_y = 1;
+  ob_panel* panel = nullptr;
+  OB_TRY(ob_panel_create(ctx, &pd, &panel));
+  const int nq = (int)c.quantiles.size();
+  std::vector<double> rows((size_t)(1 + c.reps) * 3 * nq);
+  std::vector<uint8_t> ok(1 + c.reps, 0);
+  const uint64_t seed = c.has_seed ? c.seed : fresh_seed();
+  int rc = mm_run(panel, seed, c.sims, c.quantiles.data(), nq, 0, c.reps, true, rows.data(), ok.data(), nullptr);
+  ob_panel_destroy(panel);
+  if (rc != OB_OK) return rc;
+  if (!ok[0])  // the point pass failed (:231-236)
+    return fail(OB_E_LINALG, "%sFailed to estimate a sufficient number of quantile regressions.",
+                error_prefix(OB_E_LINALG));
+  ob_qd_results* res = new ob_qd_results();
+  for (int64_t r = 0; r < f.nrows; ++r) {  // n_a / n_b over the whole frame (:423-441)
+    if (!g.valid[r]) continue;
+    res->n_a += g.s[r] == name_a;
+    res->n_b += g.s[r] == name_b;
+  }
+  uint64_t ng = 0;
+  for (uint64_t r = 0; r < c.reps; ++r) ng += ok[1 + r] ? 1 : 0;
+  res->n_failed = (int64_t)(c.reps - ng);
+  // keys "q{floor(100 tau)}" (:270); a repeated key keeps the later quantile (HashMap::insert)
+  std::vector<int> slot_of_key;
+  for (int j = 0; j < nq; ++j) {
+    const std::string key = "q" + std::to_string((uint32_t)(c.quantiles[j] * 100.0));
+    auto it = std::find(res->keys.begin(), res->keys.end(), key);
+    if (it == res->keys.end()) {
+      res->keys.push_back(key);
+      slot_of_key.push_back(j);
+    } else {
+      slot_of_key[it - res->keys.begin()] = j;
+    }
+  }
+  static const char* names[3] = {"Total Gap", "Characteristics", "Coefficients"};
+  std::vector<double> v;
+  for (size_t e = 0; e < res->keys.size(); ++e) {
+    const int j = slot_of_key[e];
+    std::vector<ob_results::Comp> cs;
+    for (int k = 0; k < 3; ++k) {
+      v.clear();
+      for (uint64_t r = 0; r < c.reps; ++r)
+        if (ok[1 + r]) v.push_back(rows[(1 + r) * 3 * nq + 3 * j + k]);
+      double s4[4];
+      bootstrap_stats(v.data(), (int64_t)v.size(), s4);
+      const double pt = rows[3 * j + k];
+      cs.push_back({names[k], pt, s4[0], std::fabs(s4[0]) > 1e-9 ? pt / s4[0] : 0.0, s4[1], s4[2], s4[3]});
+    }
+    res->comps.push_back(std::move(cs));
+  }
+  *out = res;
+  return OB_OK;
+}
+
+}  // namespace ob
+
+extern "C" {
+
+int ob_quantile_decomposition_run(ob_ctx* ctx, const ob_column* cols, int32_t n_cols, int64_t n_rows,
+                                  const ob_qd_config* cfg, ob_qd_results** out) {
+  if (!ctx || !cfg || !out) return ob::fail(OB_E_INVALID, "null pointer");
+  *out = nullptr;
+  if (!cfg->outcome || !cfg->group || !cfg->reference_group) return ob::fail(OB_E_INVALID, "incomplete config");
+  ob::QdConfig c;
+  c.outcome = cfg->outcome;
+  c.group = cfg->group;
+  c.reference_group = cfg->reference_group;
+  for (int i = 0; i < cfg->n_predictors; ++i) c.predictors.emplace_back(cfg->predictors[i]);
+  for (int i = 0; i < cfg->n_categorical; ++i) c.categorical.emplace_back(cfg->categorical[i]);
+  if (cfg->quantiles && cfg->n_quantiles > 0)
+    c.quantiles.assign(cfg->quantiles, cfg->quantiles + cfg->n_quantiles);
+  else
+    c.quantiles = {0.1, 0.25, 0.5, 0.75, 0.9};  // :56
+  c.sims = cfg->simulations;
+  c.reps = cfg->bootstrap_reps;
+  c.has_seed = cfg->has_seed != 0;
+  c.seed = cfg->seed;
+  ob::Frame f;
+  OB_TRY(ob::load_frame(cols, n_cols, n_rows, f));
+  return ob::qd_run(ctx, f, c, out);
+}
+
+int ob_qd_results_dims(const ob_qd_results* r, int32_t* n_entries, int64_t* n_a, int64_t* n_b) {
+  if (!r) return ob::fail(OB_E_INVALID, "null pointer");
+  if (n_entries) *n_entries = (int32_t)r->keys.size();
+  if (n_a) *n_a = r->n_a;
+  if (n_b) *n_b = r->n_b;
+  return OB_OK;
+}
+
+int ob_qd_results_get(const ob_qd_results* r, int32_t i, const char** key, ob_component* comps) {
+  if (!r || i < 0 || i >= (int32_t)r->keys.size()) return ob::fail(OB_E_INVALID, "entry index out of range");
+  if (key) *key = r->keys[i].c_str();
+  if (comps)
+    for (int k = 0; k < 3; ++k) {
+      const auto& c = r->comps[i][k];
+      comps[k] = {c.name.c_str(), c.estimate, c.std_err, c.t_stat, c.p_value, c.ci_lower, c.ci_upper};
+    }
+  return OB_OK;
+}
+
+int64_t ob_qd_results_n_failed(const ob_qd_results* r) { return r ? r->n_failed : 0; }
+
+void ob_qd_results_free(ob_qd_results* r) { delete r; }
+
+}  // extern "C"
 
 extern "C" {
 

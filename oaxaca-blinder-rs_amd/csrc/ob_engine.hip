@@ -1079,6 +1079,42 @@ int engine_point_estimate(ob_panel* p, int ref_mode, double* row, double* resid_
   return rc;
 }
 
+// OBRS-1 resample counts for replicates [first_rep, first_rep + n_reps) without the Gram: level-1
+// tile counts into d_m1 ([tile][rep_pad]) and the level-2 count images into d_counts (the
+// ob_engine.hpp layout, replicate batches of 64). Used by the Machado-Mata driver (ob_mm.hip).
+int engine_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_reps, hipStream_t s,
+                  uint32_t* nb_rep, uint32_t* rep_pad) {
+  HIP_OK(hipSetDevice(p->ctx->device));
+  if (n_reps == 0) return OB_OK;
+  if (first_rep + n_reps > 0xFFFFFFFFull)
+    return ob::fail(OB_E_INVALID, "replicate ids must stay below 2^32 - 1 (OBRS-1 / MM-1 counter word)");
+  const uint32_t tiles = p->ntiles[0] + p->ntiles[1];
+  Plan pl = make_plan(p, n_reps, false);
+  OB_TRY(ensure_buf(&p->d_m1, p->cap_m1, (size_t)tiles * pl.rep_pad));
+  OB_TRY(ensure_buf(&p->d_counts, p->cap_counts, (size_t)tiles * pl.nb_rep * 4 * kCimgWords));
+  HIP_OK(hipMemsetAsync(p->d_flags, 0, sizeof(uint32_t), s));
+  const uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
+  const size_t lds_l1 = sizeof(uint32_t) * std::max(p->ntiles[0], p->ntiles[1]);
+  HIP_OK(hipFuncSetAttribute((const void*)ob_level1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_l1));
+  hipLaunchKernelGGL(ob_level1_kernel, dim3(n_reps, 2), dim3(kBlock), lds_l1, s, p->n[0], p->n[1], p->ntiles[0],
+                     (uint32_t)first_rep, pl.rep_pad, key0, key1, p->d_m1);
+  HIP_OK(hipGetLastError());
+  GramArgs ga = gram_args(p, pl);
+  ga.m1 = p->d_m1;
+  ga.n_reps = n_reps;
+  ga.first_rep = (uint32_t)first_rep;
+  ga.key0 = key0;
+  ga.key1 = key1;
+  ga.counts = p->d_counts;
+  ga.tiles_total = tiles;
+  hipLaunchKernelGGL(ob_count_kernel, dim3((tiles + kCntTilesPerBlock - 1) / kCntTilesPerBlock, pl.nb_rep),
+                     dim3(kBlock), 0, s, ga);
+  HIP_OK(hipGetLastError());
+  *nb_rep = pl.nb_rep;
+  *rep_pad = pl.rep_pad;
+  return OB_OK;
+}
+
 int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps, int ref_mode, double* d_rows,
                 uint8_t* d_ok, hipStream_t stream) {
   ob_ctx* ctx = p->ctx;

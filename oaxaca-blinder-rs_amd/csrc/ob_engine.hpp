@@ -77,4 +77,6 @@ int engine_point_estimate(ob_panel* p, int ref_mode, double* row, double* resid_
 int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps, int ref_mode,
                 double* d_rows, uint8_t* d_ok, hipStream_t stream);
 int engine_collect(ob_panel* p);
+int engine_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_reps, hipStream_t s,
+                  uint32_t* nb_rep, uint32_t* rep_pad);
 }  // namespace ob

@@ -1,0 +1,824 @@
+// ob_mm.hip -- Machado-Mata on the GPU (QuantileDecompositionBuilder, quantile_decomposition.rs:21-445).
+//
+// A pass (run_single_pass, :173-279) solves `simulations` quantile regressions per group at the
+// MM-1 quantiles (csrc/ob_spec.h), draws one row per group per successful simulation, and takes
+// empirical quantiles of the three predictions. The reference solves each QR as a sparse LP with
+// Clarabel (math/quantile_regression.rs:22-129); here every fit of a replicate runs at once as a
+// Mehrotra predictor-corrector interior-point method on the bounded dual LP
+//     max y'x  s.t.  X'x = (1 - tau) X'c,  0 <= x <= c        (c = the replicate's row counts)
+// whose equality multipliers are the QR coefficients beta (tools/qr_ipm_proto.py is the numpy
+// statement of the same iteration). The start is primal and dual feasible (x = (1 - tau) c, beta =
+// weighted OLS, z - w = X beta - y), so every iteration only drives the complementarity gap.
+//
+// Layout: lane = fit (64 quantiles of one replicate and group per wave), so a row's design values
+// are wave-uniform (scalar loads) and the per-(fit, row) state [row][fit] is read coalesced.
+// Per iteration, three passes over the rows, each writing per-(chunk, fit) partials that are
+// reduced in a fixed chunk order (bitwise reproducible), and one-wave-per-fit solves:
+//   mm_assemble<K>   (apply the last step,) M = X'QX, X'Q r, gap, objective
+//   mm_affine<K>     affine direction: step-length bounds, mu_aff terms, corrector right-hand sides
+//   mm_final<K>      corrector direction, step-length bounds; stores the direction
+//   mm_finish        per replicate: successful fits in quantile order, MM-1 row picks (through
+//                    the count images for resamples), predictions, LDS bitonic sorts, quantiles
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "ob_device.hpp"
+#include "ob_engine.hpp"
+#include "ob_mm.hpp"
+#include "ob_spec.h"
+
+namespace {
+
+constexpr double kEta = 0.99995;  // fraction of the distance to the boundary per step
+constexpr double kTol = 1e-12;    // relative duality gap at convergence
+constexpr uint32_t kDone = 1u, kFailed = 2u;
+constexpr uint32_t kRc = 2048;  // rows per chunk (a function of the panel only: determinism)
+
+enum { FS_TAU, FS_GAP, FS_OBJ, FS_MU, FS_SIGMU, FS_AP, FS_AD, FS_NACT, FS_DELTA, kFs };
+
+#define MM_OK(expr)                                                                      \
+  do {                                                                                   \
+    hipError_t e_ = (expr);                                                              \
+    if (e_ != hipSuccess)                                                                \
+      return ob::fail(OB_E_HIP, "HIP error %s at %s:%d", hipGetErrorString(e_), __FILE__, \
+                      __LINE__);                                                         \
+  } while (0)
+
+struct MmArgs {
+  const double* cols[2];  // [col][ld]: x_1..x_p, y (intercept implicit)
+  int64_t ld[2];
+  uint32_t n[2];
+  uint32_t tiles0;
+  int p;
+  int S, S_pad;
+  uint32_t n_rb;           // replicates in this batch
+  uint32_t rep0;           // MM-1 replicate id of slot 0 (OB_MM_POINT_REP: every row once)
+  uint32_t seg0;           // slot 0's position in the count-image segment
+  const uint32_t* counts;  // level-2 count images (ob_engine.hpp layout); null for the point
+  const uint32_t* m1;      // level-1 tile counts [tile][rep_pad]
+  uint32_t nb_rep, rep_pad;
+  uint32_t nch[2];
+  size_t rep_rows;         // n0 + n1: state rows per replicate
+  double *x, *z, *w, *dx, *dz, *dw;  // [slot][row (A then B)][S_pad]
+  double *beta, *dba, *db;           // [fit][K]
+  double* L;                         // [fit][K*K]
+  double* fs;                        // [fit][kFs]
+  uint32_t* fstat;                   // [fit]
+  double* partial;                   // [slot][chunk (A then B)][S_pad][nv]
+  double* red;                       // [slot][group][S_pad][nv]
+  uint32_t* active;
+  uint32_t* tprefix;                 // [slot][group][tiles + 1] (finish kernel scratch)
+  uint32_t key0, key1;
+  int n_q;
+  const double* quantiles;
+  double* rows;  // [slot][3 n_q]
+  uint8_t* ok;
+};
+
+__device__ __forceinline__ size_t fit_index(const MmArgs& a, uint32_t slot, uint32_t g, int s) {
+  return ((size_t)slot * 2 + g) * a.S_pad + s;
+}
+
+// Count of `row` of group g in replicate slot `slot` (1 for the point estimate).
+__device__ __forceinline__ uint32_t row_count(const MmArgs& a, uint32_t slot, uint32_t g, uint32_t row) {
+  if (!a.counts) return 1u;
+  const uint32_t pos = a.seg0 + slot;
+  const size_t tt = (g ? a.tiles0 : 0u) + (row >> 8);
+  const uint32_t word =
+      a.counts[((tt * a.nb_rep + (pos >> 6)) * 4 + ((row & 255u) >> 6)) * kCimgWords + (pos & 63u) * kCimgStride +
+               ((row & 63u) >> 2)];
+  return (word >> ((row & 3u) * 8u)) & 255u;
+}
+
+struct Work {
+  uint32_t g, ch, gch, slot;
+  int s, lane;
+};
+
+__device__ __forceinline__ Work work(const MmArgs& a) {
+  Work w;
+  w.lane = threadIdx.x;
+  w.gch = blockIdx.x;
+  w.g = w.gch >= a.nch[0] ? 1u : 0u;
+  w.ch = w.gch - (w.g ? a.nch[0] : 0u);
+  w.slot = blockIdx.z;
+  w.s = blockIdx.y * 64 + w.lane;
+  return w;
+}
+
+__device__ __forceinline__ double* partial_row(const MmArgs& a, const Work& w, int nv) {
+  return a.partial + (((size_t)w.slot * (a.nch[0] + a.nch[1]) + w.gch) * a.S_pad + w.s) * nv;
+}
+
+// mode 0: weighted OLS of the replicate (q = c, rho = y; lane 0 only) -> M, X'Cy, sum c y^2, n_act
+// mode 1: start point (x = (1 - tau) c, z/w from the OLS residual) + assemble
+// mode 2: apply the last step (x += ap dx, z += ad dz, w += ad dw) + assemble
+template <int K>
+__global__ __launch_bounds__(64) void mm_assemble_kernel(const MmArgs a, int mode) {
+  constexpr int NP = K * (K + 1) / 2, NV = NP + K + 2;
+  const Work wk = work(a);
+  const size_t F = fit_index(a, wk.slot, wk.g, wk.s);
+  const uint32_t st = wk.s < a.S ? a.fstat[F] : kDone;
+  const bool live = mode == 0 ? wk.lane == 0 : !(st & (kDone | kFailed));
+  double beta[K];
+  double tau = 0.0, ap = 0.0, ad = 0.0, delta = 0.0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) beta[k] = (live && mode) ? a.beta[F * K + k] : 0.0;
+  if (live && mode) {
+    tau = a.fs[F * kFs + FS_TAU];
+    ap = a.fs[F * kFs + FS_AP];
+    ad = a.fs[F * kFs + FS_AD];
+    delta = a.fs[F * kFs + FS_DELTA];
+  }
+  double acc[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) acc[i] = 0.0;
+  const double* X = a.cols[wk.g];
+  const int64_t ld = a.ld[wk.g];
+  const uint32_t n = a.n[wk.g];
+  const size_t sb = ((size_t)wk.slot * a.rep_rows + (wk.g ? a.n[0] : 0u)) * a.S_pad + wk.s;
+  const uint32_t r0 = wk.ch * kRc, r1 = min(n, r0 + kRc);
+  if (__any(live))
+    for (uint32_t row = r0; row < r1; ++row) {
+      const uint32_t cu = row_count(a, wk.slot, wk.g, row);
+      if (cu == 0) continue;
+      double xr[K];
+      xr[0] = 1.0;
+#pragma unroll
+      for (int k = 1; k < K; ++k) xr[k] = X[(size_t)(k - 1) * ld + row];
+      const double y = X[(size_t)a.p * ld + row];
+      if (!live) continue;
+      const double c = (double)cu;
+      double q, rho;
+      if (mode == 0) {
+        q = c;
+        rho = y;
+        acc[NP + K] += c * y * y;
+        acc[NP + K + 1] += 1.0;
+      } else {
+        const size_t si = sb + (size_t)row * a.S_pad;
+        double xb = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) xb += xr[k] * beta[k];
+        const double r = y - xb;
+        double xv, zv, wv;
+        if (mode == 1) {
+          xv = (1.0 - tau) * c;
+          zv = fmax(-r, 0.0) + delta;
+          wv = fmax(r, 0.0) + delta;
+        } else {
+          xv = a.x[si] + ap * a.dx[si];
+          zv = a.z[si] + ad * a.dz[si];
+          wv = a.w[si] + ad * a.dw[si];
+        }
+        a.x[si] = xv;
+        a.z[si] = zv;
+        a.w[si] = wv;
+        const double sv = c - xv;
+        q = 1.0 / (zv / xv + wv / sv);
+        rho = r;  // rho_aff = r_d + w - z = y - X beta
+        acc[NP + K] += xv * zv + sv * wv;
+        acc[NP + K + 1] += y * xv;
+      }
+      int e = 0;
+#pragma unroll
+      for (int i = 0; i < K; ++i) {
+        const double t = q * xr[i];
+#pragma unroll
+        for (int j = i; j < K; ++j) acc[e++] += t * xr[j];
+      }
+      const double qr = q * rho;
+#pragma unroll
+      for (int k = 0; k < K; ++k) acc[NP + k] += qr * xr[k];
+    }
+  double* P = partial_row(a, wk, NV);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) P[i] = acc[i];
+}
+
+// Per-row affine direction from the current state (shared by mm_affine / mm_final).
+struct Affine {
+  double xv, zv, wv, sv, q, r, dxa, dza, dwa;
+};
+
+template <int K>
+__device__ __forceinline__ Affine affine_row(const MmArgs& a, size_t si, double c, const double (&xr)[K], double y,
+                                             const double (&beta)[K], const double (&dba)[K]) {
+  Affine f;
+  f.xv = a.x[si];
+  f.zv = a.z[si];
+  f.wv = a.w[si];
+  f.sv = c - f.xv;
+  double xb = 0.0, xd = 0.0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    xb += xr[k] * beta[k];
+    xd += xr[k] * dba[k];
+  }
+  f.r = y - xb;
+  f.q = 1.0 / (f.zv / f.xv + f.wv / f.sv);
+  f.dxa = f.q * (f.r - xd);
+  f.dza = -f.zv - f.zv * f.dxa / f.xv;
+  f.dwa = -f.wv + f.wv * f.dxa / f.sv;
+  return f;
+}
+
+// [0] primal step bound, [1] dual step bound, [2..4] mu_aff terms, then X'q rho0, X'q rho1.
+template <int K>
+__global__ __launch_bounds__(64) void mm_affine_kernel(const MmArgs a) {
+  constexpr int NV = 5 + 2 * K;
+  const Work wk = work(a);
+  const size_t F = fit_index(a, wk.slot, wk.g, wk.s);
+  const bool live = wk.s < a.S && !(a.fstat[F] & (kDone | kFailed));
+  double beta[K], dba[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    beta[k] = live ? a.beta[F * K + k] : 0.0;
+    dba[k] = live ? a.dba[F * K + k] : 0.0;
+  }
+  double acc[NV];
+  acc[0] = acc[1] = 1e300;
+#pragma unroll
+  for (int i = 2; i < NV; ++i) acc[i] = 0.0;
+  const double* X = a.cols[wk.g];
+  const int64_t ld = a.ld[wk.g];
+  const uint32_t n = a.n[wk.g];
+  const size_t sb = ((size_t)wk.slot * a.rep_rows + (wk.g ? a.n[0] : 0u)) * a.S_pad + wk.s;
+  const uint32_t r0 = wk.ch * kRc, r1 = min(n, r0 + kRc);
+  if (__any(live))
+    for (uint32_t row = r0; row < r1; ++row) {
+      const uint32_t cu = row_count(a, wk.slot, wk.g, row);
+      if (cu == 0) continue;
+      double xr[K];
+      xr[0] = 1.0;
+#pragma unroll
+      for (int k = 1; k < K; ++k) xr[k] = X[(size_t)(k - 1) * ld + row];
+      const double y = X[(size_t)a.p * ld + row];
+      if (!live) continue;
+      const Affine f = affine_row<K>(a, sb + (size_t)row * a.S_pad, (double)cu, xr, y, beta, dba);
+      if (f.dxa < 0.0) acc[0] = fmin(acc[0], -f.xv / f.dxa);
+      if (f.dxa > 0.0) acc[0] = fmin(acc[0], f.sv / f.dxa);
+      if (f.dza < 0.0) acc[1] = fmin(acc[1], -f.zv / f.dza);
+      if (f.dwa < 0.0) acc[1] = fmin(acc[1], -f.wv / f.dwa);
+      acc[2] += f.xv * f.dza + f.sv * f.dwa;
+      acc[3] += f.zv * f.dxa - f.wv * f.dxa;
+      acc[4] += f.dxa * f.dza - f.dxa * f.dwa;
+      const double q0 = f.q * (f.r - f.dxa * (f.dwa / f.sv + f.dza / f.xv));
+      const double q1 = f.q * (1.0 / f.xv - 1.0 / f.sv);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        acc[5 + k] += q0 * xr[k];
+        acc[5 + K + k] += q1 * xr[k];
+      }
+    }
+  double* P = partial_row(a, wk, NV);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) P[i] = acc[i];
+}
+
+// Corrector direction (stored for the next assemble) and its step-length bounds.
+template <int K>
+__global__ __launch_bounds__(64) void mm_final_kernel(const MmArgs a) {
+  const Work wk = work(a);
+  const size_t F = fit_index(a, wk.slot, wk.g, wk.s);
+  const bool live = wk.s < a.S && !(a.fstat[F] & (kDone | kFailed));
+  double beta[K], dba[K], db[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    beta[k] = live ? a.beta[F * K + k] : 0.0;
+    dba[k] = live ? a.dba[F * K + k] : 0.0;
+    db[k] = live ? a.db[F * K + k] : 0.0;
+  }
+  const double sigmu = live ? a.fs[F * kFs + FS_SIGMU] : 0.0;
+  double bp = 1e300, bd = 1e300;
+  const double* X = a.cols[wk.g];
+  const int64_t ld = a.ld[wk.g];
+  const uint32_t n = a.n[wk.g];
+  const size_t sb = ((size_t)wk.slot * a.rep_rows + (wk.g ? a.n[0] : 0u)) * a.S_pad + wk.s;
+  const uint32_t r0 = wk.ch * kRc, r1 = min(n, r0 + kRc);
+  if (__any(live))
+    for (uint32_t row = r0; row < r1; ++row) {
+      const uint32_t cu = row_count(a, wk.slot, wk.g, row);
+      if (cu == 0) continue;
+      double xr[K];
+      xr[0] = 1.0;
+#pragma unroll
+      for (int k = 1; k < K; ++k) xr[k] = X[(size_t)(k - 1) * ld + row];
+      const double y = X[(size_t)a.p * ld + row];
+      if (!live) continue;
+      const size_t si = sb + (size_t)row * a.S_pad;
+      const Affine f = affine_row<K>(a, si, (double)cu, xr, y, beta, dba);
+      const double rho = f.r - f.dxa * (f.dwa / f.sv + f.dza / f.xv) + sigmu * (1.0 / f.xv - 1.0 / f.sv);
+      double xd = 0.0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) xd += xr[k] * db[k];
+      const double dx = f.q * (rho - xd);
+      const double rxz = sigmu - f.xv * f.zv - f.dxa * f.dza;
+      const double rsw = sigmu - f.sv * f.wv + f.dxa * f.dwa;
+      const double dz = (rxz - f.zv * dx) / f.xv;
+      const double dw = (rsw + f.wv * dx) / f.sv;
+      a.dx[si] = dx;
+      a.dz[si] = dz;
+      a.dw[si] = dw;
+      if (dx < 0.0) bp = fmin(bp, -f.xv / dx);
+      if (dx > 0.0) bp = fmin(bp, f.sv / dx);
+      if (dz < 0.0) bd = fmin(bd, -f.zv / dz);
+      if (dw < 0.0) bd = fmin(bd, -f.wv / dw);
+    }
+  double* P = partial_row(a, wk, 2);
+  P[0] = bp;
+  P[1] = bd;
+}
+
+// Chunk partials -> per-fit values, chunks in a fixed order; the first n_min values are minima.
+__global__ __launch_bounds__(256) void mm_reduce_kernel(const MmArgs a, int nv, int n_min) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t per_slot = (size_t)2 * a.S_pad * nv;
+  if (i >= (size_t)a.n_rb * per_slot) return;
+  const uint32_t slot = (uint32_t)(i / per_slot);
+  const size_t rem = i % per_slot;
+  const uint32_t g = (uint32_t)(rem / ((size_t)a.S_pad * nv));
+  const size_t sv = rem % ((size_t)a.S_pad * nv);
+  const uint32_t c0 = g ? a.nch[0] : 0u, nc = a.nch[g];
+  const size_t stride = (size_t)a.S_pad * nv;
+  const double* P = a.partial + ((size_t)slot * (a.nch[0] + a.nch[1]) + c0) * stride + sv;
+  const bool is_min = (int)(sv % nv) < n_min;
+  double v = is_min ? 1e300 : 0.0;
+  for (uint32_t c = 0; c < nc; ++c) v = is_min ? fmin(v, P[c * stride]) : v + P[c * stride];
+  a.red[((size_t)slot * 2 + g) * stride + sv] = v;
+}
+
+// Weighted OLS of each (slot, group) -> the start of all its fits (wave per (slot, group)).
+__global__ __launch_bounds__(64) void mm_start_kernel(const MmArgs a, int K) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int lane = threadIdx.x;
+  const uint32_t slot = blockIdx.x >> 1, g = blockIdx.x & 1;
+  const int NP = K * (K + 1) / 2, NV = NP + K + 2;
+  const double* R = a.red + (((size_t)slot * 2 + g) * a.S_pad) * NV;  // fit 0 holds the sums
+  double* M = sm;
+  double* v = sm + K * K;
+  for (int i = lane; i < K * K; i += 64) {
+    const int r = i % K, c = i / K;
+    M[i] = R[r <= c ? ob_pair_index(r, c, K) : ob_pair_index(c, r, K)];
+  }
+  for (int i = lane; i < K; i += 64) v[i] = R[NP + i];
+  __syncthreads();
+  const bool chol = wave_cholesky(M, K, lane);
+  if (chol) wave_chol_solve(M, K, v, lane);
+  __syncthreads();
+  double delta = 0.0;
+  if (chol) {
+    double bv = 0.0;
+    for (int k = 0; k < K; ++k) bv += v[k] * R[NP + k];
+    const double ssr = fmax(R[NP + K] - bv, 0.0), sc = R[0];
+    delta = 1e-3 * (1.0 + sqrt(ssr / sc));
+  }
+  const uint32_t rep = a.rep0 == OB_MM_POINT_REP ? OB_MM_POINT_REP : a.rep0 + slot;
+  for (int s = lane; s < a.S_pad; s += 64) {
+    const size_t F = ((size_t)slot * 2 + g) * a.S_pad + s;
+    if (s >= a.S) {
+      a.fstat[F] = kDone | kFailed;
+      continue;
+    }
+    a.fstat[F] = chol ? 0u : kFailed;
+    for (int k = 0; k < K; ++k) a.beta[F * K + k] = chol ? v[k] : 0.0;
+    double* f = a.fs + F * kFs;
+    f[FS_TAU] = ob_mm_tau((uint32_t)s, rep, a.key0, a.key1);
+    f[FS_DELTA] = delta;
+    f[FS_NACT] = R[NP + K + 1];
+    f[FS_AP] = f[FS_AD] = 0.0;
+  }
+}
+
+// Convergence test, Cholesky of M, affine direction (wave per fit).
+__global__ __launch_bounds__(64) void mm_solve_affine_kernel(const MmArgs a, int K) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int lane = threadIdx.x;
+  const size_t F = blockIdx.x;
+  if (a.fstat[F] & (kDone | kFailed)) return;
+  const int NP = K * (K + 1) / 2, NV = NP + K + 2;
+  const double* R = a.red + F * NV;
+  double* f = a.fs + F * kFs;
+  const double gap = R[NP + K], obj = R[NP + K + 1];
+  if (lane == 0) {
+    f[FS_GAP] = gap;
+    f[FS_OBJ] = obj;
+  }
+  if (gap < kTol * (1.0 + fabs(obj))) {  // converged: beta is the QR solution
+    if (lane == 0) a.fstat[F] = kDone;
+    return;
+  }
+  double* M = sm;
+  double* v = sm + K * K;
+  for (int i = lane; i < K * K; i += 64) {
+    const int r = i % K, c = i / K;
+    M[i] = R[r <= c ? ob_pair_index(r, c, K) : ob_pair_index(c, r, K)];
+  }
+  for (int i = lane; i < K; i += 64) v[i] = R[NP + i];
+  __syncthreads();
+  if (!wave_cholesky(M, K, lane)) {  // the normal matrix lost rank: accept a near-optimal point
+    if (lane == 0) a.fstat[F] = gap < 1e-9 * (1.0 + fabs(obj)) ? kDone : (kDone | kFailed);
+    return;
+  }
+  wave_chol_solve(M, K, v, lane);
+  for (int i = lane; i < K * K; i += 64) a.L[F * K * K + i] = M[i];
+  for (int i = lane; i < K; i += 64) a.dba[F * K + i] = v[i];
+  if (lane == 0) {
+    f[FS_MU] = gap / (2.0 * f[FS_NACT]);
+    atomicAdd(a.active, 1u);
+  }
+}
+
+// sigma from the affine step, corrector direction (wave per fit).
+__global__ __launch_bounds__(64) void mm_solve_corrector_kernel(const MmArgs a, int K) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int lane = threadIdx.x;
+  const size_t F = blockIdx.x;
+  if (a.fstat[F] & (kDone | kFailed)) return;
+  const int NV = 5 + 2 * K;
+  const double* R = a.red + F * NV;
+  double* f = a.fs + F * kFs;
+  const double ap = fmin(1.0, R[0]), ad = fmin(1.0, R[1]);
+  const double n2 = 2.0 * f[FS_NACT];
+  const double mu_aff = (f[FS_GAP] + ad * R[2] + ap * R[3] + ap * ad * R[4]) / n2;
+  const double mu = f[FS_MU];
+  const double ratio = mu_aff / mu;
+  const double sigmu = ratio * ratio * ratio * mu;
+  double* Lm = sm;
+  double* v = sm + K * K;
+  for (int i = lane; i < K * K; i += 64) Lm[i] = a.L[F * K * K + i];
+  for (int i = lane; i < K; i += 64) v[i] = R[5 + i] + sigmu * R[5 + K + i];
+  __syncthreads();
+  wave_chol_solve(Lm, K, v, lane);
+  for (int i = lane; i < K; i += 64) a.db[F * K + i] = v[i];
+  if (lane == 0) f[FS_SIGMU] = sigmu;
+}
+
+// Step lengths and the dual update of beta (thread per fit).
+__global__ __launch_bounds__(256) void mm_step_kernel(const MmArgs a, int K, size_t n_fits) {
+  const size_t F = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (F >= n_fits || (a.fstat[F] & (kDone | kFailed))) return;
+  const double* R = a.red + F * 2;
+  const double ap = fmin(1.0, kEta * R[0]), ad = fmin(1.0, kEta * R[1]);
+  for (int k = 0; k < K; ++k) a.beta[F * K + k] += ad * a.db[F * K + k];
+  a.fs[F * kFs + FS_AP] = ap;
+  a.fs[F * kFs + FS_AD] = ad;
+}
+
+__global__ __launch_bounds__(256) void mm_expire_kernel(const MmArgs a, size_t n_fits) {
+  const size_t F = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (F < n_fits && !(a.fstat[F] & (kDone | kFailed))) a.fstat[F] = kDone | kFailed;  // no convergence
+}
+
+// In-place ascending bitonic sort of v[0, m) (m a power of two) by the block.
+__device__ void block_sort(double* v, int m) {
+  for (int k = 2; k <= m; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < m; i += blockDim.x) {
+        const int l = i ^ j;
+        if (l > i) {
+          const bool up = (i & k) == 0;
+          const double x = v[i], y = v[l];
+          if ((x > y) == up) {
+            v[i] = y;
+            v[l] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+}
+
+// Sample position -> row of group g in replicate slot (rows in order, each repeated by count).
+__device__ uint32_t position_row(const MmArgs& a, uint32_t slot, uint32_t g, uint32_t j, const uint32_t* pre,
+                                 uint32_t ntiles) {
+  if (!a.counts) return j;
+  uint32_t lo = 0, hi = ntiles;  // last tile t with pre[t] <= j
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (pre[mid] <= j)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  uint32_t rem = j - pre[lo];
+  const uint32_t base = lo * OB_TILE_ROWS, rows = min(OB_TILE_ROWS, a.n[g] - base);
+  for (uint32_t r = 0; r < rows; ++r) {
+    const uint32_t c = row_count(a, slot, g, base + r);
+    if (rem < c) return base + r;
+    rem -= c;
+  }
+  return base + rows - 1;  // unreachable when the counts are consistent
+}
+
+// One block per replicate slot: run_single_pass (quantile_decomposition.rs:221-279) after the fits.
+__global__ __launch_bounds__(256) void mm_finish_kernel(const MmArgs a, int K, int m2) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* yaa = sm;
+  double* ybb = yaa + m2;
+  double* yab = ybb + m2;
+  uint16_t* ia = reinterpret_cast<uint16_t*>(yab + m2);
+  uint16_t* ib = ia + m2;
+  __shared__ uint32_t cnt[2];
+  const uint32_t slot = blockIdx.x;
+  const uint32_t rep = a.rep0 == OB_MM_POINT_REP ? OB_MM_POINT_REP : a.rep0 + slot;
+  double* row = a.rows + (size_t)slot * 3 * a.n_q;
+  if (threadIdx.x < 2) {  // successful fits in simulation order (filter_map, :221-229)
+    const uint32_t g = threadIdx.x;
+    uint16_t* idx = g ? ib : ia;
+    uint32_t k = 0;
+    for (int s = 0; s < a.S; ++s)
+      if (a.fstat[fit_index(a, slot, g, s)] == kDone) idx[k++] = (uint16_t)s;
+    cnt[g] = k;
+  }
+  // exclusive tile prefixes of the replicate's level-1 counts (both groups)
+  const uint32_t nt[2] = {(a.n[0] + OB_TILE_ROWS - 1) / OB_TILE_ROWS, (a.n[1] + OB_TILE_ROWS - 1) / OB_TILE_ROWS};
+  uint32_t* pre[2] = {a.tprefix + ((size_t)slot * 2) * (a.tiles0 + 1 + nt[1] + 1),
+                      a.tprefix + ((size_t)slot * 2) * (a.tiles0 + 1 + nt[1] + 1) + nt[0] + 1};
+  if (a.counts && threadIdx.x < 2) {
+    const uint32_t g = threadIdx.x, pos = a.seg0 + slot;
+    uint32_t s = 0;
+    for (uint32_t t = 0; t < nt[g]; ++t) {
+      pre[g][t] = s;
+      s += a.m1[(size_t)((g ? a.tiles0 : 0u) + t) * a.rep_pad + pos];
+    }
+    pre[g][nt[g]] = s;
+  }
+  __syncthreads();
+  const uint32_t na = cnt[0], nb = cnt[1];
+  if ((int)na < a.S / 2 || (int)nb < a.S / 2) {  // :231-236
+    if (threadIdx.x == 0) {
+      a.ok[slot] = 0;
+      for (int i = 0; i < 3 * a.n_q; ++i) row[i] = __builtin_nan("");
+    }
+    return;
+  }
+  const uint32_t num = min(na, nb);
+  const double* XA = a.cols[0];
+  const double* XB = a.cols[1];
+  for (uint32_t i = threadIdx.x; i < (uint32_t)m2; i += blockDim.x) {
+    if (i >= num) {
+      yaa[i] = ybb[i] = yab[i] = INFINITY;
+      continue;
+    }
+    const uint32_t ra = position_row(a, slot, 0, ob_mm_pick(i, rep, 0, a.n[0], a.key0, a.key1), pre[0], nt[0]);
+    const uint32_t rb = position_row(a, slot, 1, ob_mm_pick(i, rep, 1, a.n[1], a.key0, a.key1), pre[1], nt[1]);
+    const double* ba = a.beta + fit_index(a, slot, 0, ia[i]) * K;
+    const double* bb = a.beta + fit_index(a, slot, 1, ib[i]) * K;
+    double vaa = ba[0], vbb = bb[0], vab = bb[0];  // x_i . beta with x_0 = 1 (:249-255)
+    for (int k = 1; k < K; ++k) {
+      const double xa = XA[(size_t)(k - 1) * a.ld[0] + ra], xb = XB[(size_t)(k - 1) * a.ld[1] + rb];
+      vaa += xa * ba[k];
+      vbb += xb * bb[k];
+      vab += xa * bb[k];
+    }
+    yaa[i] = vaa;
+    ybb[i] = vbb;
+    yab[i] = vab;
+  }
+  __syncthreads();
+  block_sort(yaa, m2);
+  block_sort(ybb, m2);
+  block_sort(yab, m2);
+  if (threadIdx.x == 0) {  // empirical_quantile (:164-171) per target quantile
+    for (int j = 0; j < a.n_q; ++j) {
+      const uint32_t k = min((uint32_t)((double)num * a.quantiles[j]), num - 1);
+      row[3 * j + 0] = yaa[k] - ybb[k];
+      row[3 * j + 1] = yab[k] - ybb[k];
+      row[3 * j + 2] = yaa[k] - yab[k];
+    }
+    a.ok[slot] = 1;
+  }
+}
+
+template <int K>
+struct Kernels {
+  static void assemble(const MmArgs& a, dim3 grid, int mode, hipStream_t s) {
+    hipLaunchKernelGGL(mm_assemble_kernel<K>, grid, dim3(64), 0, s, a, mode);
+  }
+  static void affine(const MmArgs& a, dim3 grid, hipStream_t s) {
+    hipLaunchKernelGGL(mm_affine_kernel<K>, grid, dim3(64), 0, s, a);
+  }
+  static void final_(const MmArgs& a, dim3 grid, hipStream_t s) {
+    hipLaunchKernelGGL(mm_final_kernel<K>, grid, dim3(64), 0, s, a);
+  }
+};
+
+template <int K>
+void launch_pass(int which, const MmArgs& a, dim3 grid, int mode, hipStream_t s) {
+  if (which == 0)
+    Kernels<K>::assemble(a, grid, mode, s);
+  else if (which == 1)
+    Kernels<K>::affine(a, grid, s);
+  else
+    Kernels<K>::final_(a, grid, s);
+}
+
+void pass(int K, int which, const MmArgs& a, dim3 grid, int mode, hipStream_t s) {
+  switch (K) {
+#define OB_MM_K(k) \
+  case k: launch_pass<k>(which, a, grid, mode, s); break;
+    OB_MM_K(1) OB_MM_K(2) OB_MM_K(3) OB_MM_K(4) OB_MM_K(5) OB_MM_K(6) OB_MM_K(7) OB_MM_K(8)
+    OB_MM_K(9) OB_MM_K(10) OB_MM_K(11) OB_MM_K(12) OB_MM_K(13) OB_MM_K(14) OB_MM_K(15) OB_MM_K(16)
+#undef OB_MM_K
+    default: break;
+  }
+}
+
+struct Buffers {
+  double *x = nullptr, *z = nullptr, *w = nullptr, *dx = nullptr, *dz = nullptr, *dw = nullptr;
+  double *beta = nullptr, *dba = nullptr, *db = nullptr, *L = nullptr, *fs = nullptr;
+  double *partial = nullptr, *red = nullptr, *quant = nullptr, *rows = nullptr;
+  uint32_t *fstat = nullptr, *active = nullptr, *tprefix = nullptr;
+  uint8_t* ok = nullptr;
+  ~Buffers() {
+    for (void* p : {(void*)x, (void*)z, (void*)w, (void*)dx, (void*)dz, (void*)dw, (void*)beta, (void*)dba, (void*)db,
+                    (void*)L, (void*)fs, (void*)partial, (void*)red, (void*)quant, (void*)rows, (void*)fstat,
+                    (void*)active, (void*)tprefix, (void*)ok})
+      (void)hipFree(p);
+  }
+};
+
+// One batch of replicate slots: start, IPM iterations, finish. Rows/ok -> host.
+int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, int* iters) {
+  const uint32_t nch = a.nch[0] + a.nch[1];
+  const int NP = K * (K + 1) / 2;
+  const int nv1 = NP + K + 2, nv2 = 5 + 2 * K;
+  const size_t n_fits = (size_t)a.n_rb * 2 * a.S_pad;
+  const dim3 grid(nch, a.S_pad / 64, a.n_rb);
+  auto reduce = [&](int nv, int n_min) -> hipError_t {
+    const size_t tot = n_fits * nv;
+    hipLaunchKernelGGL(mm_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, a, nv, n_min);
+    return hipGetLastError();
+  };
+  const size_t lds_solve = sizeof(double) * ((size_t)K * K + K);
+  // start: weighted OLS per (slot, group)
+  pass(K, 0, a, dim3(nch, 1, a.n_rb), 0, s);
+  MM_OK(hipGetLastError());
+  MM_OK(reduce(nv1, 0));
+  hipLaunchKernelGGL(mm_start_kernel, dim3(a.n_rb * 2), dim3(64), lds_solve, s, a, K);
+  MM_OK(hipGetLastError());
+  int it = 0;
+  for (it = 1; it <= ob::kMmMaxIter; ++it) {
+    pass(K, 0, a, grid, it == 1 ? 1 : 2, s);
+    MM_OK(hipGetLastError());
+    MM_OK(reduce(nv1, 0));
+    MM_OK(hipMemsetAsync(a.active, 0, sizeof(uint32_t), s));
+    hipLaunchKernelGGL(mm_solve_affine_kernel, dim3((unsigned)n_fits), dim3(64), lds_solve, s, a, K);
+    MM_OK(hipGetLastError());
+    uint32_t active = 0;
+    MM_OK(hipMemcpyAsync(&active, a.active, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    MM_OK(hipStreamSynchronize(s));
+    if (active == 0) break;
+    pass(K, 1, a, grid, 0, s);
+    MM_OK(hipGetLastError());
+    MM_OK(reduce(nv2, 2));
+    hipLaunchKernelGGL(mm_solve_corrector_kernel, dim3((unsigned)n_fits), dim3(64), lds_solve, s, a, K);
+    MM_OK(hipGetLastError());
+    pass(K, 2, a, grid, 0, s);
+    MM_OK(hipGetLastError());
+    MM_OK(reduce(2, 2));
+    hipLaunchKernelGGL(mm_step_kernel, dim3((unsigned)((n_fits + 255) / 256)), dim3(256), 0, s, a, K, n_fits);
+    MM_OK(hipGetLastError());
+  }
+  hipLaunchKernelGGL(mm_expire_kernel, dim3((unsigned)((n_fits + 255) / 256)), dim3(256), 0, s, a, n_fits);
+  MM_OK(hipGetLastError());
+  int m2 = 1;
+  while (m2 < a.S) m2 <<= 1;
+  const size_t lds_fin = (size_t)m2 * (3 * sizeof(double) + 2 * sizeof(uint16_t));
+  MM_OK(hipFuncSetAttribute((const void*)mm_finish_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fin));
+  hipLaunchKernelGGL(mm_finish_kernel, dim3(a.n_rb), dim3(256), lds_fin, s, a, K, m2);
+  MM_OK(hipGetLastError());
+  MM_OK(hipMemcpyAsync(rows_h, a.rows, sizeof(double) * a.n_rb * 3 * a.n_q, hipMemcpyDeviceToHost, s));
+  MM_OK(hipMemcpyAsync(ok_h, a.ok, a.n_rb, hipMemcpyDeviceToHost, s));
+  MM_OK(hipStreamSynchronize(s));
+  if (iters) *iters = std::max(*iters, std::min(it, ob::kMmMaxIter));
+  return OB_OK;
+}
+
+}  // namespace
+
+namespace ob {
+
+int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_q, uint64_t first_rep,
+           uint64_t n_reps, bool with_point, double* rows, uint8_t* ok, int* max_iters) {
+  ob_ctx* ctx = p->ctx;
+  MM_OK(hipSetDevice(ctx->device));
+  const int K = p->k;
+  if (K > kMmMaxK) return ob::fail(OB_E_UNSUPPORTED, "Machado-Mata takes at most %d columns (intercept included), got %d", kMmMaxK, K);
+  if (p->weighted || p->heckman || p->n_y != 1) return ob::fail(OB_E_INVALID, "Machado-Mata panels are unweighted, one outcome");
+  if (sims < 1 || sims > kMmMaxSims) return ob::fail(OB_E_UNSUPPORTED, "simulations must be in [1, %d]", kMmMaxSims);
+  if (n_q < 1) return ob::fail(OB_E_INVALID, "no target quantiles");
+  if (p->n[0] < 1 || p->n[1] < 1) return ob::fail(OB_E_GROUP, "%sOne group has insufficient data", error_prefix(OB_E_GROUP));
+  if (first_rep + n_reps >= 0xFFFFFFFFull) return ob::fail(OB_E_INVALID, "replicate ids must stay below 2^32 - 1");
+  hipStream_t s = ctx->stream;
+  const int S_pad = (sims + 63) / 64 * 64;
+  const size_t rep_rows = (size_t)p->n[0] + p->n[1];
+  const uint32_t nch0 = (p->n[0] + kRc - 1) / kRc, nch1 = (p->n[1] + kRc - 1) / kRc;
+  // replicate slots per batch: IPM state (6 f64 per fit and row) within 48 GB
+  const size_t state_per_rep = 6 * rep_rows * S_pad * sizeof(double);
+  const uint64_t want = std::max<uint64_t>(n_reps, 1);
+  const uint32_t rb_cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({want, 256, (48ull << 30) / state_per_rep}));
+  const size_t fits = (size_t)rb_cap * 2 * S_pad;
+  const int nv_max = K * (K + 1) / 2 + K + 2 > 5 + 2 * K ? K * (K + 1) / 2 + K + 2 : 5 + 2 * K;
+  Buffers b;
+  const size_t st_elems = (size_t)rb_cap * rep_rows * S_pad;
+  for (double** q : {&b.x, &b.z, &b.w, &b.dx, &b.dz, &b.dw}) MM_OK(hipMalloc(q, sizeof(double) * st_elems));
+  MM_OK(hipMalloc(&b.beta, sizeof(double) * fits * K));
+  MM_OK(hipMalloc(&b.dba, sizeof(double) * fits * K));
+  MM_OK(hipMalloc(&b.db, sizeof(double) * fits * K));
+  MM_OK(hipMalloc(&b.L, sizeof(double) * fits * K * K));
+  MM_OK(hipMalloc(&b.fs, sizeof(double) * fits * kFs));
+  MM_OK(hipMalloc(&b.fstat, sizeof(uint32_t) * fits));
+  MM_OK(hipMalloc(&b.partial, sizeof(double) * (size_t)rb_cap * (nch0 + nch1) * S_pad * nv_max));
+  MM_OK(hipMalloc(&b.red, sizeof(double) * fits * nv_max));
+  MM_OK(hipMalloc(&b.active, sizeof(uint32_t)));
+  MM_OK(hipMalloc(&b.quant, sizeof(double) * n_q));
+  MM_OK(hipMalloc(&b.rows, sizeof(double) * rb_cap * 3 * n_q));
+  MM_OK(hipMalloc(&b.ok, rb_cap));
+  const uint32_t nt1 = (p->n[1] + OB_TILE_ROWS - 1) / OB_TILE_ROWS;
+  MM_OK(hipMalloc(&b.tprefix, sizeof(uint32_t) * rb_cap * 2 * (p->ntiles[0] + 1 + nt1 + 1)));
+  MM_OK(hipMemcpy(b.quant, quantiles, sizeof(double) * n_q, hipMemcpyHostToDevice));
+
+  MmArgs a{};
+  for (int g = 0; g < 2; ++g) {
+    a.cols[g] = p->d_cols[g];
+    a.ld[g] = p->ld[g];
+    a.n[g] = p->n[g];
+  }
+  a.tiles0 = p->ntiles[0];
+  a.p = p->p;
+  a.S = sims;
+  a.S_pad = S_pad;
+  a.nch[0] = nch0;
+  a.nch[1] = nch1;
+  a.rep_rows = rep_rows;
+  a.x = b.x;
+  a.z = b.z;
+  a.w = b.w;
+  a.dx = b.dx;
+  a.dz = b.dz;
+  a.dw = b.dw;
+  a.beta = b.beta;
+  a.dba = b.dba;
+  a.db = b.db;
+  a.L = b.L;
+  a.fs = b.fs;
+  a.fstat = b.fstat;
+  a.partial = b.partial;
+  a.red = b.red;
+  a.active = b.active;
+  a.tprefix = b.tprefix;
+  a.key0 = (uint32_t)seed;
+  a.key1 = (uint32_t)(seed >> 32);
+  a.n_q = n_q;
+  a.quantiles = b.quant;
+  a.rows = b.rows;
+  a.ok = b.ok;
+  if (max_iters) *max_iters = 0;
+  size_t out = 0;
+  if (with_point) {  // every row once, MM-1 replicate OB_MM_POINT_REP
+    MmArgs pa = a;
+    pa.n_rb = 1;
+    pa.rep0 = OB_MM_POINT_REP;
+    pa.counts = nullptr;
+    OB_TRY(run_batch(pa, K, s, rows, ok, max_iters));
+    out = 1;
+  }
+  // resamples: OBRS-1 count images per segment, then batches of rb_cap slots
+  const uint64_t seg_cap = 4096;
+  for (uint64_t s0 = 0; s0 < n_reps; s0 += seg_cap) {
+    const uint32_t ns = (uint32_t)std::min<uint64_t>(seg_cap, n_reps - s0);
+    uint32_t nb_rep = 0, rep_pad = 0;
+    OB_TRY(engine_counts(p, seed, first_rep + s0, ns, s, &nb_rep, &rep_pad));
+    for (uint32_t b0 = 0; b0 < ns; b0 += rb_cap) {
+      MmArgs ba = a;
+      ba.n_rb = std::min(rb_cap, ns - b0);
+      ba.rep0 = (uint32_t)(first_rep + s0 + b0);
+      ba.seg0 = b0;
+      ba.counts = p->d_counts;
+      ba.m1 = p->d_m1;
+      ba.nb_rep = nb_rep;
+      ba.rep_pad = rep_pad;
+      OB_TRY(run_batch(ba, K, s, rows + (out + s0 + b0) * 3 * n_q, ok + out + s0 + b0, max_iters));
+    }
+  }
+  uint32_t flag = 0;
+  MM_OK(hipMemcpy(&flag, p->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (flag) return ob::fail(OB_E_OVERFLOW, "a resampled row was drawn more than 255 times in one replicate");
+  return OB_OK;
+}
+
+}  // namespace ob
+
+extern "C" int ob_mm_run(ob_panel* panel, uint64_t seed, int32_t simulations, const double* quantiles,
+                         int32_t n_quantiles, uint64_t first_rep, uint64_t n_reps, int32_t with_point,
+                         double* rows, uint8_t* ok) {
+  if (!panel || !quantiles || !rows || !ok) return ob::fail(OB_E_INVALID, "null pointer");
+  return ob::mm_run(panel, seed, simulations, quantiles, n_quantiles, first_rep, n_reps, with_point != 0, rows, ok,
+                    nullptr);
+}

@@ -72,3 +72,38 @@ OB_HD int ob_row_len(int k, int n_base) { return 6 + 2 * (k + n_base) + 5 * k; }
 OB_HD int ob_pair_index(int a, int b, int k1) {  // requires a <= b
   return a * k1 - (a * (a - 1)) / 2 + (b - a);
 }
+
+// ---- MM-1: the Machado-Mata draws (quantile_decomposition.rs:215-258) ------------------------
+// The reference draws from an unseeded thread_rng: `simulations` quantiles tau ~ U(0.01, 0.99)
+// shared by both groups, then one random row of X_A and of X_B per successful simulation. MM-1
+// draws the same laws from the counter-based stream, so a pass is a pure function of
+// (seed, replicate id):
+//   tau_s   = 0.01 + 0.98 u, u = (hi27(x) 2^26 + hi26(y)) 2^-53 of Philox({s, rep, 0, MMT1}) (x, y)
+//             words, kept below 0.99;
+//   pick_i  = exact uniform position on [0, n_g): Lemire on word (j & 3) of
+//             Philox({i, rep, g, MMR1 + (j >> 2)}) for attempt j (reject iff low32(w n) < 2^32 mod n).
+// A position of a bootstrap sample maps to the row whose cumulative count first exceeds it (the
+// sample in row order; any fixed order of a uniform position has the same law). The point
+// estimate runs as replicate OB_MM_POINT_REP with every row once.
+#define OB_TAG_MMT 0x4D4D5431u /* "MMT1" */
+#define OB_TAG_MMR 0x4D4D5231u /* "MMR1" */
+#define OB_MM_POINT_REP 0xFFFFFFFFu
+
+OB_HD double ob_mm_tau(uint32_t s, uint32_t rep, uint32_t k0, uint32_t k1) {
+  const ob_u32x4 u = ob_philox(s, rep, 0u, OB_TAG_MMT, k0, k1);
+  const double v = ((double)(u.x >> 5) * 67108864.0 + (double)(u.y >> 6)) * (1.0 / 9007199254740992.0);
+  const double t = 0.01 + 0.98 * v;
+  return t < 0.99 ? t : 0.98999999999999999;
+}
+
+OB_HD uint32_t ob_mm_pick(uint32_t i, uint32_t rep, uint32_t g, uint32_t n, uint32_t k0, uint32_t k1) {
+  const uint32_t thresh = (0u - n) % n;
+  for (uint32_t j = 0;; j += 4) {
+    const ob_u32x4 u = ob_philox(i, rep, g, OB_TAG_MMR + (j >> 2), k0, k1);
+    const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
+    for (int h = 0; h < 4; ++h) {
+      const uint64_t m = (uint64_t)wd[h] * n;
+      if ((uint32_t)m >= thresh) return (uint32_t)(m >> 32);
+    }
+  }
+}

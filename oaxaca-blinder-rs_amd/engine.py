@@ -102,6 +102,17 @@ class Panel:
                                         ok.ctypes.data_as(C.POINTER(C.c_uint8))))
         return (rows[0], ok[0]) if self.n_y == 1 else (rows, ok)
 
+    def mm(self, seed: int, simulations: int, quantiles, first_rep: int = 0, n_reps: int = 0, with_point=True):
+        """Machado-Mata passes (ob_mm_run): rows [gap, characteristics, coefficients] per quantile,
+        the point pass first when ``with_point``; ok = 0 where a pass failed."""
+        q = np.ascontiguousarray(quantiles, dtype=np.float64)
+        m = int(bool(with_point)) + n_reps
+        rows = np.empty((m, 3 * q.size))
+        ok = np.zeros(m, dtype=np.uint8)
+        N.check(N.lib().ob_mm_run(self._h, seed & ((1 << 64) - 1), int(simulations), _dp(q), int(q.size), first_rep,
+                                  n_reps, int(bool(with_point)), _dp(rows), ok.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return rows, ok
+
     def boot_device(self, seed: int, first_rep: int, n_reps: int, rows_ptr: int, ok_ptr: int,
                     ref=ReferenceCoefficients.GroupA, stream: int | None = None):
         N.check(N.lib().ob_boot_run_device(self._h, seed & ((1 << 64) - 1), first_rep, n_reps, int(ref),

@@ -582,6 +582,166 @@ def heckman_row_len(k, ks):
 
 
 # ---------------------------------------------------------------------------------------------
+# Machado-Mata (quantile_decomposition.rs:21-445, math/quantile_regression.rs:22-129)
+# QR is solved exactly with HiGHS (scipy) on the dual LP  max y'a  s.t.  X'a = (1 - tau) X'c,
+# 0 <= a <= c (c = resample counts); the equality multipliers are beta. The reference solves the
+# primal LP with Clarabel's interior-point method (default tolerances ~1e-8); for a unique
+# optimum both give the same beta up to that tolerance (its own tests use 1e-4). The draws follow
+# MM-1 (csrc/ob_spec.h) in place of the reference's unseeded thread_rng.
+# ---------------------------------------------------------------------------------------------
+TAG_MMT, TAG_MMR, MM_POINT_REP = 0x4D4D5431, 0x4D4D5231, 0xFFFFFFFF
+
+
+def mm_tau(seed, rep, s):  # MM-1 tau_s (quantile_decomposition.rs:215-219)
+    x, y, _, _ = philox([s, rep, 0, TAG_MMT], [seed & 0xFFFFFFFF, seed >> 32])
+    t = 0.01 + 0.98 * (((x >> 5) * 67108864.0 + (y >> 6)) * (1.0 / 9007199254740992.0))
+    return t if t < 0.99 else 0.98999999999999999
+
+
+def mm_pick(seed, rep, g, i, n):  # MM-1 position of pick i (quantile_decomposition.rs:246-247)
+    thresh = (2**32 - n) % n
+    j = 0
+    while True:
+        w = philox([i, rep, g, TAG_MMR + (j >> 2)], [seed & 0xFFFFFFFF, seed >> 32])
+        for h in range(4):
+            m = w[h] * n
+            if (m & 0xFFFFFFFF) >= thresh:
+                return m >> 32
+        j += 4
+
+
+def qr_exact(x, y, c, tau):
+    """solve_qr (quantile_regression.rs:22-129) on the rows with c > 0; None where it fails."""
+    from scipy.optimize import linprog
+
+    act = c > 0
+    xa, ya, ca = x[act], y[act], c[act].astype(float)
+    if not np.all(np.isfinite(xa)) or not np.all(np.isfinite(ya)):
+        return None
+    res = linprog(-ya, A_eq=xa.T, b_eq=(1.0 - tau) * (xa.T @ ca), bounds=list(zip(np.zeros(len(ca)), ca)),
+                  method="highs")
+    if res.status != 0:
+        return None
+    return -np.asarray(res.eqlin.marginals, dtype=float)
+
+
+def empirical_quantile(v, q):  # quantile_decomposition.rs:164-171
+    if len(v) == 0:
+        return 0.0
+    v = np.sort(np.asarray(v, dtype=float))
+    return float(v[min(int(len(v) * q), len(v) - 1)])
+
+
+def mm_single_pass(xa, ya, ca, xb, yb, cb, seed, rep, sims, quantiles):
+    """run_single_pass (quantile_decomposition.rs:173-279) on count-weighted groups; returns the
+    row [gap, characteristics, coefficients] per target quantile."""
+    taus = [mm_tau(seed, rep, s) for s in range(sims)]
+    ba = [b for b in (qr_exact(xa, ya, ca, t) for t in taus) if b is not None]
+    bb = [b for b in (qr_exact(xb, yb, cb, t) for t in taus) if b is not None]
+    if len(ba) < sims // 2 or len(bb) < sims // 2:
+        raise OracleError("NalgebraError", "Failed to estimate a sufficient number of quantile regressions.")
+    num = min(len(ba), len(bb))
+    cuma, cumb = np.cumsum(ca), np.cumsum(cb)
+    yaa, ybb, yab = [], [], []
+    for i in range(num):
+        ra = int(np.searchsorted(cuma, mm_pick(seed, rep, 0, i, len(ya)), side="right"))
+        rb = int(np.searchsorted(cumb, mm_pick(seed, rep, 1, i, len(yb)), side="right"))
+        yaa.append(float(xa[ra] @ ba[i]))
+        ybb.append(float(xb[rb] @ bb[i]))
+        yab.append(float(xa[ra] @ bb[i]))
+    row = []
+    for q in quantiles:
+        qaa, qbb, qab = empirical_quantile(yaa, q), empirical_quantile(ybb, q), empirical_quantile(yab, q)
+        row += [qaa - qbb, qab - qbb, qaa - qab]
+    return np.array(row)
+
+
+class OracleQuantileDecomposition:
+    """QuantileDecompositionBuilder (quantile_decomposition.rs:21-445) over {name: list} frames."""
+
+    def __init__(self, frame, outcome, group, reference_group):
+        self.frame = {k: list(v) for k, v in frame.items()}
+        self.outcome, self.group, self.reference_group = outcome, group, reference_group
+        self.predictors, self.categorical = [], []
+        self.quantiles, self.simulations, self.reps, self.seed = [0.1, 0.25, 0.5, 0.75, 0.9], 200, 20, 0x0B5EED
+
+    def set(self, predictors=(), categorical=(), quantiles=None, simulations=200, reps=20, seed=0x0B5EED):
+        self.predictors, self.categorical = list(predictors), list(categorical)
+        if quantiles is not None:
+            self.quantiles = list(quantiles)
+        self.simulations, self.reps, self.seed = simulations, reps, seed
+        return self
+
+    def _groups(self):
+        g = self.frame[self.group]
+        levels = sorted(set(v for v in g if v is not None))
+        b = self.reference_group
+        a = levels[0] if levels and levels[0] != b else (levels[1] if len(levels) > 1 else "")
+        return a, b
+
+    def _design(self, rows, dummies):  # prepare_data (quantile_decomposition.rs:96-141)
+        y = self.frame[self.outcome]
+        if _kind(y) != "f64":
+            raise OracleError("PolarsError", "invalid series dtype: expected `Float64`")
+        if any(y[i] is None for i in rows):
+            raise OracleError("InvalidGroupVariable", "Null outcome encountered")
+        cols = [[1.0] * len(rows)]
+        for nm in self.predictors:
+            cols.append([np.nan if self.frame[nm][i] is None else float(self.frame[nm][i]) for i in rows])
+        for nm in dummies:
+            cols.append([dummies[nm][i] for i in rows])
+        return np.array(cols, dtype=float).T, np.array([float(y[i]) for i in rows])
+
+    def prepared(self):
+        dummies = {}
+        for cat in self.categorical:  # create_dummies_manual (quantile_decomposition.rs:143-161)
+            vals = self.frame[cat]
+            if _kind(vals) != "str":
+                raise OracleError("PolarsError", "invalid series dtype: expected `String`")
+            for lv in sorted(set(v for v in vals if v is not None))[1:]:
+                dummies[f"{cat}_{lv}"] = [np.nan if v is None else (1.0 if v == lv else 0.0) for v in vals]
+        a, b = self._groups()
+        g = self.frame[self.group]
+        ia = [i for i, v in enumerate(g) if v == a]
+        ib = [i for i, v in enumerate(g) if v == b]
+        if len(ia) < 2 or len(ib) < 2:
+            raise OracleError("InvalidGroupVariable", "One group has insufficient data")
+        xa, ya = self._design(ia, dummies)
+        xb, yb = self._design(ib, dummies)
+        return xa, ya, xb, yb
+
+    def run(self):
+        xa, ya, xb, yb = self.prepared()
+        one_a, one_b = np.ones(len(ya), dtype=np.int64), np.ones(len(yb), dtype=np.int64)
+        point = mm_single_pass(xa, ya, one_a, xb, yb, one_b, self.seed, MM_POINT_REP, self.simulations,
+                               self.quantiles)
+        rows = np.full((self.reps, len(point)), np.nan)
+        ok = np.zeros(self.reps, dtype=np.uint8)
+        for r in range(self.reps):
+            ca = np.bincount(resample_indices(self.seed, r, 0, len(ya)), minlength=len(ya))
+            cb = np.bincount(resample_indices(self.seed, r, 1, len(yb)), minlength=len(yb))
+            try:
+                rows[r] = mm_single_pass(xa, ya, ca, xb, yb, cb, self.seed, r, self.simulations, self.quantiles)
+                ok[r] = 1
+            except OracleError:
+                pass
+        good = rows[ok.astype(bool)]
+        out = {}
+        for qi, q in enumerate(self.quantiles):
+            det = {}
+            for k, nm in enumerate(("Total Gap", "Characteristics", "Coefficients")):
+                pt = point[3 * qi + k]
+                se, p, (lo, hi) = bootstrap_stats(good[:, 3 * qi + k] if len(good) else np.zeros(0))
+                det[nm] = dict(name=nm, estimate=pt, std_err=se, t_stat=pt / se if abs(se) > 1e-9 else 0.0,
+                               p_value=p, ci_lower=lo, ci_upper=hi)
+            out[f"q{int(q * 100.0)}"] = det
+        a, b = self._groups()
+        g = self.frame[self.group]
+        return dict(results_by_quantile=out, n_a=sum(v == a for v in g), n_b=sum(v == b for v in g), point=point,
+                    rows=rows, ok=ok)
+
+
+# ---------------------------------------------------------------------------------------------
 # synthetic wage panel (SURVEY.md §8d), deterministic from a seed
 # ---------------------------------------------------------------------------------------------
 def synthetic_panel(n, p, weighted, seed=20260424):

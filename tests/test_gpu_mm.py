@@ -1,0 +1,139 @@
+"""Machado-Mata on the MI355X engine (QuantileDecompositionBuilder, ob_mm.hip) vs the oracle:
+HiGHS-exact quantile regressions and the same MM-1 draws (oracle.mm_single_pass). Pass rows,
+builder results, the reference's MM test frame, determinism and identities at a larger size.
+The GPU's interior-point QR matches the exact LP vertex to ~1e-10 (tools/qr_ipm_proto.py); the
+tolerance below is the suite's 1e-6, relative to the scale of the compared quantities."""
+import numpy as np
+import pytest
+
+from test_gpu_parity import RTOL, SEED, close
+
+pytestmark = pytest.mark.gpu
+
+QS = [0.1, 0.25, 0.5, 0.75, 0.9]
+
+
+def mm_data(n, p, seed):
+    """Continuous covariates (unique QR optima); heteroskedastic t(4) errors so quantiles differ."""
+    rng = np.random.default_rng(seed)
+    out = {}
+    for g, ng in (("a", n // 2), ("b", n - n // 2)):
+        x = rng.normal(size=(ng, p)) + (0.3 if g == "a" else 0.0)
+        x[:, 0] = rng.uniform(8.0, 20.0, ng)
+        y = 1.0 + x @ np.linspace(0.1, 0.5, p) + (0.3 if g == "a" else 0.0) + rng.standard_t(4, ng) * (
+            0.5 + 0.05 * x[:, 0])
+        out["x" + g], out["y" + g] = x, y
+    return out
+
+
+def oracle_rows(O, d, sims, qs, reps):
+    xa, xb = O.with_intercept(d["xa"]), O.with_intercept(d["xb"])
+    na, nb = len(d["ya"]), len(d["yb"])
+    rows = [O.mm_single_pass(xa, d["ya"], np.ones(na, np.int64), xb, d["yb"], np.ones(nb, np.int64), SEED,
+                             O.MM_POINT_REP, sims, qs)]
+    for r in range(reps):
+        ca = np.bincount(O.resample_indices(SEED, r, 0, na), minlength=na)
+        cb = np.bincount(O.resample_indices(SEED, r, 1, nb), minlength=nb)
+        rows.append(O.mm_single_pass(xa, d["ya"], ca, xb, d["yb"], cb, SEED, r, sims, qs))
+    return np.array(rows)
+
+
+@pytest.mark.parametrize("n,p,sims", [(600, 1, 30), (1500, 3, 40), (3000, 5, 24), (5000, 15, 12)])
+def test_mm_rows_match_oracle(ob, O, n, p, sims):
+    d = mm_data(n, p, seed=n + p)
+    panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"])
+    try:
+        rows, ok = panel.mm(SEED, sims, QS, 0, 3)
+    finally:
+        panel.close()
+    want = oracle_rows(O, d, sims, QS, 3)
+    assert ok.all()
+    good, worst = close(rows, want, np.abs(want).max())
+    assert good, worst
+
+
+def mm_frame(n, seed=4):
+    rng = np.random.default_rng(seed)
+    g = np.where(rng.random(n) < 0.5, "M", "F")
+    edu = rng.uniform(8, 20, n)
+    exp_ = rng.uniform(0, 40, n)
+    sector = rng.choice(["a", "b", "c"], n)
+    y = 1.0 + 0.08 * edu + 0.02 * exp_ + 0.2 * (g == "M") + 0.1 * (sector == "c") + rng.standard_t(4, n) * 0.4
+    return {"wage": y.tolist(), "education": edu.tolist(), "experience": exp_.tolist(), "sector": sector.tolist(),
+            "gender": g.tolist()}
+
+
+def test_mm_builder_matches_oracle(ob, O):
+    f = mm_frame(2400)
+    r = (ob.QuantileDecompositionBuilder(f, "wage", "gender", "F").predictors(["education", "experience"])
+         .categorical_predictors(["sector"]).quantiles([0.1, 0.5, 0.9]).simulations(30).bootstrap_reps(6)
+         .seed(SEED).run())
+    o = (O.OracleQuantileDecomposition(f, "wage", "gender", "F")
+         .set(["education", "experience"], ["sector"], [0.1, 0.5, 0.9], 30, 6, SEED).run())
+    assert (r.n_a, r.n_b) == (o["n_a"], o["n_b"]) and r.n_failed == 0
+    assert sorted(r.results_by_quantile) == sorted(o["results_by_quantile"]) == ["q10", "q50", "q90"]
+    scale = np.abs(o["rows"]).max()
+    for key, det in r.results_by_quantile.items():
+        want = o["results_by_quantile"][key]
+        for c in (det.total_gap, det.characteristics_effect, det.coefficients_effect):
+            w = want[c.name]
+            for fld in ("estimate", "std_err", "ci_lower", "ci_upper"):
+                assert abs(getattr(c, fld) - w[fld]) <= RTOL * max(abs(w[fld]), scale), (key, c.name, fld)
+            assert c.p_value == w["p_value"]
+
+
+def test_mm_reference_test_frame(ob):  # tests/integration_test.rs:165-198
+    f = {"wage": [10.0, 12.0, 11.0, 13.0, 15.0, 20.0, 22.0, 21.0, 23.0, 25.0, 9.0, 18.0],
+         "education": [12.0, 16.0, 14.0, 16.0, 18.0, 12.0, 16.0, 14.0, 16.0, 18.0, 10.0, 20.0],
+         "gender": ["F"] * 6 + ["M"] * 6}
+    r = (ob.QuantileDecompositionBuilder(f, "wage", "gender", "F").predictors(["education"])
+         .quantiles([0.25, 0.5, 0.75]).simulations(10).bootstrap_reps(2).run())
+    for key in ("q25", "q50", "q75"):
+        d = r.results_by_quantile[key]
+        assert abs(d.characteristics_effect.estimate + d.coefficients_effect.estimate - d.total_gap.estimate) < 1e-9
+    assert r.n_a == 6 and r.n_b == 6
+
+
+def test_mm_errors(ob, N):
+    f = mm_frame(200)
+    with pytest.raises(N.OaxacaError) as e:
+        ob.QuantileDecompositionBuilder(f, "wage", "gender", "F").predictors(["nope"]).run()
+    assert e.value.code == N.OB_E_COLUMN
+    g = dict(f, wage=[None] + f["wage"][1:])
+    with pytest.raises(N.OaxacaError) as e:  # quantile_decomposition.rs:103-110
+        ob.QuantileDecompositionBuilder(g, "wage", "gender", "F").predictors(["education"]).run()
+    assert e.value.code == N.OB_E_GROUP and "Null outcome" in str(e.value)
+    h = dict(f, gender=["F"] * 199 + ["M"])
+    with pytest.raises(N.OaxacaError) as e:  # :202-206
+        ob.QuantileDecompositionBuilder(h, "wage", "gender", "F").predictors(["education"]).run()
+    assert "insufficient data" in str(e.value)
+
+
+def test_mm_deterministic_and_shard_invariant(ob):
+    d = mm_data(4000, 4, seed=7)
+    panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"])
+    try:
+        r0, k0 = panel.mm(SEED, 64, QS, 0, 6)
+        r1, k1 = panel.mm(SEED, 64, QS, 2, 4, with_point=False)
+        r2, _ = panel.mm(SEED, 64, QS, 0, 6)
+    finally:
+        panel.close()
+    assert np.array_equal(r0, r2) and k0.all()
+    assert np.array_equal(r0[3:], r1) and np.array_equal(k0[3:], k1)
+
+
+def test_mm_identities_at_size(ob):
+    """200k rows, 15 predictors (K = 16, configs[4]'s width), 100 simulations, 3 replicates: every
+    pass succeeds, characteristics + coefficients = gap at every quantile, and the median gap is the
+    raw median difference up to simulation noise."""
+    d = mm_data(200_000, 15, seed=11)
+    panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"])
+    try:
+        rows, ok = panel.mm(SEED, 100, QS, 0, 3)
+    finally:
+        panel.close()
+    assert ok.all()
+    r = rows.reshape(len(rows), len(QS), 3)
+    assert np.allclose(r[..., 1] + r[..., 2], r[..., 0], rtol=0, atol=1e-9)
+    # the point gap at the median approximates the difference of the groups' median outcomes
+    assert abs(r[0, 2, 0] - (np.median(d["ya"]) - np.median(d["yb"]))) < 0.3
