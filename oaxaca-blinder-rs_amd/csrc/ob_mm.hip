@@ -23,6 +23,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -72,6 +74,7 @@ struct MmArgs {
   double* red;                       // [slot][group][S_pad][nv]
   uint32_t* active;
   uint32_t* tprefix;                 // [slot][group][tiles + 1] (finish kernel scratch)
+  uint32_t* lane_of;                 // [slot][group][simulation] -> fit lane (lanes in ascending tau)
   uint32_t key0, key1;
   int n_q;
   const double* quantiles;
@@ -375,9 +378,8 @@ __global__ __launch_bounds__(64) void mm_start_kernel(const MmArgs a, int K) {
     double bv = 0.0;
     for (int k = 0; k < K; ++k) bv += v[k] * R[NP + k];
     const double ssr = fmax(R[NP + K] - bv, 0.0), sc = R[0];
-    delta = 1e-3 * (1.0 + sqrt(ssr / sc));
+    delta = 0.1 * (1.0 + sqrt(ssr / sc));  // dual start offset (tools/qr_ipm_proto.py)
   }
-  const uint32_t rep = a.rep0 == OB_MM_POINT_REP ? OB_MM_POINT_REP : a.rep0 + slot;
   for (int s = lane; s < a.S_pad; s += 64) {
     const size_t F = ((size_t)slot * 2 + g) * a.S_pad + s;
     if (s >= a.S) {
@@ -387,10 +389,48 @@ __global__ __launch_bounds__(64) void mm_start_kernel(const MmArgs a, int K) {
     a.fstat[F] = chol ? 0u : kFailed;
     for (int k = 0; k < K; ++k) a.beta[F * K + k] = chol ? v[k] : 0.0;
     double* f = a.fs + F * kFs;
-    f[FS_TAU] = ob_mm_tau((uint32_t)s, rep, a.key0, a.key1);
     f[FS_DELTA] = delta;
     f[FS_NACT] = R[NP + K + 1];
     f[FS_AP] = f[FS_AD] = 0.0;
+  }
+}
+
+// MM-1 quantiles of each (slot, group), lanes in ascending tau (block per (slot, group)): the
+// extreme quantiles, which need the most iterations, share fit batches, so the batches of the
+// others stop costing passes early. lane_of maps simulation -> lane for the finish kernel.
+__global__ __launch_bounds__(256) void mm_order_kernel(const MmArgs a, int m2) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  double* key = sm;
+  uint32_t* val = reinterpret_cast<uint32_t*>(sm + m2);
+  const uint32_t slot = blockIdx.x >> 1, g = blockIdx.x & 1;
+  const uint32_t rep = a.rep0 == OB_MM_POINT_REP ? OB_MM_POINT_REP : a.rep0 + slot;
+  for (int i = threadIdx.x; i < m2; i += blockDim.x) {
+    key[i] = i < a.S ? ob_mm_tau((uint32_t)i, rep, a.key0, a.key1) : INFINITY;
+    val[i] = (uint32_t)i;
+  }
+  __syncthreads();
+  for (int k = 2; k <= m2; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < m2; i += blockDim.x) {
+        const int l = i ^ j;
+        if (l > i) {
+          const bool up = (i & k) == 0;
+          const double x = key[i], y = key[l];
+          if ((x > y || (x == y && val[i] > val[l])) == up) {
+            key[i] = y;
+            key[l] = x;
+            const uint32_t t = val[i];
+            val[i] = val[l];
+            val[l] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  const size_t base = ((size_t)slot * 2 + g) * a.S_pad;
+  for (int j = threadIdx.x; j < a.S; j += blockDim.x) {
+    a.fs[(base + j) * kFs + FS_TAU] = key[j];
+    a.lane_of[base + val[j]] = (uint32_t)j;
   }
 }
 
@@ -531,8 +571,11 @@ __global__ __launch_bounds__(256) void mm_finish_kernel(const MmArgs a, int K, i
     const uint32_t g = threadIdx.x;
     uint16_t* idx = g ? ib : ia;
     uint32_t k = 0;
-    for (int s = 0; s < a.S; ++s)
-      if (a.fstat[fit_index(a, slot, g, s)] == kDone) idx[k++] = (uint16_t)s;
+    const uint32_t* lanes = a.lane_of + ((size_t)slot * 2 + g) * a.S_pad;
+    for (int s = 0; s < a.S; ++s) {
+      const uint32_t j = lanes[s];
+      if (a.fstat[fit_index(a, slot, g, (int)j)] == kDone) idx[k++] = (uint16_t)j;
+    }
     cnt[g] = k;
   }
   // exclusive tile prefixes of the replicate's level-1 counts (both groups)
@@ -633,15 +676,21 @@ struct Buffers {
   double *x = nullptr, *z = nullptr, *w = nullptr, *dx = nullptr, *dz = nullptr, *dw = nullptr;
   double *beta = nullptr, *dba = nullptr, *db = nullptr, *L = nullptr, *fs = nullptr;
   double *partial = nullptr, *red = nullptr, *quant = nullptr, *rows = nullptr;
-  uint32_t *fstat = nullptr, *active = nullptr, *tprefix = nullptr;
+  uint32_t *fstat = nullptr, *active = nullptr, *tprefix = nullptr, *lane_of = nullptr;
   uint8_t* ok = nullptr;
   ~Buffers() {
     for (void* p : {(void*)x, (void*)z, (void*)w, (void*)dx, (void*)dz, (void*)dw, (void*)beta, (void*)dba, (void*)db,
                     (void*)L, (void*)fs, (void*)partial, (void*)red, (void*)quant, (void*)rows, (void*)fstat,
-                    (void*)active, (void*)tprefix, (void*)ok})
+                    (void*)active, (void*)tprefix, (void*)lane_of, (void*)ok})
       (void)hipFree(p);
   }
 };
+
+// OB_MM_TRACE=1: per-iteration active fits and the final fit statuses on stderr.
+bool trace() {
+  static const bool t = getenv("OB_MM_TRACE") != nullptr;
+  return t;
+}
 
 // One batch of replicate slots: start, IPM iterations, finish. Rows/ok -> host.
 int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, int* iters) {
@@ -662,6 +711,12 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, int
   MM_OK(reduce(nv1, 0));
   hipLaunchKernelGGL(mm_start_kernel, dim3(a.n_rb * 2), dim3(64), lds_solve, s, a, K);
   MM_OK(hipGetLastError());
+  int m2 = 1;
+  while (m2 < a.S) m2 <<= 1;
+  const size_t lds_ord = (size_t)m2 * (sizeof(double) + sizeof(uint32_t));
+  MM_OK(hipFuncSetAttribute((const void*)mm_order_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_ord));
+  hipLaunchKernelGGL(mm_order_kernel, dim3(a.n_rb * 2), dim3(256), lds_ord, s, a, m2);
+  MM_OK(hipGetLastError());
   int it = 0;
   for (it = 1; it <= ob::kMmMaxIter; ++it) {
     pass(K, 0, a, grid, it == 1 ? 1 : 2, s);
@@ -673,6 +728,7 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, int
     uint32_t active = 0;
     MM_OK(hipMemcpyAsync(&active, a.active, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     MM_OK(hipStreamSynchronize(s));
+    if (trace()) fprintf(stderr, "[mm] iteration %d: %u of %zu fits active\n", it, active, n_fits);
     if (active == 0) break;
     pass(K, 1, a, grid, 0, s);
     MM_OK(hipGetLastError());
@@ -685,10 +741,27 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, int
     hipLaunchKernelGGL(mm_step_kernel, dim3((unsigned)((n_fits + 255) / 256)), dim3(256), 0, s, a, K, n_fits);
     MM_OK(hipGetLastError());
   }
+  if (trace()) {
+    std::vector<uint32_t> st(n_fits);
+    std::vector<double> fsh(n_fits * kFs);
+    MM_OK(hipMemcpy(st.data(), a.fstat, sizeof(uint32_t) * n_fits, hipMemcpyDeviceToHost));
+    MM_OK(hipMemcpy(fsh.data(), a.fs, sizeof(double) * n_fits * kFs, hipMemcpyDeviceToHost));
+    size_t done = 0, failed = 0, live = 0;
+    for (size_t f = 0; f < n_fits; ++f) {
+      if ((int)(f % a.S_pad) >= a.S) continue;
+      if (st[f] == kDone) ++done;
+      else if (st[f] & kFailed) ++failed;
+      else {
+        if (live < 8)
+          fprintf(stderr, "[mm] live fit %zu tau %.4f gap %.3e obj %.3e rel %.3e\n", f, fsh[f * kFs + FS_TAU],
+                  fsh[f * kFs + FS_GAP], fsh[f * kFs + FS_OBJ], fsh[f * kFs + FS_GAP] / (1 + fabs(fsh[f * kFs + FS_OBJ])));
+        ++live;
+      }
+    }
+    fprintf(stderr, "[mm] after %d iterations: %zu converged, %zu failed, %zu still live\n", it, done, failed, live);
+  }
   hipLaunchKernelGGL(mm_expire_kernel, dim3((unsigned)((n_fits + 255) / 256)), dim3(256), 0, s, a, n_fits);
   MM_OK(hipGetLastError());
-  int m2 = 1;
-  while (m2 < a.S) m2 <<= 1;
   const size_t lds_fin = (size_t)m2 * (3 * sizeof(double) + 2 * sizeof(uint16_t));
   MM_OK(hipFuncSetAttribute((const void*)mm_finish_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fin));
   hipLaunchKernelGGL(mm_finish_kernel, dim3(a.n_rb), dim3(256), lds_fin, s, a, K, m2);
@@ -734,6 +807,7 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   MM_OK(hipMalloc(&b.L, sizeof(double) * fits * K * K));
   MM_OK(hipMalloc(&b.fs, sizeof(double) * fits * kFs));
   MM_OK(hipMalloc(&b.fstat, sizeof(uint32_t) * fits));
+  MM_OK(hipMalloc(&b.lane_of, sizeof(uint32_t) * fits));
   MM_OK(hipMalloc(&b.partial, sizeof(double) * (size_t)rb_cap * (nch0 + nch1) * S_pad * nv_max));
   MM_OK(hipMalloc(&b.red, sizeof(double) * fits * nv_max));
   MM_OK(hipMalloc(&b.active, sizeof(uint32_t)));
@@ -773,6 +847,7 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   a.red = b.red;
   a.active = b.active;
   a.tprefix = b.tprefix;
+  a.lane_of = b.lane_of;
   a.key0 = (uint32_t)seed;
   a.key1 = (uint32_t)(seed >> 32);
   a.n_q = n_q;

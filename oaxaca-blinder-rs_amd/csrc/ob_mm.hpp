@@ -8,7 +8,7 @@
 namespace ob {
 constexpr int kMmMaxK = 16;      // intercept + predictors (register-resident normal matrix)
 constexpr int kMmMaxSims = 4096;  // simulations per pass (LDS sort in the finish kernel)
-constexpr int kMmMaxIter = 100;   // IPM iterations per fit
+constexpr int kMmMaxIter = 200;   // IPM iterations per fit (Clarabel's default max_iter)
 
 // One MM pass per replicate of [first_rep, first_rep + n_reps) (OBRS-1 resamples), preceded by
 // the point estimate (every row once, MM-1 replicate OB_MM_POINT_REP) when with_point. Rows:

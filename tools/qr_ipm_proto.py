@@ -21,7 +21,7 @@ def qr_ipm(X, y, c, tau, tol=1e-12, max_iter=100, eta=0.99995):
     G = (X.T * c) @ X
     beta = np.linalg.solve(G, X.T @ (c * y))
     r = y - X @ beta
-    dlt = 1e-3 * (1.0 + np.sqrt((c * r * r).sum() / c.sum()))  # from the OLS Gram on the GPU
+    dlt = 0.1 * (1.0 + np.sqrt((c * r * r).sum() / c.sum()))  # from the OLS Gram on the GPU
     z = np.maximum(-r, 0.0) + dlt
     w = np.maximum(r, 0.0) + dlt
     for it in range(1, max_iter + 1):
