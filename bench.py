@@ -74,6 +74,96 @@ def cpu_baseline(d, preds, weighted, ref, target_s, threads):
                       f"{threads} threads, {dt:.1f} s"}
 
 
+def cpu_baseline_mm(d, sims, target_s):
+    """The oracle's QR (HiGHS exact LP, one group's full design) timed on host cores; an MM
+    replicate is 2 x sims such fits (quantile_decomposition.rs:221-229), so replicates/s =
+    fits/s / (2 sims). The reference's own solver (Clarabel IPM) is not runnable here."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    x = O.with_intercept(d["xa"])
+    c = np.ones(len(d["ya"]), dtype=np.int64)
+    t0, n = time.perf_counter(), 0
+    while True:
+        O.qr_exact(x, d["ya"], c, 0.1 + 0.8 * ((n * 0.618) % 1.0))
+        n += 1
+        if time.perf_counter() - t0 > target_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt / (2 * sims), "unit": "replicates/s", "cores": 1, "kind": "port",
+            "sample": f"{n} HiGHS QR fits of group A ({len(d['ya'])} rows x {x.shape[1]} columns), {dt:.1f} s; "
+                      f"replicates/s = fits/s / {2 * sims}"}
+
+
+def bench_mm(args, world, rank, local, dist):
+    """configs[4]: Machado-Mata, R bootstrap replicates per GPU per step (no point pass)."""
+    import torch
+
+    ob = importlib.import_module("oaxaca-blinder-rs_amd")
+    d = synthetic(args.rows, args.preds, False)
+    panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"], device=local)
+    qs = [0.1, 0.25, 0.5, 0.75, 0.9]
+    R, seed = args.reps, 0x0B5EED
+    dev = torch.device("cuda", local)
+
+    def step(i):
+        rows, ok = panel.mm(seed, args.sims, qs, (i * world + rank) * R, R, with_point=False)
+        t = panel.timing()
+        if dist:
+            g = torch.from_numpy(rows).to(dev)
+            out = torch.empty((world * R, rows.shape[1]), dtype=torch.float64, device=dev)
+            dist.all_gather_into_tensor(out, g)
+            rows = out.cpu().numpy()
+        return rows, ok, t
+
+    for i in range(args.warmup):
+        step(i)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    asm_ms, fit_rows, iters, last = 0.0, 0.0, 0, None
+    for i in range(args.steps):
+        rows, ok, t = step(args.warmup + i)
+        asm_ms += t["mm_assemble_ms"]
+        fit_rows += t["mm_fit_rows"]
+        iters = max(iters, t["mm_iterations"])
+        last = (rows, ok)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    elapsed = float(tt[0])
+    if rank != 0:
+        return
+    k = args.preds + 1
+    bytes_row = 72.0  # mm_assemble per live (fit, row): x, z, w, dx, dz, dw read, x, z, w written
+    flops_row = 2.0 * (k * (k + 1) / 2 + 2 * k)  # X'QX pairs, X'Q r, X beta
+    gbps = fit_rows * bytes_row / (asm_ms * 1e-3) / 1e9
+    value = world * R * args.steps / elapsed
+    out = {
+        "metric": "Machado-Mata bootstrap replicates/sec (configs[4]: 1000 QR draws per group per replicate)",
+        "value": value, "unit": "replicates/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64", "data": "synthetic (SURVEY.md §8d wage panel, numpy seed 20260424; OBRS-1/MM-1 seed 0x0B5EED)",
+        "config": {"workload": "configs[4]: Machado-Mata, 1000 simulations, quantiles 0.1/0.25/0.5/0.75/0.9",
+                   "rows": args.rows, "predictors": args.preds, "simulations": args.sims,
+                   "replicates_per_gpu_per_step": R, "parallelism": f"replicates sharded x{world}, RCCL all-gather"},
+        "roofline": {"bound": "hbm", "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": gbps / HBM_PEAK_GBPS, "traffic": None, "kernel": "mm_assemble_kernel<16>",
+                     "assemble_ms": asm_ms, "live_fit_rows": fit_rows, "bytes_per_fit_row": bytes_row,
+                     "tflops": fit_rows * flops_row / (asm_ms * 1e-3) / 1e12, "max_ipm_iterations": iters},
+    }
+    out["cpu_baseline"] = cpu_baseline_mm(d, args.sims, args.cpu_seconds) if world == 1 and args.cpu_seconds > 0 \
+        else None
+    rows, ok = last
+    out["check"] = {"ok_replicates": int(ok.sum()), "q50_gap_mean": float(np.nanmean(rows[:, 6]))}
+    print(json.dumps(out), flush=True)
+
+
 def load_traffic(rows, preds, reps):
     """HBM bytes per ob_gram_kernel launch from the committed rocprofv3 PMC summary."""
     path = os.path.join(ROOT, "profiles", "pmc_gram.json")
@@ -102,8 +192,20 @@ def main():
     ap.add_argument("--taus", type=str, default="",
                     help="configs[3]: comma-separated RIF quantiles sharing one bootstrap (e.g. 0.1,0.5,0.9); "
                          "reports replicate-quantiles/s instead of the headline metric")
+    ap.add_argument("--mm", action="store_true",
+                    help="configs[4]: Machado-Mata (defaults 500k rows x 15 predictors, 1000 simulations, "
+                         "2 replicates per GPU per step); reports MM replicates/s")
+    ap.add_argument("--sims", type=int, default=1000, help="--mm: quantile regressions per group per replicate")
     args = ap.parse_args()
     taus = [float(t) for t in args.taus.split(",") if t.strip()]
+    if args.mm:
+        explicit = set(a.split("=")[0] for a in sys.argv[1:])
+        if "--rows" not in explicit:
+            args.rows = 500_000
+        if "--preds" not in explicit:
+            args.preds = 15
+        if "--reps" not in explicit:
+            args.reps = 2
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -118,6 +220,11 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(local)
+    if args.mm:
+        bench_mm(args, world, rank, local, dist)
+        if dist:
+            dist.destroy_process_group()
+        return
     ob = importlib.import_module("oaxaca-blinder-rs_amd")
     weighted = not args.unweighted
     d = synthetic(args.rows, args.preds, weighted)

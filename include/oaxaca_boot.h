@@ -154,6 +154,10 @@ typedef struct {
   double counts_ms; /* level-2 count images (ob_count_kernel) */
   double heckman_ms; /* Heckman panels: probit iterations + IMR sums + two-step solve (in solve_ms too) */
   int32_t probit_iterations; /* Heckman panels: probit iterations of the last segment */
+  double mm_assemble_ms;     /* ob_mm_run: mm_assemble kernel time (HIP events), summed */
+  double mm_fit_rows;        /* ob_mm_run: live (fit, row) pairs those launches processed */
+  int32_t mm_iterations;     /* ob_mm_run: most IPM iterations of a batch */
+  double mm_ms;              /* ob_mm_run: whole call, host clock */
 } ob_timing;
 int ob_panel_last_timing(const ob_panel* panel, ob_timing* out);
 /* Synchronize the stream used by the last *_device call and collect its timings. */

@@ -68,7 +68,9 @@ class ob_timing(C.Structure):
     _fields_ = [("level1_ms", C.c_double), ("gram_ms", C.c_double), ("reduce_ms", C.c_double),
                 ("solve_ms", C.c_double), ("gram_launches", C.c_int32), ("chunks", C.c_int32),
                 ("blocks", C.c_int32), ("counts_ms", C.c_double),
-                ("heckman_ms", C.c_double), ("probit_iterations", C.c_int32)]
+                ("heckman_ms", C.c_double), ("probit_iterations", C.c_int32),
+                ("mm_assemble_ms", C.c_double), ("mm_fit_rows", C.c_double), ("mm_iterations", C.c_int32),
+                ("mm_ms", C.c_double)]
 
 
 class ob_column(C.Structure):

@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -73,6 +74,7 @@ struct MmArgs {
   double* partial;                   // [slot][chunk (A then B)][S_pad][nv]
   double* red;                       // [slot][group][S_pad][nv]
   uint32_t* active;
+  unsigned long long* active_rows;   // live (fit, row) pairs of the next passes
   uint32_t* tprefix;                 // [slot][group][tiles + 1] (finish kernel scratch)
   uint32_t* lane_of;                 // [slot][group][simulation] -> fit lane (lanes in ascending tau)
   uint32_t key0, key1;
@@ -393,6 +395,7 @@ __global__ __launch_bounds__(64) void mm_start_kernel(const MmArgs a, int K) {
     f[FS_NACT] = R[NP + K + 1];
     f[FS_AP] = f[FS_AD] = 0.0;
   }
+  if (lane == 0 && chol) atomicAdd(a.active_rows, (unsigned long long)a.S * (unsigned long long)R[NP + K + 1]);
 }
 
 // MM-1 quantiles of each (slot, group), lanes in ascending tau (block per (slot, group)): the
@@ -470,6 +473,7 @@ __global__ __launch_bounds__(64) void mm_solve_affine_kernel(const MmArgs a, int
   if (lane == 0) {
     f[FS_MU] = gap / (2.0 * f[FS_NACT]);
     atomicAdd(a.active, 1u);
+    atomicAdd(a.active_rows, (unsigned long long)f[FS_NACT]);
   }
 }
 
@@ -677,11 +681,12 @@ struct Buffers {
   double *beta = nullptr, *dba = nullptr, *db = nullptr, *L = nullptr, *fs = nullptr;
   double *partial = nullptr, *red = nullptr, *quant = nullptr, *rows = nullptr;
   uint32_t *fstat = nullptr, *active = nullptr, *tprefix = nullptr, *lane_of = nullptr;
+  unsigned long long* active_rows = nullptr;
   uint8_t* ok = nullptr;
   ~Buffers() {
     for (void* p : {(void*)x, (void*)z, (void*)w, (void*)dx, (void*)dz, (void*)dw, (void*)beta, (void*)dba, (void*)db,
                     (void*)L, (void*)fs, (void*)partial, (void*)red, (void*)quant, (void*)rows, (void*)fstat,
-                    (void*)active, (void*)tprefix, (void*)lane_of, (void*)ok})
+                    (void*)active, (void*)active_rows, (void*)tprefix, (void*)lane_of, (void*)ok})
       (void)hipFree(p);
   }
 };
@@ -692,8 +697,14 @@ bool trace() {
   return t;
 }
 
+struct MmStats {
+  double assemble_ms = 0.0, fit_rows = 0.0;
+  int iterations = 0;
+  hipEvent_t ev[2] = {nullptr, nullptr};
+};
+
 // One batch of replicate slots: start, IPM iterations, finish. Rows/ok -> host.
-int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, int* iters) {
+int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, MmStats& st) {
   const uint32_t nch = a.nch[0] + a.nch[1];
   const int NP = K * (K + 1) / 2;
   const int nv1 = NP + K + 2, nv2 = 5 + 2 * K;
@@ -706,6 +717,7 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, int
   };
   const size_t lds_solve = sizeof(double) * ((size_t)K * K + K);
   // start: weighted OLS per (slot, group)
+  MM_OK(hipMemsetAsync(a.active_rows, 0, sizeof(unsigned long long), s));
   pass(K, 0, a, dim3(nch, 1, a.n_rb), 0, s);
   MM_OK(hipGetLastError());
   MM_OK(reduce(nv1, 0));
@@ -718,16 +730,33 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, int
   hipLaunchKernelGGL(mm_order_kernel, dim3(a.n_rb * 2), dim3(256), lds_ord, s, a, m2);
   MM_OK(hipGetLastError());
   int it = 0;
+  uint64_t live_rows = 0;  // first assemble: every fit of a group whose OLS start exists (mm_start_kernel)
+  {
+    unsigned long long v = 0;
+    MM_OK(hipMemcpyAsync(&v, a.active_rows, sizeof(v), hipMemcpyDeviceToHost, s));
+    MM_OK(hipStreamSynchronize(s));
+    live_rows = v;
+  }
   for (it = 1; it <= ob::kMmMaxIter; ++it) {
+    MM_OK(hipEventRecord(st.ev[0], s));
     pass(K, 0, a, grid, it == 1 ? 1 : 2, s);
     MM_OK(hipGetLastError());
+    MM_OK(hipEventRecord(st.ev[1], s));
     MM_OK(reduce(nv1, 0));
     MM_OK(hipMemsetAsync(a.active, 0, sizeof(uint32_t), s));
+    MM_OK(hipMemsetAsync(a.active_rows, 0, sizeof(unsigned long long), s));
     hipLaunchKernelGGL(mm_solve_affine_kernel, dim3((unsigned)n_fits), dim3(64), lds_solve, s, a, K);
     MM_OK(hipGetLastError());
     uint32_t active = 0;
+    unsigned long long arows = 0;
     MM_OK(hipMemcpyAsync(&active, a.active, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    MM_OK(hipMemcpyAsync(&arows, a.active_rows, sizeof(arows), hipMemcpyDeviceToHost, s));
     MM_OK(hipStreamSynchronize(s));
+    float ms = 0.f;
+    MM_OK(hipEventElapsedTime(&ms, st.ev[0], st.ev[1]));
+    st.assemble_ms += ms;
+    st.fit_rows += (double)live_rows;
+    live_rows = arows;
     if (trace()) fprintf(stderr, "[mm] iteration %d: %u of %zu fits active\n", it, active, n_fits);
     if (active == 0) break;
     pass(K, 1, a, grid, 0, s);
@@ -769,7 +798,7 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, int
   MM_OK(hipMemcpyAsync(rows_h, a.rows, sizeof(double) * a.n_rb * 3 * a.n_q, hipMemcpyDeviceToHost, s));
   MM_OK(hipMemcpyAsync(ok_h, a.ok, a.n_rb, hipMemcpyDeviceToHost, s));
   MM_OK(hipStreamSynchronize(s));
-  if (iters) *iters = std::max(*iters, std::min(it, ob::kMmMaxIter));
+  st.iterations = std::max(st.iterations, std::min(it, ob::kMmMaxIter));
   return OB_OK;
 }
 
@@ -811,6 +840,7 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   MM_OK(hipMalloc(&b.partial, sizeof(double) * (size_t)rb_cap * (nch0 + nch1) * S_pad * nv_max));
   MM_OK(hipMalloc(&b.red, sizeof(double) * fits * nv_max));
   MM_OK(hipMalloc(&b.active, sizeof(uint32_t)));
+  MM_OK(hipMalloc(&b.active_rows, sizeof(unsigned long long)));
   MM_OK(hipMalloc(&b.quant, sizeof(double) * n_q));
   MM_OK(hipMalloc(&b.rows, sizeof(double) * rb_cap * 3 * n_q));
   MM_OK(hipMalloc(&b.ok, rb_cap));
@@ -846,6 +876,7 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   a.partial = b.partial;
   a.red = b.red;
   a.active = b.active;
+  a.active_rows = b.active_rows;
   a.tprefix = b.tprefix;
   a.lane_of = b.lane_of;
   a.key0 = (uint32_t)seed;
@@ -854,14 +885,24 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   a.quantiles = b.quant;
   a.rows = b.rows;
   a.ok = b.ok;
-  if (max_iters) *max_iters = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  MmStats st;
+  MM_OK(hipEventCreate(&st.ev[0]));
+  MM_OK(hipEventCreate(&st.ev[1]));
+  struct EvGuard {
+    MmStats& s;
+    ~EvGuard() {
+      for (hipEvent_t e : s.ev)
+        if (e) (void)hipEventDestroy(e);
+    }
+  } evg{st};
   size_t out = 0;
   if (with_point) {  // every row once, MM-1 replicate OB_MM_POINT_REP
     MmArgs pa = a;
     pa.n_rb = 1;
     pa.rep0 = OB_MM_POINT_REP;
     pa.counts = nullptr;
-    OB_TRY(run_batch(pa, K, s, rows, ok, max_iters));
+    OB_TRY(run_batch(pa, K, s, rows, ok, st));
     out = 1;
   }
   // resamples: OBRS-1 count images per segment, then batches of rb_cap slots
@@ -879,12 +920,17 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
       ba.m1 = p->d_m1;
       ba.nb_rep = nb_rep;
       ba.rep_pad = rep_pad;
-      OB_TRY(run_batch(ba, K, s, rows + (out + s0 + b0) * 3 * n_q, ok + out + s0 + b0, max_iters));
+      OB_TRY(run_batch(ba, K, s, rows + (out + s0 + b0) * 3 * n_q, ok + out + s0 + b0, st));
     }
   }
   uint32_t flag = 0;
   MM_OK(hipMemcpy(&flag, p->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost));
   if (flag) return ob::fail(OB_E_OVERFLOW, "a resampled row was drawn more than 255 times in one replicate");
+  p->timing.mm_assemble_ms = st.assemble_ms;
+  p->timing.mm_fit_rows = st.fit_rows;
+  p->timing.mm_iterations = st.iterations;
+  p->timing.mm_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (max_iters) *max_iters = st.iterations;
   return OB_OK;
 }
 
