@@ -301,3 +301,47 @@ def test_heckman_pooled_unsupported(O):  # builder.rs:500-507 panics: beta_star 
                                                                                              ref_mode=2)
     with pytest.raises(O.OracleError):
         ob.heckman("selection", ["z"]).run()
+
+
+# --- Machado-Mata (quantile_decomposition.rs, math/quantile_regression.rs) ------------------
+@pytest.mark.parametrize("tau", [0.5, 0.25])
+def test_qr_linear_data_kat(O, tau):  # quantile_regression.rs:136-170 (tolerance 1e-4 there)
+    y = np.array([1.0, 2.0, 3.0, 4.0, 5.0])
+    x = np.column_stack([np.ones(5), [1.0, 2.0, 3.0, 4.0, 5.0]])
+    b = O.qr_exact(x, y, np.ones(5, dtype=np.int64), tau)
+    assert len(b) == 2 and abs(b[0]) < 1e-9 and abs(b[1] - 1.0) < 1e-9
+
+
+def test_qr_counts_equal_duplicated_rows(O):
+    """Counts c_i are the bootstrap's duplicated rows: the weighted LP equals the LP on the
+    expanded sample."""
+    rng = np.random.default_rng(0)
+    x = np.column_stack([np.ones(40), rng.normal(size=40)])
+    y = x @ [1.0, 2.0] + rng.standard_t(3, 40)
+    c = rng.integers(0, 3, 40)
+    idx = np.repeat(np.arange(40), c)
+    b1 = O.qr_exact(x, y, c, 0.3)
+    b2 = O.qr_exact(x[idx], y[idx], np.ones(len(idx), dtype=np.int64), 0.3)
+    assert np.allclose(b1, b2, atol=1e-9)
+
+
+def test_mm_integration_kat(O):  # tests/integration_test.rs:165-198
+    f = {"wage": [10.0, 12.0, 11.0, 13.0, 15.0, 20.0, 22.0, 21.0, 23.0, 25.0, 9.0, 18.0],
+         "education": [12.0, 16.0, 14.0, 16.0, 18.0, 12.0, 16.0, 14.0, 16.0, 18.0, 10.0, 20.0],
+         "gender": ["F"] * 6 + ["M"] * 6}
+    r = O.OracleQuantileDecomposition(f, "wage", "gender", "F").set(["education"], quantiles=[0.25, 0.5, 0.75],
+                                                                     simulations=10, reps=2).run()
+    assert sorted(r["results_by_quantile"]) == ["q25", "q50", "q75"]
+    for det in r["results_by_quantile"].values():
+        gap, ch, co = (det[k]["estimate"] for k in ("Total Gap", "Characteristics", "Coefficients"))
+        assert abs(ch + co - gap) < 1e-9
+
+
+def test_mm1_draws(O):
+    """MM-1: tau_s in [0.01, 0.99) with the uniform law; row picks exactly uniform (chi-square)."""
+    taus = np.array([O.mm_tau(0xABC, 3, s) for s in range(4000)])
+    assert taus.min() >= 0.01 and taus.max() < 0.99 and abs(taus.mean() - 0.5) < 0.02
+    n = 37
+    cnt = np.bincount([O.mm_pick(0xABC, 5, 1, i, n) for i in range(37 * 200)], minlength=n)
+    chi2 = ((cnt - 200.0) ** 2 / 200.0).sum()
+    assert abs(chi2 - (n - 1)) < 6 * np.sqrt(2 * (n - 1))
