@@ -119,16 +119,37 @@ __device__ __forceinline__ double* partial_row(const MmArgs& a, const Work& w, i
   return a.partial + (((size_t)w.slot * (a.nch[0] + a.nch[1]) + w.gch) * a.S_pad + w.s) * nv;
 }
 
-// mode 0: weighted OLS of the replicate (q = c, rho = y; lane 0 only) -> M, X'Cy, sum c y^2, n_act
-// mode 1: start point (x = (1 - tau) c, z/w from the OLS residual) + assemble
-// mode 2: apply the last step (x += ap dx, z += ad dz, w += ad dw) + assemble
+// mm_assemble: mode 0: weighted OLS of the replicate (q = c, rho = y) -> M, X'Cy, sum c y^2, n_act;
+// mode 1: start point (x = (1 - tau) c, z/w from the OLS residual) + assemble; mode 2: apply the
+// last step (x += ap dx, z += ad dz, w += ad dw) + assemble.
+// The same pass with X'QX and X'Q r on f64 MFMA (v_mfma_f64_16x16x4: A = q of 16 fits x 4 rows,
+// B = the rows' pair products, the counts-Gram kernel's shape). Block = 4 waves on the same 64
+// fits and a chunk of rows; per 64-row sub-tile: the rows' values are staged in LDS, then thread
+// (fit = t & 63, row group = wave) applies the last step and writes q and q r into LDS images,
+// then wave w runs the MFMAs of column blocks w, w + 4, w + 8 (pair blocks, then the X'Q r block).
+constexpr int kXs = 17;     // LDS stride of a staged row: [1, x_1..x_p, pad.., y at 16]
+constexpr int kQs = 65;     // LDS stride of a q-image row (64 fits + pad)
+constexpr int kMfmaCb = 3;  // column blocks per wave (4 waves x 3 >= 9 pair blocks + 1)
+typedef double mm_d4 __attribute__((ext_vector_type(4)));
+
 template <int K>
-__global__ __launch_bounds__(64) void mm_assemble_kernel(const MmArgs a, int mode) {
+__global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a, int mode) {
   constexpr int NP = K * (K + 1) / 2, NV = NP + K + 2;
-  const Work wk = work(a);
-  const size_t F = fit_index(a, wk.slot, wk.g, wk.s);
-  const uint32_t st = wk.s < a.S ? a.fstat[F] : kDone;
-  const bool live = mode == 0 ? wk.lane == 0 : !(st & (kDone | kFailed));
+  constexpr int NCB = (NP + 15) / 16;  // pair column blocks; block NCB is X'Q r
+  __shared__ double xs[64 * kXs];
+  __shared__ double qi[64 * kQs];
+  __shared__ double qri[64 * kQs];
+  __shared__ double red[2][4][64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t gch = blockIdx.x, fb = blockIdx.y, slot = blockIdx.z;
+  const uint32_t g = gch >= a.nch[0] ? 1u : 0u;
+  const uint32_t ch = gch - (g ? a.nch[0] : 0u);
+  // phase-1 role: fit = lane, rows of row group `wave`
+  const int s = (int)fb * 64 + lane;
+  const size_t F = fit_index(a, slot, g, s);
+  const uint32_t st = s < a.S ? a.fstat[F] : kDone;
+  const bool live = mode == 0 ? s < a.S_pad : !(st & (kDone | kFailed));
   double beta[K];
   double tau = 0.0, ap = 0.0, ad = 0.0, delta = 0.0;
 #pragma unroll
@@ -139,70 +160,165 @@ __global__ __launch_bounds__(64) void mm_assemble_kernel(const MmArgs a, int mod
     ad = a.fs[F * kFs + FS_AD];
     delta = a.fs[F * kFs + FS_DELTA];
   }
-  double acc[NV];
+  double gap = 0.0, obj = 0.0;
+  // phase-2 role: column blocks of this wave and their pair columns
+  int pa[kMfmaCb], pb[kMfmaCb];
 #pragma unroll
-  for (int i = 0; i < NV; ++i) acc[i] = 0.0;
-  const double* X = a.cols[wk.g];
-  const int64_t ld = a.ld[wk.g];
-  const uint32_t n = a.n[wk.g];
-  const size_t sb = ((size_t)wk.slot * a.rep_rows + (wk.g ? a.n[0] : 0u)) * a.S_pad + wk.s;
-  const uint32_t r0 = wk.ch * kRc, r1 = min(n, r0 + kRc);
-  if (__any(live))
-    for (uint32_t row = r0; row < r1; ++row) {
-      const uint32_t cu = row_count(a, wk.slot, wk.g, row);
-      if (cu == 0) continue;
-      double xr[K];
-      xr[0] = 1.0;
-#pragma unroll
-      for (int k = 1; k < K; ++k) xr[k] = X[(size_t)(k - 1) * ld + row];
-      const double y = X[(size_t)a.p * ld + row];
-      if (!live) continue;
-      const double c = (double)cu;
-      double q, rho;
-      if (mode == 0) {
-        q = c;
-        rho = y;
-        acc[NP + K] += c * y * y;
-        acc[NP + K + 1] += 1.0;
-      } else {
-        const size_t si = sb + (size_t)row * a.S_pad;
-        double xb = 0.0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) xb += xr[k] * beta[k];
-        const double r = y - xb;
-        double xv, zv, wv;
-        if (mode == 1) {
-          xv = (1.0 - tau) * c;
-          zv = fmax(-r, 0.0) + delta;
-          wv = fmax(r, 0.0) + delta;
-        } else {
-          xv = a.x[si] + ap * a.dx[si];
-          zv = a.z[si] + ad * a.dz[si];
-          wv = a.w[si] + ad * a.dw[si];
+  for (int c = 0; c < kMfmaCb; ++c) {
+    const int cb = wave + 4 * c;
+    pa[c] = pb[c] = -1;
+    if (cb < NCB) {
+      const int e = cb * 16 + (lane & 15);
+      if (e < NP) {  // e -> (i, j), i <= j, i-major (ob_pair_index order)
+        int i = 0, e0 = 0;
+        while (e >= e0 + (K - i)) {
+          e0 += K - i;
+          ++i;
         }
-        a.x[si] = xv;
-        a.z[si] = zv;
-        a.w[si] = wv;
-        const double sv = c - xv;
-        q = 1.0 / (zv / xv + wv / sv);
-        rho = r;  // rho_aff = r_d + w - z = y - X beta
-        acc[NP + K] += xv * zv + sv * wv;
-        acc[NP + K + 1] += y * xv;
+        pa[c] = i;
+        pb[c] = i + (e - e0);
       }
-      int e = 0;
-#pragma unroll
-      for (int i = 0; i < K; ++i) {
-        const double t = q * xr[i];
-#pragma unroll
-        for (int j = i; j < K; ++j) acc[e++] += t * xr[j];
-      }
-      const double qr = q * rho;
-#pragma unroll
-      for (int k = 0; k < K; ++k) acc[NP + k] += qr * xr[k];
+    } else if (cb == NCB && (lane & 15) < K) {
+      pa[c] = lane & 15;  // X'Q r: B is the x column itself, A = q r
+      pb[c] = 0;
     }
-  double* P = partial_row(a, wk, NV);
+  }
+  mm_d4 acc[4][kMfmaCb];
 #pragma unroll
-  for (int i = 0; i < NV; ++i) P[i] = acc[i];
+  for (int q4 = 0; q4 < 4; ++q4)
+#pragma unroll
+    for (int c = 0; c < kMfmaCb; ++c) acc[q4][c] = (mm_d4){0.0, 0.0, 0.0, 0.0};
+  const double* X = a.cols[g];
+  const int64_t ld = a.ld[g];
+  const uint32_t n = a.n[g];
+  const size_t sb = ((size_t)slot * a.rep_rows + (g ? a.n[0] : 0u)) * a.S_pad + s;
+  const uint32_t r0 = ch * kRc, r1 = min(n, r0 + kRc);
+  const bool any_live = __syncthreads_or(live);
+  if (any_live)
+    for (uint32_t t0 = r0; t0 < r1; t0 += 64) {
+      const uint32_t nr = min(64u, r1 - t0);
+      // stage the sub-tile's rows: [1, x_1..x_{K-1}, 0.., y]
+      for (int i = tid; i < 64 * kXs; i += 256) {
+        const int rr = i / kXs, col = i % kXs;
+        double v = 0.0;
+        if ((uint32_t)rr < nr) {
+          if (col == 0)
+            v = 1.0;
+          else if (col < K)
+            v = X[(size_t)(col - 1) * ld + t0 + rr];
+          else if (col == kXs - 1)
+            v = X[(size_t)a.p * ld + t0 + rr];
+        }
+        xs[i] = v;
+      }
+      __syncthreads();
+      // phase 1: rows wave, wave + 4, ... of the sub-tile for fit `lane`; the state of the next
+      // row is loaded before this row's stores (software prefetch)
+      const bool pref = mode == 2 && live;
+      double nx = 0.0, nz = 0.0, nw = 0.0, ndx = 0.0, ndz = 0.0, ndw = 0.0;
+      auto load_state = [&](int rr) {
+        if (pref && (uint32_t)rr < nr) {
+          const size_t si = sb + (size_t)(t0 + rr) * a.S_pad;
+          nx = a.x[si];
+          nz = a.z[si];
+          nw = a.w[si];
+          ndx = a.dx[si];
+          ndz = a.dz[si];
+          ndw = a.dw[si];
+        }
+      };
+      load_state(wave);
+      for (int rr = wave; rr < 64; rr += 4) {
+        const double cx = nx, cz = nz, cw = nw, cdx = ndx, cdz = ndz, cdw = ndw;
+        load_state(rr + 4);
+        double q = 0.0, qr = 0.0;
+        const uint32_t row = t0 + rr;
+        const uint32_t cu = (uint32_t)rr < nr ? row_count(a, slot, g, row) : 0u;
+        if (cu != 0 && live) {
+          const double c = (double)cu;
+          const double* xr = xs + rr * kXs;
+          const double y = xr[kXs - 1];
+          if (mode == 0) {
+            q = c;
+            qr = c * y;
+            gap += c * y * y;
+            obj += 1.0;
+          } else {
+            const size_t si = sb + (size_t)row * a.S_pad;
+            double xb = 0.0;
+#pragma unroll
+            for (int k = 0; k < K; ++k) xb += xr[k] * beta[k];
+            const double r = y - xb;
+            double xv, zv, wv;
+            if (mode == 1) {
+              xv = (1.0 - tau) * c;
+              zv = fmax(-r, 0.0) + delta;
+              wv = fmax(r, 0.0) + delta;
+            } else {
+              xv = cx + ap * cdx;
+              zv = cz + ad * cdz;
+              wv = cw + ad * cdw;
+            }
+            a.x[si] = xv;
+            a.z[si] = zv;
+            a.w[si] = wv;
+            const double sv = c - xv;
+            q = 1.0 / (zv / xv + wv / sv);
+            qr = q * r;  // rho_aff = r_d + w - z = y - X beta
+            gap += xv * zv + sv * wv;
+            obj += y * xv;
+          }
+        }
+        qi[rr * kQs + lane] = q;
+        qri[rr * kQs + lane] = qr;
+      }
+      __syncthreads();
+      // phase 2: acc[q4][c] += A(q of fits 16 q4.., rows 4 ks..) x B(pair products)
+#pragma unroll 2
+      for (int ks = 0; ks < 16; ++ks) {
+        const int rr = 4 * ks + (lane >> 4);
+        const double* xr = xs + rr * kXs;
+        double bv[kMfmaCb];
+#pragma unroll
+        for (int c = 0; c < kMfmaCb; ++c)
+          bv[c] = pa[c] < 0 ? 0.0 : (wave + 4 * c == NCB ? xr[pa[c]] : xr[pa[c]] * xr[pb[c]]);
+#pragma unroll
+        for (int q4 = 0; q4 < 4; ++q4) {
+          const double aq = qi[rr * kQs + 16 * q4 + (lane & 15)];
+          const double aqr = qri[rr * kQs + 16 * q4 + (lane & 15)];
+#pragma unroll
+          for (int c = 0; c < kMfmaCb; ++c)
+            if (wave + 4 * c <= NCB)
+              acc[q4][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(wave + 4 * c == NCB ? aqr : aq, bv[c], acc[q4][c], 0,
+                                                                0, 0);
+        }
+      }
+      __syncthreads();
+    }
+  // partials: pairs and X'Q r from the MFMA accumulators, gap / objective from phase 1
+  double* P = a.partial + ((size_t)slot * (a.nch[0] + a.nch[1]) + gch) * a.S_pad * NV;
+#pragma unroll
+  for (int c = 0; c < kMfmaCb; ++c) {
+    const int cb = wave + 4 * c;
+    if (cb > NCB) continue;
+    const int col = cb * 16 + (lane & 15);
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const size_t fit = (size_t)fb * 64 + 16 * q4 + (lane >> 4) + 4 * r;
+        if (cb < NCB && col < NP) P[fit * NV + col] = acc[q4][c][r];
+        if (cb == NCB && (lane & 15) < K) P[fit * NV + NP + (lane & 15)] = acc[q4][c][r];
+      }
+  }
+  red[0][wave][lane] = gap;
+  red[1][wave][lane] = obj;
+  __syncthreads();
+  if (wave == 0) {
+    const size_t fit = (size_t)fb * 64 + lane;
+    P[fit * NV + NP + K] = ((red[0][0][lane] + red[0][1][lane]) + red[0][2][lane]) + red[0][3][lane];
+    P[fit * NV + NP + K + 1] = ((red[1][0][lane] + red[1][1][lane]) + red[1][2][lane]) + red[1][3][lane];
+  }
 }
 
 // Per-row affine direction from the current state (shared by mm_affine / mm_final).
@@ -211,12 +327,12 @@ struct Affine {
 };
 
 template <int K>
-__device__ __forceinline__ Affine affine_row(const MmArgs& a, size_t si, double c, const double (&xr)[K], double y,
-                                             const double (&beta)[K], const double (&dba)[K]) {
+__device__ __forceinline__ Affine affine_row(double xv, double zv, double wv, double c, const double (&xr)[K],
+                                             double y, const double (&beta)[K], const double (&dba)[K]) {
   Affine f;
-  f.xv = a.x[si];
-  f.zv = a.z[si];
-  f.wv = a.w[si];
+  f.xv = xv;
+  f.zv = zv;
+  f.wv = wv;
   f.sv = c - f.xv;
   double xb = 0.0, xd = 0.0;
 #pragma unroll
@@ -230,6 +346,31 @@ __device__ __forceinline__ Affine affine_row(const MmArgs& a, size_t si, double 
   f.dza = -f.zv - f.zv * f.dxa / f.xv;
   f.dwa = -f.wv + f.wv * f.dxa / f.sv;
   return f;
+}
+
+// One row's inputs for the affine / final passes, loaded a row ahead (software prefetch: the loads
+// of row i + 1 are issued before row i's stores, which the compiler could not reorder itself).
+template <int K>
+struct RowIn {
+  double xr[K], y, xv, zv, wv;
+  uint32_t cu;
+};
+
+template <int K>
+__device__ __forceinline__ void load_row(const MmArgs& a, const Work& wk, const double* X, int64_t ld, size_t sb,
+                                         bool live, uint32_t row, RowIn<K>& in) {
+  in.cu = row_count(a, wk.slot, wk.g, row);
+  in.xr[0] = 1.0;
+#pragma unroll
+  for (int k = 1; k < K; ++k) in.xr[k] = X[(size_t)(k - 1) * ld + row];
+  in.y = X[(size_t)a.p * ld + row];
+  in.xv = in.zv = in.wv = 0.0;
+  if (live) {
+    const size_t si = sb + (size_t)row * a.S_pad;
+    in.xv = a.x[si];
+    in.zv = a.z[si];
+    in.wv = a.w[si];
+  }
 }
 
 // [0] primal step bound, [1] dual step bound, [2..4] mu_aff terms, then X'q rho0, X'q rho1.
@@ -254,17 +395,15 @@ __global__ __launch_bounds__(64) void mm_affine_kernel(const MmArgs a) {
   const uint32_t n = a.n[wk.g];
   const size_t sb = ((size_t)wk.slot * a.rep_rows + (wk.g ? a.n[0] : 0u)) * a.S_pad + wk.s;
   const uint32_t r0 = wk.ch * kRc, r1 = min(n, r0 + kRc);
-  if (__any(live))
+  if (__any(live) && r0 < r1) {
+    RowIn<K> nxt;
+    load_row<K>(a, wk, X, ld, sb, live, r0, nxt);
     for (uint32_t row = r0; row < r1; ++row) {
-      const uint32_t cu = row_count(a, wk.slot, wk.g, row);
-      if (cu == 0) continue;
-      double xr[K];
-      xr[0] = 1.0;
-#pragma unroll
-      for (int k = 1; k < K; ++k) xr[k] = X[(size_t)(k - 1) * ld + row];
-      const double y = X[(size_t)a.p * ld + row];
-      if (!live) continue;
-      const Affine f = affine_row<K>(a, sb + (size_t)row * a.S_pad, (double)cu, xr, y, beta, dba);
+      const RowIn<K> cur = nxt;
+      if (row + 1 < r1) load_row<K>(a, wk, X, ld, sb, live, row + 1, nxt);
+      if (cur.cu == 0 || !live) continue;
+      const Affine f = affine_row<K>(cur.xv, cur.zv, cur.wv, (double)cur.cu, cur.xr, cur.y, beta, dba);
+      const double(&xr)[K] = cur.xr;
       if (f.dxa < 0.0) acc[0] = fmin(acc[0], -f.xv / f.dxa);
       if (f.dxa > 0.0) acc[0] = fmin(acc[0], f.sv / f.dxa);
       if (f.dza < 0.0) acc[1] = fmin(acc[1], -f.zv / f.dza);
@@ -280,6 +419,7 @@ __global__ __launch_bounds__(64) void mm_affine_kernel(const MmArgs a) {
         acc[5 + K + k] += q1 * xr[k];
       }
     }
+  }
   double* P = partial_row(a, wk, NV);
 #pragma unroll
   for (int i = 0; i < NV; ++i) P[i] = acc[i];
@@ -305,18 +445,16 @@ __global__ __launch_bounds__(64) void mm_final_kernel(const MmArgs a) {
   const uint32_t n = a.n[wk.g];
   const size_t sb = ((size_t)wk.slot * a.rep_rows + (wk.g ? a.n[0] : 0u)) * a.S_pad + wk.s;
   const uint32_t r0 = wk.ch * kRc, r1 = min(n, r0 + kRc);
-  if (__any(live))
+  if (__any(live) && r0 < r1) {
+    RowIn<K> nxt;
+    load_row<K>(a, wk, X, ld, sb, live, r0, nxt);
     for (uint32_t row = r0; row < r1; ++row) {
-      const uint32_t cu = row_count(a, wk.slot, wk.g, row);
-      if (cu == 0) continue;
-      double xr[K];
-      xr[0] = 1.0;
-#pragma unroll
-      for (int k = 1; k < K; ++k) xr[k] = X[(size_t)(k - 1) * ld + row];
-      const double y = X[(size_t)a.p * ld + row];
-      if (!live) continue;
+      const RowIn<K> cur = nxt;
+      if (row + 1 < r1) load_row<K>(a, wk, X, ld, sb, live, row + 1, nxt);
+      if (cur.cu == 0 || !live) continue;
       const size_t si = sb + (size_t)row * a.S_pad;
-      const Affine f = affine_row<K>(a, si, (double)cu, xr, y, beta, dba);
+      const Affine f = affine_row<K>(cur.xv, cur.zv, cur.wv, (double)cur.cu, cur.xr, cur.y, beta, dba);
+      const double(&xr)[K] = cur.xr;
       const double rho = f.r - f.dxa * (f.dwa / f.sv + f.dza / f.xv) + sigmu * (1.0 / f.xv - 1.0 / f.sv);
       double xd = 0.0;
 #pragma unroll
@@ -334,6 +472,7 @@ __global__ __launch_bounds__(64) void mm_final_kernel(const MmArgs a) {
       if (dz < 0.0) bd = fmin(bd, -f.zv / dz);
       if (dw < 0.0) bd = fmin(bd, -f.wv / dw);
     }
+  }
   double* P = partial_row(a, wk, 2);
   P[0] = bp;
   P[1] = bd;
@@ -645,7 +784,7 @@ __global__ __launch_bounds__(256) void mm_finish_kernel(const MmArgs a, int K, i
 template <int K>
 struct Kernels {
   static void assemble(const MmArgs& a, dim3 grid, int mode, hipStream_t s) {
-    hipLaunchKernelGGL(mm_assemble_kernel<K>, grid, dim3(64), 0, s, a, mode);
+    hipLaunchKernelGGL(mm_assemble_mfma_kernel<K>, grid, dim3(256), 0, s, a, mode);
   }
   static void affine(const MmArgs& a, dim3 grid, hipStream_t s) {
     hipLaunchKernelGGL(mm_affine_kernel<K>, grid, dim3(64), 0, s, a);
