@@ -99,26 +99,6 @@ __device__ __forceinline__ uint32_t row_count(const MmArgs& a, uint32_t slot, ui
   return (word >> ((row & 3u) * 8u)) & 255u;
 }
 
-struct Work {
-  uint32_t g, ch, gch, slot;
-  int s, lane;
-};
-
-__device__ __forceinline__ Work work(const MmArgs& a) {
-  Work w;
-  w.lane = threadIdx.x;
-  w.gch = blockIdx.x;
-  w.g = w.gch >= a.nch[0] ? 1u : 0u;
-  w.ch = w.gch - (w.g ? a.nch[0] : 0u);
-  w.slot = blockIdx.z;
-  w.s = blockIdx.y * 64 + w.lane;
-  return w;
-}
-
-__device__ __forceinline__ double* partial_row(const MmArgs& a, const Work& w, int nv) {
-  return a.partial + (((size_t)w.slot * (a.nch[0] + a.nch[1]) + w.gch) * a.S_pad + w.s) * nv;
-}
-
 // mm_assemble: mode 0: weighted OLS of the replicate (q = c, rho = y) -> M, X'Cy, sum c y^2, n_act;
 // mode 1: start point (x = (1 - tau) c, z/w from the OLS residual) + assemble; mode 2: apply the
 // last step (x += ap dx, z += ad dz, w += ad dw) + assemble.
@@ -263,7 +243,7 @@ __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a
             a.z[si] = zv;
             a.w[si] = wv;
             const double sv = c - xv;
-            q = 1.0 / (zv / xv + wv / sv);
+            q = xv * sv / (zv * sv + wv * xv);  // 1 / (z/x + w/s)
             qr = q * r;  // rho_aff = r_d + w - z = y - X beta
             gap += xv * zv + sv * wv;
             obj += y * xv;
@@ -323,7 +303,7 @@ __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a
 
 // Per-row affine direction from the current state (shared by mm_affine / mm_final).
 struct Affine {
-  double xv, zv, wv, sv, q, r, dxa, dza, dwa;
+  double xv, zv, wv, sv, ix, is, q, r, dxa, dza, dwa;  // ix = 1/x, is = 1/s (divisions shared)
 };
 
 template <int K>
@@ -341,141 +321,221 @@ __device__ __forceinline__ Affine affine_row(double xv, double zv, double wv, do
     xd += xr[k] * dba[k];
   }
   f.r = y - xb;
-  f.q = 1.0 / (f.zv / f.xv + f.wv / f.sv);
+  f.ix = 1.0 / f.xv;
+  f.is = 1.0 / f.sv;
+  f.q = 1.0 / (f.zv * f.ix + f.wv * f.is);
   f.dxa = f.q * (f.r - xd);
-  f.dza = -f.zv - f.zv * f.dxa / f.xv;
-  f.dwa = -f.wv + f.wv * f.dxa / f.sv;
+  f.dza = -f.zv - f.zv * f.dxa * f.ix;
+  f.dwa = -f.wv + f.wv * f.dxa * f.is;
   return f;
 }
 
-// One row's inputs for the affine / final passes, loaded a row ahead (software prefetch: the loads
-// of row i + 1 are issued before row i's stores, which the compiler could not reorder itself).
-template <int K>
-struct RowIn {
-  double xr[K], y, xv, zv, wv;
-  uint32_t cu;
+// Shared shape of the affine / final passes: block = 4 waves on the same 64 fits (fit = lane),
+// each wave every fourth row of a 64-row sub-tile whose design values are staged in LDS (broadcast
+// reads), the state of the wave's next row with a nonzero count loaded before this row's work,
+// per-thread accumulators reduced over the 4 waves in a fixed order at the end.
+struct PassCtx {
+  uint32_t g, ch, gch, slot, fb;
+  int lane, wave, s;
+  size_t F, sb;
+  bool live;
+  const double* X;
+  int64_t ld;
+  uint32_t r0, r1;
 };
 
+__device__ __forceinline__ PassCtx pass_ctx(const MmArgs& a) {
+  PassCtx c;
+  c.lane = threadIdx.x & 63;
+  c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  c.gch = blockIdx.x;
+  c.fb = blockIdx.y;
+  c.slot = blockIdx.z;
+  c.g = c.gch >= a.nch[0] ? 1u : 0u;
+  c.ch = c.gch - (c.g ? a.nch[0] : 0u);
+  c.s = (int)c.fb * 64 + c.lane;
+  c.F = fit_index(a, c.slot, c.g, c.s);
+  c.live = c.s < a.S && !(a.fstat[c.F] & (kDone | kFailed));
+  c.X = a.cols[c.g];
+  c.ld = a.ld[c.g];
+  c.sb = ((size_t)c.slot * a.rep_rows + (c.g ? a.n[0] : 0u)) * a.S_pad + c.s;
+  c.r0 = c.ch * kRc;
+  c.r1 = min(a.n[c.g], c.r0 + kRc);
+  return c;
+}
+
+// Stage rows [t0, t0 + 64) as [1, x_1..x_{K-1}, 0.., y at kXs - 1] (zeros past the chunk).
 template <int K>
-__device__ __forceinline__ void load_row(const MmArgs& a, const Work& wk, const double* X, int64_t ld, size_t sb,
-                                         bool live, uint32_t row, RowIn<K>& in) {
-  in.cu = row_count(a, wk.slot, wk.g, row);
-  in.xr[0] = 1.0;
-#pragma unroll
-  for (int k = 1; k < K; ++k) in.xr[k] = X[(size_t)(k - 1) * ld + row];
-  in.y = X[(size_t)a.p * ld + row];
-  in.xv = in.zv = in.wv = 0.0;
-  if (live) {
-    const size_t si = sb + (size_t)row * a.S_pad;
-    in.xv = a.x[si];
-    in.zv = a.z[si];
-    in.wv = a.w[si];
+__device__ __forceinline__ void stage_rows(const MmArgs& a, const PassCtx& c, uint32_t t0, uint32_t nr, double* xs) {
+  for (int i = threadIdx.x; i < 64 * kXs; i += blockDim.x) {
+    const int rr = i / kXs, col = i % kXs;
+    double v = 0.0;
+    if ((uint32_t)rr < nr) {
+      if (col == 0)
+        v = 1.0;
+      else if (col < K)
+        v = c.X[(size_t)(col - 1) * c.ld + t0 + rr];
+      else if (col == kXs - 1)
+        v = c.X[(size_t)a.p * c.ld + t0 + rr];
+    }
+    xs[i] = v;
   }
 }
 
+// Fixed-order sum (or min for i < n_min) of acc over the 4 waves into wave 0 (red: 64 x (N + 1)).
+template <int N>
+__device__ __forceinline__ void waves_reduce(double (&acc)[N], double* red, int wave, int lane, int n_min) {
+#pragma unroll 1
+  for (int w = 3; w >= 1; --w) {
+    if (wave == w)
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        double* r = red + lane * (N + 1) + i;
+        *r = w == 3 ? acc[i] : (i < n_min ? fmin(*r, acc[i]) : *r + acc[i]);
+      }
+    __syncthreads();
+  }
+  if (wave == 0)
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const double r = red[lane * (N + 1) + i];
+      acc[i] = i < n_min ? fmin(r, acc[i]) : r + acc[i];
+    }
+}
+
+// The next row's count and state (x, z, w) for the affine / final passes (a 4-deep ring of rows
+// measured no faster than this one row of prefetch).
+constexpr int kPrefetch = 1;
+struct StateRing {
+  uint32_t cu[kPrefetch];
+  double x[kPrefetch], z[kPrefetch], w[kPrefetch];
+  __device__ __forceinline__ void load(const MmArgs& a, const PassCtx& c, uint32_t t0, uint32_t nr, int rr, int k) {
+    cu[k] = (uint32_t)rr < nr ? row_count(a, c.slot, c.g, t0 + rr) : 0u;
+    x[k] = z[k] = w[k] = 0.0;
+    if (cu[k] && c.live) {
+      const size_t si = c.sb + (size_t)(t0 + rr) * a.S_pad;
+      x[k] = a.x[si];
+      z[k] = a.z[si];
+      w[k] = a.w[si];
+    }
+  }
+};
+
 // [0] primal step bound, [1] dual step bound, [2..4] mu_aff terms, then X'q rho0, X'q rho1.
 template <int K>
-__global__ __launch_bounds__(64) void mm_affine_kernel(const MmArgs a) {
+__global__ __launch_bounds__(256, 2) void mm_affine_kernel(const MmArgs a) {
   constexpr int NV = 5 + 2 * K;
-  const Work wk = work(a);
-  const size_t F = fit_index(a, wk.slot, wk.g, wk.s);
-  const bool live = wk.s < a.S && !(a.fstat[F] & (kDone | kFailed));
+  __shared__ double xs[64 * kXs];
+  __shared__ double red[64 * (NV + 1)];
+  const PassCtx c = pass_ctx(a);
   double beta[K], dba[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    beta[k] = live ? a.beta[F * K + k] : 0.0;
-    dba[k] = live ? a.dba[F * K + k] : 0.0;
+    beta[k] = c.live ? a.beta[c.F * K + k] : 0.0;
+    dba[k] = c.live ? a.dba[c.F * K + k] : 0.0;
   }
   double acc[NV];
   acc[0] = acc[1] = 1e300;
 #pragma unroll
   for (int i = 2; i < NV; ++i) acc[i] = 0.0;
-  const double* X = a.cols[wk.g];
-  const int64_t ld = a.ld[wk.g];
-  const uint32_t n = a.n[wk.g];
-  const size_t sb = ((size_t)wk.slot * a.rep_rows + (wk.g ? a.n[0] : 0u)) * a.S_pad + wk.s;
-  const uint32_t r0 = wk.ch * kRc, r1 = min(n, r0 + kRc);
-  if (__any(live) && r0 < r1) {
-    RowIn<K> nxt;
-    load_row<K>(a, wk, X, ld, sb, live, r0, nxt);
-    for (uint32_t row = r0; row < r1; ++row) {
-      const RowIn<K> cur = nxt;
-      if (row + 1 < r1) load_row<K>(a, wk, X, ld, sb, live, row + 1, nxt);
-      if (cur.cu == 0 || !live) continue;
-      const Affine f = affine_row<K>(cur.xv, cur.zv, cur.wv, (double)cur.cu, cur.xr, cur.y, beta, dba);
-      const double(&xr)[K] = cur.xr;
-      if (f.dxa < 0.0) acc[0] = fmin(acc[0], -f.xv / f.dxa);
-      if (f.dxa > 0.0) acc[0] = fmin(acc[0], f.sv / f.dxa);
-      if (f.dza < 0.0) acc[1] = fmin(acc[1], -f.zv / f.dza);
-      if (f.dwa < 0.0) acc[1] = fmin(acc[1], -f.wv / f.dwa);
-      acc[2] += f.xv * f.dza + f.sv * f.dwa;
-      acc[3] += f.zv * f.dxa - f.wv * f.dxa;
-      acc[4] += f.dxa * f.dza - f.dxa * f.dwa;
-      const double q0 = f.q * (f.r - f.dxa * (f.dwa / f.sv + f.dza / f.xv));
-      const double q1 = f.q * (1.0 / f.xv - 1.0 / f.sv);
+  if (__syncthreads_or(c.live))
+    for (uint32_t t0 = c.r0; t0 < c.r1; t0 += 64) {
+      const uint32_t nr = min(64u, c.r1 - t0);
+      stage_rows<K>(a, c, t0, nr, xs);
+      __syncthreads();
+      // the state of the wave's next row is loaded before this row's work (software prefetch)
+      StateRing ring;
+      ring.load(a, c, t0, nr, c.wave, 0);
+      for (int rr = c.wave; rr < 64; rr += 4) {
+        const uint32_t cu = ring.cu[0];
+        const double xv = ring.x[0], zv = ring.z[0], wv = ring.w[0];
+        ring.load(a, c, t0, nr, rr + 4, 0);
+        if (!cu || !c.live) continue;
+        double xr[K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) {
-        acc[5 + k] += q0 * xr[k];
-        acc[5 + K + k] += q1 * xr[k];
+        for (int k = 0; k < K; ++k) xr[k] = xs[rr * kXs + k];
+        const Affine f = affine_row<K>(xv, zv, wv, (double)cu, xr, xs[rr * kXs + kXs - 1], beta, dba);
+        if (f.dxa != 0.0) acc[0] = fmin(acc[0], (f.dxa < 0.0 ? -f.xv : f.sv) / f.dxa);
+        if (f.dza < 0.0) acc[1] = fmin(acc[1], -f.zv / f.dza);
+        if (f.dwa < 0.0) acc[1] = fmin(acc[1], -f.wv / f.dwa);
+        acc[2] += f.xv * f.dza + f.sv * f.dwa;
+        acc[3] += f.zv * f.dxa - f.wv * f.dxa;
+        acc[4] += f.dxa * f.dza - f.dxa * f.dwa;
+        const double q0 = f.q * (f.r - f.dxa * (f.dwa * f.is + f.dza * f.ix));
+        const double q1 = f.q * (f.ix - f.is);
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          acc[5 + k] += q0 * xr[k];
+          acc[5 + K + k] += q1 * xr[k];
+        }
       }
+      __syncthreads();
     }
-  }
-  double* P = partial_row(a, wk, NV);
+  waves_reduce<NV>(acc, red, c.wave, c.lane, 2);
+  if (c.wave == 0) {
+    double* P = a.partial + (((size_t)c.slot * (a.nch[0] + a.nch[1]) + c.gch) * a.S_pad + c.s) * NV;
 #pragma unroll
-  for (int i = 0; i < NV; ++i) P[i] = acc[i];
+    for (int i = 0; i < NV; ++i) P[i] = acc[i];
+  }
 }
 
 // Corrector direction (stored for the next assemble) and its step-length bounds.
 template <int K>
-__global__ __launch_bounds__(64) void mm_final_kernel(const MmArgs a) {
-  const Work wk = work(a);
-  const size_t F = fit_index(a, wk.slot, wk.g, wk.s);
-  const bool live = wk.s < a.S && !(a.fstat[F] & (kDone | kFailed));
+__global__ __launch_bounds__(256, 2) void mm_final_kernel(const MmArgs a) {
+  __shared__ double xs[64 * kXs];
+  __shared__ double red[64 * 3];
+  const PassCtx c = pass_ctx(a);
   double beta[K], dba[K], db[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    beta[k] = live ? a.beta[F * K + k] : 0.0;
-    dba[k] = live ? a.dba[F * K + k] : 0.0;
-    db[k] = live ? a.db[F * K + k] : 0.0;
+    beta[k] = c.live ? a.beta[c.F * K + k] : 0.0;
+    dba[k] = c.live ? a.dba[c.F * K + k] : 0.0;
+    db[k] = c.live ? a.db[c.F * K + k] : 0.0;
   }
-  const double sigmu = live ? a.fs[F * kFs + FS_SIGMU] : 0.0;
-  double bp = 1e300, bd = 1e300;
-  const double* X = a.cols[wk.g];
-  const int64_t ld = a.ld[wk.g];
-  const uint32_t n = a.n[wk.g];
-  const size_t sb = ((size_t)wk.slot * a.rep_rows + (wk.g ? a.n[0] : 0u)) * a.S_pad + wk.s;
-  const uint32_t r0 = wk.ch * kRc, r1 = min(n, r0 + kRc);
-  if (__any(live) && r0 < r1) {
-    RowIn<K> nxt;
-    load_row<K>(a, wk, X, ld, sb, live, r0, nxt);
-    for (uint32_t row = r0; row < r1; ++row) {
-      const RowIn<K> cur = nxt;
-      if (row + 1 < r1) load_row<K>(a, wk, X, ld, sb, live, row + 1, nxt);
-      if (cur.cu == 0 || !live) continue;
-      const size_t si = sb + (size_t)row * a.S_pad;
-      const Affine f = affine_row<K>(cur.xv, cur.zv, cur.wv, (double)cur.cu, cur.xr, cur.y, beta, dba);
-      const double(&xr)[K] = cur.xr;
-      const double rho = f.r - f.dxa * (f.dwa / f.sv + f.dza / f.xv) + sigmu * (1.0 / f.xv - 1.0 / f.sv);
-      double xd = 0.0;
+  const double sigmu = c.live ? a.fs[c.F * kFs + FS_SIGMU] : 0.0;
+  double acc[2] = {1e300, 1e300};
+  if (__syncthreads_or(c.live))
+    for (uint32_t t0 = c.r0; t0 < c.r1; t0 += 64) {
+      const uint32_t nr = min(64u, c.r1 - t0);
+      stage_rows<K>(a, c, t0, nr, xs);
+      __syncthreads();
+      // the state of the wave's next row is loaded before this row's work (software prefetch)
+      StateRing ring;
+      ring.load(a, c, t0, nr, c.wave, 0);
+      for (int rr = c.wave; rr < 64; rr += 4) {
+        const uint32_t cu = ring.cu[0];
+        const double xv = ring.x[0], zv = ring.z[0], wv = ring.w[0];
+        ring.load(a, c, t0, nr, rr + 4, 0);
+        if (!cu || !c.live) continue;
+        double xr[K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) xd += xr[k] * db[k];
-      const double dx = f.q * (rho - xd);
-      const double rxz = sigmu - f.xv * f.zv - f.dxa * f.dza;
-      const double rsw = sigmu - f.sv * f.wv + f.dxa * f.dwa;
-      const double dz = (rxz - f.zv * dx) / f.xv;
-      const double dw = (rsw + f.wv * dx) / f.sv;
-      a.dx[si] = dx;
-      a.dz[si] = dz;
-      a.dw[si] = dw;
-      if (dx < 0.0) bp = fmin(bp, -f.xv / dx);
-      if (dx > 0.0) bp = fmin(bp, f.sv / dx);
-      if (dz < 0.0) bd = fmin(bd, -f.zv / dz);
-      if (dw < 0.0) bd = fmin(bd, -f.wv / dw);
+        for (int k = 0; k < K; ++k) xr[k] = xs[rr * kXs + k];
+        const Affine f = affine_row<K>(xv, zv, wv, (double)cu, xr, xs[rr * kXs + kXs - 1], beta, dba);
+        const double rho = f.r - f.dxa * (f.dwa * f.is + f.dza * f.ix) + sigmu * (f.ix - f.is);
+        double xd = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) xd += xr[k] * db[k];
+        const double dx = f.q * (rho - xd);
+        const double rxz = sigmu - f.xv * f.zv - f.dxa * f.dza;
+        const double rsw = sigmu - f.sv * f.wv + f.dxa * f.dwa;
+        const double dz = (rxz - f.zv * dx) * f.ix;
+        const double dw = (rsw + f.wv * dx) * f.is;
+        const size_t si = c.sb + (size_t)(t0 + rr) * a.S_pad;
+        a.dx[si] = dx;
+        a.dz[si] = dz;
+        a.dw[si] = dw;
+        if (dx != 0.0) acc[0] = fmin(acc[0], (dx < 0.0 ? -f.xv : f.sv) / dx);
+        if (dz < 0.0) acc[1] = fmin(acc[1], -f.zv / dz);
+        if (dw < 0.0) acc[1] = fmin(acc[1], -f.wv / dw);
+      }
+      __syncthreads();
     }
+  waves_reduce<2>(acc, red, c.wave, c.lane, 2);
+  if (c.wave == 0) {
+    double* P = a.partial + (((size_t)c.slot * (a.nch[0] + a.nch[1]) + c.gch) * a.S_pad + c.s) * 2;
+    P[0] = acc[0];
+    P[1] = acc[1];
   }
-  double* P = partial_row(a, wk, 2);
-  P[0] = bp;
-  P[1] = bd;
 }
 
 // Chunk partials -> per-fit values, chunks in a fixed order; the first n_min values are minima.
@@ -787,10 +847,10 @@ struct Kernels {
     hipLaunchKernelGGL(mm_assemble_mfma_kernel<K>, grid, dim3(256), 0, s, a, mode);
   }
   static void affine(const MmArgs& a, dim3 grid, hipStream_t s) {
-    hipLaunchKernelGGL(mm_affine_kernel<K>, grid, dim3(64), 0, s, a);
+    hipLaunchKernelGGL(mm_affine_kernel<K>, grid, dim3(256), 0, s, a);
   }
   static void final_(const MmArgs& a, dim3 grid, hipStream_t s) {
-    hipLaunchKernelGGL(mm_final_kernel<K>, grid, dim3(64), 0, s, a);
+    hipLaunchKernelGGL(mm_final_kernel<K>, grid, dim3(256), 0, s, a);
   }
 };
 
