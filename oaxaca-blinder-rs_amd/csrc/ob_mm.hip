@@ -99,6 +99,24 @@ __device__ __forceinline__ uint32_t row_count(const MmArgs& a, uint32_t slot, ui
   return (word >> ((row & 3u) * 8u)) & 255u;
 }
 
+// The replicate's 16 count words of the 64-row sub-tile at t0 (byte (i & 3) of word i >> 2 = row
+// t0 + i), staged once per sub-tile so a row's count is an LDS broadcast read (threads 0..15).
+__device__ __forceinline__ void stage_counts(const MmArgs& a, uint32_t slot, uint32_t g, uint32_t t0, uint32_t* cw) {
+  if (threadIdx.x >= 16) return;
+  if (!a.counts) {
+    cw[threadIdx.x] = 0x01010101u;
+    return;
+  }
+  const uint32_t pos = a.seg0 + slot;
+  const size_t tt = (g ? a.tiles0 : 0u) + (t0 >> 8);
+  cw[threadIdx.x] = a.counts[((tt * a.nb_rep + (pos >> 6)) * 4 + ((t0 & 255u) >> 6)) * kCimgWords +
+                             (pos & 63u) * kCimgStride + threadIdx.x];
+}
+
+__device__ __forceinline__ uint32_t staged_count(const uint32_t* cw, int rr, uint32_t nr) {
+  return (uint32_t)rr < nr ? (cw[rr >> 2] >> ((rr & 3) * 8)) & 255u : 0u;
+}
+
 // mm_assemble: mode 0: weighted OLS of the replicate (q = c, rho = y) -> M, X'Cy, sum c y^2, n_act;
 // mode 1: start point (x = (1 - tau) c, z/w from the OLS residual) + assemble; mode 2: apply the
 // last step (x += ap dx, z += ad dz, w += ad dw) + assemble.
@@ -120,6 +138,7 @@ __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a
   __shared__ double qi[64 * kQs];
   __shared__ double qri[64 * kQs];
   __shared__ double red[2][4][64];
+  __shared__ uint32_t cws[16];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint32_t gch = blockIdx.x, fb = blockIdx.y, slot = blockIdx.z;
@@ -191,6 +210,7 @@ __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a
         }
         xs[i] = v;
       }
+      stage_counts(a, slot, g, t0, cws);
       __syncthreads();
       // phase 1: rows wave, wave + 4, ... of the sub-tile for fit `lane`; the state of the next
       // row is loaded before this row's stores (software prefetch)
@@ -213,7 +233,7 @@ __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a
         load_state(rr + 4);
         double q = 0.0, qr = 0.0;
         const uint32_t row = t0 + rr;
-        const uint32_t cu = (uint32_t)rr < nr ? row_count(a, slot, g, row) : 0u;
+        const uint32_t cu = staged_count(cws, rr, nr);
         if (cu != 0 && live) {
           const double c = (double)cu;
           const double* xr = xs + rr * kXs;
@@ -409,8 +429,9 @@ constexpr int kPrefetch = 1;
 struct StateRing {
   uint32_t cu[kPrefetch];
   double x[kPrefetch], z[kPrefetch], w[kPrefetch];
-  __device__ __forceinline__ void load(const MmArgs& a, const PassCtx& c, uint32_t t0, uint32_t nr, int rr, int k) {
-    cu[k] = (uint32_t)rr < nr ? row_count(a, c.slot, c.g, t0 + rr) : 0u;
+  __device__ __forceinline__ void load(const MmArgs& a, const PassCtx& c, const uint32_t* cws, uint32_t t0,
+                                      uint32_t nr, int rr, int k) {
+    cu[k] = staged_count(cws, rr, nr);
     x[k] = z[k] = w[k] = 0.0;
     if (cu[k] && c.live) {
       const size_t si = c.sb + (size_t)(t0 + rr) * a.S_pad;
@@ -427,6 +448,7 @@ __global__ __launch_bounds__(256, 2) void mm_affine_kernel(const MmArgs a) {
   constexpr int NV = 5 + 2 * K;
   __shared__ double xs[64 * kXs];
   __shared__ double red[64 * (NV + 1)];
+  __shared__ uint32_t cws[16];
   const PassCtx c = pass_ctx(a);
   double beta[K], dba[K];
 #pragma unroll
@@ -442,14 +464,15 @@ __global__ __launch_bounds__(256, 2) void mm_affine_kernel(const MmArgs a) {
     for (uint32_t t0 = c.r0; t0 < c.r1; t0 += 64) {
       const uint32_t nr = min(64u, c.r1 - t0);
       stage_rows<K>(a, c, t0, nr, xs);
+      stage_counts(a, c.slot, c.g, t0, cws);
       __syncthreads();
       // the state of the wave's next row is loaded before this row's work (software prefetch)
       StateRing ring;
-      ring.load(a, c, t0, nr, c.wave, 0);
+      ring.load(a, c, cws, t0, nr, c.wave, 0);
       for (int rr = c.wave; rr < 64; rr += 4) {
         const uint32_t cu = ring.cu[0];
         const double xv = ring.x[0], zv = ring.z[0], wv = ring.w[0];
-        ring.load(a, c, t0, nr, rr + 4, 0);
+        ring.load(a, c, cws, t0, nr, rr + 4, 0);
         if (!cu || !c.live) continue;
         double xr[K];
 #pragma unroll
@@ -484,6 +507,7 @@ template <int K>
 __global__ __launch_bounds__(256, 2) void mm_final_kernel(const MmArgs a) {
   __shared__ double xs[64 * kXs];
   __shared__ double red[64 * 3];
+  __shared__ uint32_t cws[16];
   const PassCtx c = pass_ctx(a);
   double beta[K], dba[K], db[K];
 #pragma unroll
@@ -498,14 +522,15 @@ __global__ __launch_bounds__(256, 2) void mm_final_kernel(const MmArgs a) {
     for (uint32_t t0 = c.r0; t0 < c.r1; t0 += 64) {
       const uint32_t nr = min(64u, c.r1 - t0);
       stage_rows<K>(a, c, t0, nr, xs);
+      stage_counts(a, c.slot, c.g, t0, cws);
       __syncthreads();
       // the state of the wave's next row is loaded before this row's work (software prefetch)
       StateRing ring;
-      ring.load(a, c, t0, nr, c.wave, 0);
+      ring.load(a, c, cws, t0, nr, c.wave, 0);
       for (int rr = c.wave; rr < 64; rr += 4) {
         const uint32_t cu = ring.cu[0];
         const double xv = ring.x[0], zv = ring.z[0], wv = ring.w[0];
-        ring.load(a, c, t0, nr, rr + 4, 0);
+        ring.load(a, c, cws, t0, nr, rr + 4, 0);
         if (!cu || !c.live) continue;
         double xr[K];
 #pragma unroll
