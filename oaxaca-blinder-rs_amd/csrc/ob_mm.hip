@@ -77,6 +77,8 @@ struct MmArgs {
   unsigned long long* active_rows;   // live (fit, row) pairs of the next passes
   uint32_t* tprefix;                 // [slot][group][tiles + 1] (finish kernel scratch)
   uint32_t* lane_of;                 // [slot][group][simulation] -> fit lane (lanes in ascending tau)
+  uint32_t* rowlist;                 // [slot][chunk (A then B)][kRc] nonzero-count rows (mm_rows_kernel)
+  uint32_t* nrows;                   // [slot][chunk] list lengths
   uint32_t key0, key1;
   int n_q;
   const double* quantiles;
@@ -99,225 +101,271 @@ __device__ __forceinline__ uint32_t row_count(const MmArgs& a, uint32_t slot, ui
   return (word >> ((row & 3u) * 8u)) & 255u;
 }
 
-// The replicate's 16 count words of the 64-row sub-tile at t0 (byte (i & 3) of word i >> 2 = row
-// t0 + i), staged once per sub-tile so a row's count is an LDS broadcast read (threads 0..15).
-__device__ __forceinline__ void stage_counts(const MmArgs& a, uint32_t slot, uint32_t g, uint32_t t0, uint32_t* cw) {
-  if (threadIdx.x >= 16) return;
-  if (!a.counts) {
-    cw[threadIdx.x] = 0x01010101u;
-    return;
+// Each pass walks a chunk's rows through a list of the replicate's nonzero-count rows
+// (mm_rows_kernel, once per batch: the counts do not change across iterations). Block = 4
+// waves x 16 fits (fit = lane & 15) on one chunk; a wave step takes 4 list rows (row = lane >> 4),
+// so a lane holds one (fit, row) pair per step -- the A-fragment layout of v_mfma_f64_16x16x4
+// (m = fit, k = row), and X'QX / X'Q r / X'q rho are MFMAs with B = the rows' pair products or
+// values from LDS. The rows' design values are gathered 64 list rows at a time into
+// double-buffered LDS (loaded one sub-tile ahead); the (fit, row) state streams into registers
+// kRing steps ahead of use, across sub-tile seams.
+constexpr int kXs = 18;     // LDS stride of a staged row: [1, x_1..x_p, 0.., y at 16, 0 at 17]
+constexpr int kXy = 16, kXzero = 17;
+constexpr int kSub = 64;    // list rows per staged sub-tile (16 wave steps of 4 rows)
+constexpr int kRing = 4;    // wave steps of state in flight (affine / final)
+constexpr int kRingA = 2;   // the same for the assemble pass (6 state values per step)
+constexpr int kStoreAt = 4; // step after which the next sub-tile's staged values are written
+constexpr int kStage = (kSub * kXs + 255) / 256;  // staging values per thread
+typedef double mm_d4 __attribute__((ext_vector_type(4)));
+static_assert(kRc % 256 == 0 && kRc / 256 == 8, "mm_rows_kernel: 8 rows per thread");
+static_assert(16 % kRing == 0, "ring slots are static per unrolled step");
+
+// Nonzero-count rows of each (slot, chunk) in ascending order: (row - chunk start) << 8 | count.
+__global__ __launch_bounds__(256) void mm_rows_kernel(const MmArgs a) {
+  __shared__ uint32_t scan[256];
+  const uint32_t gch = blockIdx.x, slot = blockIdx.z, nch = a.nch[0] + a.nch[1];
+  const uint32_t g = gch >= a.nch[0] ? 1u : 0u;
+  const uint32_t r0 = (gch - (g ? a.nch[0] : 0u)) * kRc, nr = min(a.n[g] - r0, kRc);
+  const uint32_t i0 = threadIdx.x * 8;
+  uint32_t c[8], k = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    c[i] = i0 + i < nr ? row_count(a, slot, g, r0 + i0 + i) : 0u;
+    k += c[i] != 0u;
   }
-  const uint32_t pos = a.seg0 + slot;
-  const size_t tt = (g ? a.tiles0 : 0u) + (t0 >> 8);
-  cw[threadIdx.x] = a.counts[((tt * a.nb_rep + (pos >> 6)) * 4 + ((t0 & 255u) >> 6)) * kCimgWords +
-                             (pos & 63u) * kCimgStride + threadIdx.x];
+  scan[threadIdx.x] = k;
+  __syncthreads();
+  for (int d = 1; d < 256; d <<= 1) {  // inclusive scan of the per-thread counts
+    const uint32_t v = (int)threadIdx.x >= d ? scan[threadIdx.x - d] : 0u;
+    __syncthreads();
+    scan[threadIdx.x] += v;
+    __syncthreads();
+  }
+  uint32_t o = scan[threadIdx.x] - k;
+  uint32_t* L = a.rowlist + ((size_t)slot * nch + gch) * kRc;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    if (c[i]) L[o++] = ((i0 + i) << 8) | c[i];
+  if (threadIdx.x == 255) a.nrows[(size_t)slot * nch + gch] = scan[255];
 }
 
-__device__ __forceinline__ uint32_t staged_count(const uint32_t* cw, int rr, uint32_t nr) {
-  return (uint32_t)rr < nr ? (cw[rr >> 2] >> ((rr & 3) * 8)) & 255u : 0u;
+struct Blk {
+  uint32_t g, gch, slot, fb, r0, n_ent;
+  int wave, lane, fl, rl, s;
+  size_t F, sb;  // fit index; state index of (fit, group row 0)
+  bool live, wave_live;
+  const double* X;
+  int64_t ld;
+};
+
+// Block context; copies the chunk's row list into lst (caller syncs).
+__device__ __forceinline__ Blk blk_ctx(const MmArgs& a, uint32_t* lst, bool all_live) {
+  Blk b;
+  b.lane = threadIdx.x & 63;
+  b.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  b.fl = b.lane & 15;
+  b.rl = b.lane >> 4;
+  b.gch = blockIdx.x;
+  b.fb = blockIdx.y;
+  b.slot = blockIdx.z;
+  b.g = b.gch >= a.nch[0] ? 1u : 0u;
+  b.r0 = (b.gch - (b.g ? a.nch[0] : 0u)) * kRc;
+  b.s = (int)b.fb * 64 + b.wave * 16 + b.fl;
+  b.F = fit_index(a, b.slot, b.g, b.s);
+  b.live = all_live ? b.s < a.S_pad : (b.s < a.S && !(a.fstat[b.F] & (kDone | kFailed)));
+  b.wave_live = __ballot(b.live) != 0;
+  b.X = a.cols[b.g];
+  b.ld = a.ld[b.g];
+  b.sb = ((size_t)b.slot * a.rep_rows + (b.g ? a.n[0] : 0u)) * a.S_pad + b.s;
+  const size_t li = (size_t)b.slot * (a.nch[0] + a.nch[1]) + b.gch;
+  b.n_ent = a.nrows[li];
+  const uint32_t* L = a.rowlist + li * kRc;
+  for (uint32_t i = threadIdx.x; i < b.n_ent; i += 256) lst[i] = L[i];
+  return b;
+}
+
+// Sub-tile t's design values -> registers (unconditional loads at clamped addresses, then a
+// select: no branch around a load) ...
+template <int K>
+__device__ __forceinline__ void xs_load(const MmArgs& a, const Blk& b, const uint32_t* lst, uint32_t t,
+                                        double (&v)[kStage]) {
+#pragma unroll
+  for (int j = 0; j < kStage; ++j) {
+    const int i = threadIdx.x + 256 * j;
+    const int rr = i / kXs, col = i % kXs;
+    const uint32_t e = t * kSub + rr;
+    const bool in = i < kSub * kXs && e < b.n_ent;
+    const uint32_t row = b.r0 + (lst[min(e, b.n_ent - 1)] >> 8);
+    const int src = (col >= 1 && col < K) ? col - 1 : (col == kXy ? a.p : 0);
+    const double x = b.X[(size_t)src * b.ld + row];
+    v[j] = !in ? 0.0 : (col == 0 ? 1.0 : ((col < K || col == kXy) ? x : 0.0));
+  }
+}
+// ... -> LDS.
+__device__ __forceinline__ void xs_store(double* xs, const double (&v)[kStage]) {
+#pragma unroll
+  for (int j = 0; j < kStage; ++j) {
+    const int i = threadIdx.x + 256 * j;
+    if (i < kSub * kXs) xs[i] = v[j];
+  }
+}
+
+// State index of this lane's (fit, row) for list row e (clamped to the list).
+__device__ __forceinline__ size_t state_at(const MmArgs& a, const Blk& b, const uint32_t* lst, uint32_t e) {
+  return b.sb + (size_t)(b.r0 + (lst[min(e, b.n_ent - 1)] >> 8)) * a.S_pad;
+}
+
+// Sum (or min) over the 4 row lanes of each fit (lanes fl, fl + 16, fl + 32, fl + 48).
+__device__ __forceinline__ double rows_sum(double v) {
+  v += __shfl_xor(v, 16);
+  return v + __shfl_xor(v, 32);
+}
+__device__ __forceinline__ double rows_min(double v) {
+  v = fmin(v, __shfl_xor(v, 16));
+  return fmin(v, __shfl_xor(v, 32));
 }
 
 // mm_assemble: mode 0: weighted OLS of the replicate (q = c, rho = y) -> M, X'Cy, sum c y^2, n_act;
-// mode 1: start point (x = (1 - tau) c, z/w from the OLS residual) + assemble; mode 2: apply the
-// last step (x += ap dx, z += ad dz, w += ad dw) + assemble.
-// The same pass with X'QX and X'Q r on f64 MFMA (v_mfma_f64_16x16x4: A = q of 16 fits x 4 rows,
-// B = the rows' pair products, the counts-Gram kernel's shape). Block = 4 waves on the same 64
-// fits and a chunk of rows; per 64-row sub-tile: the rows' values are staged in LDS, then thread
-// (fit = t & 63, row group = wave) applies the last step and writes q and q r into LDS images,
-// then wave w runs the MFMAs of column blocks w, w + 4, w + 8 (pair blocks, then the X'Q r block).
-constexpr int kXs = 17;     // LDS stride of a staged row: [1, x_1..x_p, pad.., y at 16]
-constexpr int kQs = 65;     // LDS stride of a q-image row (64 fits + pad)
-constexpr int kMfmaCb = 3;  // column blocks per wave (4 waves x 3 >= 9 pair blocks + 1)
-typedef double mm_d4 __attribute__((ext_vector_type(4)));
-
-template <int K>
+// mode 1: start point (x = (1 - tau) c, z/w from the OLS residual) + assemble; mode 2 (STEP): apply
+// the last step (x += ap dx, z += ad dz, w += ad dw) + assemble. M = X'QX and X'Q r on f64 MFMA:
+// column block cb < NCB has B = x_i x_j of pair columns cb*16.. (ob_pair_index order), block NCB
+// has A = q r and B = x.
+template <int K, bool STEP>
 __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a, int mode) {
   constexpr int NP = K * (K + 1) / 2, NV = NP + K + 2;
-  constexpr int NCB = (NP + 15) / 16;  // pair column blocks; block NCB is X'Q r
-  __shared__ double xs[64 * kXs];
-  __shared__ double qi[64 * kQs];
-  __shared__ double qri[64 * kQs];
-  __shared__ double red[2][4][64];
-  __shared__ uint32_t cws[16];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint32_t gch = blockIdx.x, fb = blockIdx.y, slot = blockIdx.z;
-  const uint32_t g = gch >= a.nch[0] ? 1u : 0u;
-  const uint32_t ch = gch - (g ? a.nch[0] : 0u);
-  // phase-1 role: fit = lane, rows of row group `wave`
-  const int s = (int)fb * 64 + lane;
-  const size_t F = fit_index(a, slot, g, s);
-  const uint32_t st = s < a.S ? a.fstat[F] : kDone;
-  const bool live = mode == 0 ? s < a.S_pad : !(st & (kDone | kFailed));
+  constexpr int NCB = (NP + 15) / 16;
+  __shared__ __attribute__((aligned(16))) double xs[2][kSub * kXs];
+  __shared__ uint32_t lst[kRc];
+  const Blk b = blk_ctx(a, lst, mode == 0);
   double beta[K];
   double tau = 0.0, ap = 0.0, ad = 0.0, delta = 0.0;
 #pragma unroll
-  for (int k = 0; k < K; ++k) beta[k] = (live && mode) ? a.beta[F * K + k] : 0.0;
-  if (live && mode) {
-    tau = a.fs[F * kFs + FS_TAU];
-    ap = a.fs[F * kFs + FS_AP];
-    ad = a.fs[F * kFs + FS_AD];
-    delta = a.fs[F * kFs + FS_DELTA];
+  for (int k = 0; k < K; ++k) beta[k] = (b.live && mode) ? a.beta[b.F * K + k] : 0.0;
+  if (b.live && mode) {
+    tau = a.fs[b.F * kFs + FS_TAU];
+    ap = a.fs[b.F * kFs + FS_AP];
+    ad = a.fs[b.F * kFs + FS_AD];
+    delta = a.fs[b.F * kFs + FS_DELTA];
   }
+  // B-operand columns (i, j) of this lane (n = fl) per pair block, packed i | j << 8; kXzero
+  // past the last pair
+  uint32_t pp[NCB];
+#pragma unroll
+  for (int cb = 0; cb < NCB; ++cb) {
+    const int e = cb * 16 + b.fl;
+    pp[cb] = kXzero | (kXzero << 8);
+    if (e < NP) {
+      int i = 0, e0 = 0;
+      while (e >= e0 + (K - i)) {
+        e0 += K - i;
+        ++i;
+      }
+      pp[cb] = (uint32_t)i | (uint32_t)(i + (e - e0)) << 8;
+    }
+  }
+  mm_d4 acc[NCB + 1];
+#pragma unroll
+  for (int cb = 0; cb <= NCB; ++cb) acc[cb] = (mm_d4){0.0, 0.0, 0.0, 0.0};
   double gap = 0.0, obj = 0.0;
-  // phase-2 role: column blocks of this wave and their pair columns
-  int pa[kMfmaCb], pb[kMfmaCb];
-#pragma unroll
-  for (int c = 0; c < kMfmaCb; ++c) {
-    const int cb = wave + 4 * c;
-    pa[c] = pb[c] = -1;
-    if (cb < NCB) {
-      const int e = cb * 16 + (lane & 15);
-      if (e < NP) {  // e -> (i, j), i <= j, i-major (ob_pair_index order)
-        int i = 0, e0 = 0;
-        while (e >= e0 + (K - i)) {
-          e0 += K - i;
-          ++i;
-        }
-        pa[c] = i;
-        pb[c] = i + (e - e0);
+  __syncthreads();  // lst
+  const uint32_t nsub = (b.n_ent + kSub - 1) / kSub;
+  if (__syncthreads_or(b.live) && nsub) {
+    double stg[kStage];
+    xs_load<K>(a, b, lst, 0, stg);
+    xs_store(xs[0], stg);
+    double rx[kRingA], rz[kRingA], rw[kRingA], rdx[kRingA], rdz[kRingA], rdw[kRingA];
+    auto load = [&](int k, uint32_t e) {
+      if (STEP) {
+        const size_t si = state_at(a, b, lst, e);
+        rx[k] = a.x[si];
+        rz[k] = a.z[si];
+        rw[k] = a.w[si];
+        rdx[k] = a.dx[si];
+        rdz[k] = a.dz[si];
+        rdw[k] = a.dw[si];
       }
-    } else if (cb == NCB && (lane & 15) < K) {
-      pa[c] = lane & 15;  // X'Q r: B is the x column itself, A = q r
-      pb[c] = 0;
-    }
-  }
-  mm_d4 acc[4][kMfmaCb];
+    };
 #pragma unroll
-  for (int q4 = 0; q4 < 4; ++q4)
-#pragma unroll
-    for (int c = 0; c < kMfmaCb; ++c) acc[q4][c] = (mm_d4){0.0, 0.0, 0.0, 0.0};
-  const double* X = a.cols[g];
-  const int64_t ld = a.ld[g];
-  const uint32_t n = a.n[g];
-  const size_t sb = ((size_t)slot * a.rep_rows + (g ? a.n[0] : 0u)) * a.S_pad + s;
-  const uint32_t r0 = ch * kRc, r1 = min(n, r0 + kRc);
-  const bool any_live = __syncthreads_or(live);
-  if (any_live)
-    for (uint32_t t0 = r0; t0 < r1; t0 += 64) {
-      const uint32_t nr = min(64u, r1 - t0);
-      // stage the sub-tile's rows: [1, x_1..x_{K-1}, 0.., y]
-      for (int i = tid; i < 64 * kXs; i += 256) {
-        const int rr = i / kXs, col = i % kXs;
-        double v = 0.0;
-        if ((uint32_t)rr < nr) {
-          if (col == 0)
-            v = 1.0;
-          else if (col < K)
-            v = X[(size_t)(col - 1) * ld + t0 + rr];
-          else if (col == kXs - 1)
-            v = X[(size_t)a.p * ld + t0 + rr];
-        }
-        xs[i] = v;
-      }
-      stage_counts(a, slot, g, t0, cws);
-      __syncthreads();
-      // phase 1: rows wave, wave + 4, ... of the sub-tile for fit `lane`; the state of the next
-      // row is loaded before this row's stores (software prefetch)
-      const bool pref = mode == 2 && live;
-      double nx = 0.0, nz = 0.0, nw = 0.0, ndx = 0.0, ndz = 0.0, ndw = 0.0;
-      auto load_state = [&](int rr) {
-        if (pref && (uint32_t)rr < nr) {
-          const size_t si = sb + (size_t)(t0 + rr) * a.S_pad;
-          nx = a.x[si];
-          nz = a.z[si];
-          nw = a.w[si];
-          ndx = a.dx[si];
-          ndz = a.dz[si];
-          ndw = a.dw[si];
-        }
-      };
-      load_state(wave);
-      for (int rr = wave; rr < 64; rr += 4) {
-        const double cx = nx, cz = nz, cw = nw, cdx = ndx, cdz = ndz, cdw = ndw;
-        load_state(rr + 4);
-        double q = 0.0, qr = 0.0;
-        const uint32_t row = t0 + rr;
-        const uint32_t cu = staged_count(cws, rr, nr);
-        if (cu != 0 && live) {
-          const double c = (double)cu;
-          const double* xr = xs + rr * kXs;
-          const double y = xr[kXs - 1];
-          if (mode == 0) {
-            q = c;
-            qr = c * y;
-            gap += c * y * y;
-            obj += 1.0;
-          } else {
-            const size_t si = sb + (size_t)row * a.S_pad;
-            double xb = 0.0;
-#pragma unroll
-            for (int k = 0; k < K; ++k) xb += xr[k] * beta[k];
-            const double r = y - xb;
-            double xv, zv, wv;
-            if (mode == 1) {
-              xv = (1.0 - tau) * c;
-              zv = fmax(-r, 0.0) + delta;
-              wv = fmax(r, 0.0) + delta;
+    for (int k = 0; k < kRingA; ++k) load(k, 4 * k + b.rl);
+    __syncthreads();
+    for (uint32_t t = 0; t < nsub; ++t) {
+      const double* X = xs[t & 1];
+      xs_load<K>(a, b, lst, t + 1, stg);
+      auto step = [&](int j) {
+          const int k = j % kRingA;
+          const double cx = rx[k], cz = rz[k], cw = rw[k], cdx = rdx[k], cdz = rdz[k], cdw = rdw[k];
+          const uint32_t e = t * kSub + 4 * j + b.rl;
+          load(k, e + 4 * kRingA);
+          const bool valid = e < b.n_ent && b.live;
+          const double c = valid ? (double)(lst[e] & 255u) : 0.0;
+          const double* xr = X + (4 * j + b.rl) * kXs;
+          const double y = xr[kXy];
+          double q = 0.0, qr = 0.0;
+          if (valid) {
+            if (mode == 0) {
+              q = c;
+              qr = c * y;
+              gap += c * y * y;
+              obj += 1.0;
             } else {
-              xv = cx + ap * cdx;
-              zv = cz + ad * cdz;
-              wv = cw + ad * cdw;
+              double xb = 0.0;
+#pragma unroll
+              for (int k2 = 0; k2 < K; ++k2) xb += xr[k2] * beta[k2];
+              const double r = y - xb;
+              double xv, zv, wv;
+              if (!STEP) {
+                xv = (1.0 - tau) * c;
+                zv = fmax(-r, 0.0) + delta;
+                wv = fmax(r, 0.0) + delta;
+              } else {
+                xv = cx + ap * cdx;
+                zv = cz + ad * cdz;
+                wv = cw + ad * cdw;
+              }
+              const size_t si = b.sb + (size_t)(b.r0 + (lst[e] >> 8)) * a.S_pad;
+              a.x[si] = xv;
+              a.z[si] = zv;
+              a.w[si] = wv;
+              const double sv = c - xv;
+              q = xv * sv / (zv * sv + wv * xv);  // 1 / (z/x + w/s)
+              qr = q * r;                          // rho_aff = r_d + w - z = y - X beta
+              gap += xv * zv + sv * wv;
+              obj += y * xv;
             }
-            a.x[si] = xv;
-            a.z[si] = zv;
-            a.w[si] = wv;
-            const double sv = c - xv;
-            q = xv * sv / (zv * sv + wv * xv);  // 1 / (z/x + w/s)
-            qr = q * r;  // rho_aff = r_d + w - z = y - X beta
-            gap += xv * zv + sv * wv;
-            obj += y * xv;
           }
-        }
-        qi[rr * kQs + lane] = q;
-        qri[rr * kQs + lane] = qr;
-      }
-      __syncthreads();
-      // phase 2: acc[q4][c] += A(q of fits 16 q4.., rows 4 ks..) x B(pair products)
-#pragma unroll 2
-      for (int ks = 0; ks < 16; ++ks) {
-        const int rr = 4 * ks + (lane >> 4);
-        const double* xr = xs + rr * kXs;
-        double bv[kMfmaCb];
 #pragma unroll
-        for (int c = 0; c < kMfmaCb; ++c)
-          bv[c] = pa[c] < 0 ? 0.0 : (wave + 4 * c == NCB ? xr[pa[c]] : xr[pa[c]] * xr[pb[c]]);
+          for (int cb = 0; cb < NCB; ++cb)
+            acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(q, xr[pp[cb] & 255u] * xr[pp[cb] >> 8], acc[cb], 0, 0, 0);
+          acc[NCB] = __builtin_amdgcn_mfma_f64_16x16x4f64(qr, xr[b.fl], acc[NCB], 0, 0, 0);
+      };
+      // the next sub-tile's values go to the other buffer after a few steps (registers freed)
+      if (b.wave_live)
 #pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4) {
-          const double aq = qi[rr * kQs + 16 * q4 + (lane & 15)];
-          const double aqr = qri[rr * kQs + 16 * q4 + (lane & 15)];
+        for (int j = 0; j < kStoreAt; ++j) step(j);
+      xs_store(xs[(t + 1) & 1], stg);
+      if (b.wave_live)
 #pragma unroll
-          for (int c = 0; c < kMfmaCb; ++c)
-            if (wave + 4 * c <= NCB)
-              acc[q4][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(wave + 4 * c == NCB ? aqr : aq, bv[c], acc[q4][c], 0,
-                                                                0, 0);
-        }
-      }
+        for (int j = kStoreAt; j < 16; ++j) step(j);
       __syncthreads();
     }
-  // partials: pairs and X'Q r from the MFMA accumulators, gap / objective from phase 1
-  double* P = a.partial + ((size_t)slot * (a.nch[0] + a.nch[1]) + gch) * a.S_pad * NV;
-#pragma unroll
-  for (int c = 0; c < kMfmaCb; ++c) {
-    const int cb = wave + 4 * c;
-    if (cb > NCB) continue;
-    const int col = cb * 16 + (lane & 15);
-#pragma unroll
-    for (int q4 = 0; q4 < 4; ++q4)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const size_t fit = (size_t)fb * 64 + 16 * q4 + (lane >> 4) + 4 * r;
-        if (cb < NCB && col < NP) P[fit * NV + col] = acc[q4][c][r];
-        if (cb == NCB && (lane & 15) < K) P[fit * NV + NP + (lane & 15)] = acc[q4][c][r];
-      }
   }
-  red[0][wave][lane] = gap;
-  red[1][wave][lane] = obj;
-  __syncthreads();
-  if (wave == 0) {
-    const size_t fit = (size_t)fb * 64 + lane;
-    P[fit * NV + NP + K] = ((red[0][0][lane] + red[0][1][lane]) + red[0][2][lane]) + red[0][3][lane];
-    P[fit * NV + NP + K + 1] = ((red[1][0][lane] + red[1][1][lane]) + red[1][2][lane]) + red[1][3][lane];
+  // partials: D row = fit (rl + 4 r of the wave's 16), column = fl
+  double* P = a.partial + ((size_t)b.slot * (a.nch[0] + a.nch[1]) + b.gch) * a.S_pad * NV;
+  const size_t fw = (size_t)b.fb * 64 + b.wave * 16;
+#pragma unroll
+  for (int cb = 0; cb <= NCB; ++cb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const size_t fit = fw + b.rl + 4 * r;
+      const int col = cb * 16 + b.fl;
+      if (cb < NCB && col < NP) P[fit * NV + col] = acc[cb][r];
+      if (cb == NCB && b.fl < K) P[fit * NV + NP + b.fl] = acc[cb][r];
+    }
+  gap = rows_sum(gap);
+  obj = rows_sum(obj);
+  if (b.rl == 0) {
+    P[(fw + b.fl) * NV + NP + K] = gap;
+    P[(fw + b.fl) * NV + NP + K + 1] = obj;
   }
 }
 
@@ -327,8 +375,8 @@ struct Affine {
 };
 
 template <int K>
-__device__ __forceinline__ Affine affine_row(double xv, double zv, double wv, double c, const double (&xr)[K],
-                                             double y, const double (&beta)[K], const double (&dba)[K]) {
+__device__ __forceinline__ Affine affine_row(double xv, double zv, double wv, double c, const double* xr,
+                                             const double (&beta)[K], const double (&dba)[K]) {
   Affine f;
   f.xv = xv;
   f.zv = zv;
@@ -340,7 +388,7 @@ __device__ __forceinline__ Affine affine_row(double xv, double zv, double wv, do
     xb += xr[k] * beta[k];
     xd += xr[k] * dba[k];
   }
-  f.r = y - xb;
+  f.r = xr[kXy] - xb;
   f.ix = 1.0 / f.xv;
   f.is = 1.0 / f.sv;
   f.q = 1.0 / (f.zv * f.ix + f.wv * f.is);
@@ -350,214 +398,139 @@ __device__ __forceinline__ Affine affine_row(double xv, double zv, double wv, do
   return f;
 }
 
-// Shared shape of the affine / final passes: block = 4 waves on the same 64 fits (fit = lane),
-// each wave every fourth row of a 64-row sub-tile whose design values are staged in LDS (broadcast
-// reads), the state of the wave's next row with a nonzero count loaded before this row's work,
-// per-thread accumulators reduced over the 4 waves in a fixed order at the end.
-struct PassCtx {
-  uint32_t g, ch, gch, slot, fb;
-  int lane, wave, s;
-  size_t F, sb;
-  bool live;
-  const double* X;
-  int64_t ld;
-  uint32_t r0, r1;
-};
-
-__device__ __forceinline__ PassCtx pass_ctx(const MmArgs& a) {
-  PassCtx c;
-  c.lane = threadIdx.x & 63;
-  c.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  c.gch = blockIdx.x;
-  c.fb = blockIdx.y;
-  c.slot = blockIdx.z;
-  c.g = c.gch >= a.nch[0] ? 1u : 0u;
-  c.ch = c.gch - (c.g ? a.nch[0] : 0u);
-  c.s = (int)c.fb * 64 + c.lane;
-  c.F = fit_index(a, c.slot, c.g, c.s);
-  c.live = c.s < a.S && !(a.fstat[c.F] & (kDone | kFailed));
-  c.X = a.cols[c.g];
-  c.ld = a.ld[c.g];
-  c.sb = ((size_t)c.slot * a.rep_rows + (c.g ? a.n[0] : 0u)) * a.S_pad + c.s;
-  c.r0 = c.ch * kRc;
-  c.r1 = min(a.n[c.g], c.r0 + kRc);
-  return c;
-}
-
-// Stage rows [t0, t0 + 64) as [1, x_1..x_{K-1}, 0.., y at kXs - 1] (zeros past the chunk).
-template <int K>
-__device__ __forceinline__ void stage_rows(const MmArgs& a, const PassCtx& c, uint32_t t0, uint32_t nr, double* xs) {
-  for (int i = threadIdx.x; i < 64 * kXs; i += blockDim.x) {
-    const int rr = i / kXs, col = i % kXs;
-    double v = 0.0;
-    if ((uint32_t)rr < nr) {
-      if (col == 0)
-        v = 1.0;
-      else if (col < K)
-        v = c.X[(size_t)(col - 1) * c.ld + t0 + rr];
-      else if (col == kXs - 1)
-        v = c.X[(size_t)a.p * c.ld + t0 + rr];
-    }
-    xs[i] = v;
-  }
-}
-
-// Fixed-order sum (or min for i < n_min) of acc over the 4 waves into wave 0 (red: 64 x (N + 1)).
-template <int N>
-__device__ __forceinline__ void waves_reduce(double (&acc)[N], double* red, int wave, int lane, int n_min) {
-#pragma unroll 1
-  for (int w = 3; w >= 1; --w) {
-    if (wave == w)
+// The affine / final passes share the walk: state (x, z, w) streamed kRing steps ahead, the
+// design values from the double-buffered sub-tiles. body(j-th step's state, valid, count, xr, e).
+template <int K, typename Body>
+__device__ __forceinline__ void state_walk(const MmArgs& a, const Blk& b, const uint32_t* lst, double (*xs)[kSub * kXs],
+                                           Body&& body) {
+  const uint32_t nsub = (b.n_ent + kSub - 1) / kSub;
+  if (!__syncthreads_or(b.live) || !nsub) return;
+  double stg[kStage];
+  xs_load<K>(a, b, lst, 0, stg);
+  xs_store(xs[0], stg);
+  double rx[kRing], rz[kRing], rw[kRing];
+  auto load = [&](int k, uint32_t e) {
+    const size_t si = state_at(a, b, lst, e);
+    rx[k] = a.x[si];
+    rz[k] = a.z[si];
+    rw[k] = a.w[si];
+  };
 #pragma unroll
-      for (int i = 0; i < N; ++i) {
-        double* r = red + lane * (N + 1) + i;
-        *r = w == 3 ? acc[i] : (i < n_min ? fmin(*r, acc[i]) : *r + acc[i]);
-      }
+  for (int k = 0; k < kRing; ++k) load(k, 4 * k + b.rl);
+  __syncthreads();
+  for (uint32_t t = 0; t < nsub; ++t) {
+    const double* X = xs[t & 1];
+    xs_load<K>(a, b, lst, t + 1, stg);
+    auto step = [&](int j) {
+      const int k = j % kRing;
+      const double xv = rx[k], zv = rz[k], wv = rw[k];
+      const uint32_t e = t * kSub + 4 * j + b.rl;
+      load(k, e + 4 * kRing);
+      const bool valid = e < b.n_ent && b.live;
+      body(xv, zv, wv, valid, valid ? (double)(lst[e] & 255u) : 1.0, X + (4 * j + b.rl) * kXs, e);
+    };
+    if (b.wave_live)
+#pragma unroll
+      for (int j = 0; j < kStoreAt; ++j) step(j);
+    xs_store(xs[(t + 1) & 1], stg);
+    if (b.wave_live)
+#pragma unroll
+      for (int j = kStoreAt; j < 16; ++j) step(j);
     __syncthreads();
   }
-  if (wave == 0)
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const double r = red[lane * (N + 1) + i];
-      acc[i] = i < n_min ? fmin(r, acc[i]) : r + acc[i];
-    }
 }
-
-// The next row's count and state (x, z, w) for the affine / final passes (a 4-deep ring of rows
-// measured no faster than this one row of prefetch).
-constexpr int kPrefetch = 1;
-struct StateRing {
-  uint32_t cu[kPrefetch];
-  double x[kPrefetch], z[kPrefetch], w[kPrefetch];
-  __device__ __forceinline__ void load(const MmArgs& a, const PassCtx& c, const uint32_t* cws, uint32_t t0,
-                                      uint32_t nr, int rr, int k) {
-    cu[k] = staged_count(cws, rr, nr);
-    x[k] = z[k] = w[k] = 0.0;
-    if (cu[k] && c.live) {
-      const size_t si = c.sb + (size_t)(t0 + rr) * a.S_pad;
-      x[k] = a.x[si];
-      z[k] = a.z[si];
-      w[k] = a.w[si];
-    }
-  }
-};
 
 // [0] primal step bound, [1] dual step bound, [2..4] mu_aff terms, then X'q rho0, X'q rho1.
 template <int K>
 __global__ __launch_bounds__(256, 2) void mm_affine_kernel(const MmArgs a) {
   constexpr int NV = 5 + 2 * K;
-  __shared__ double xs[64 * kXs];
-  __shared__ double red[64 * (NV + 1)];
-  __shared__ uint32_t cws[16];
-  const PassCtx c = pass_ctx(a);
+  __shared__ __attribute__((aligned(16))) double xs[2][kSub * kXs];
+  __shared__ uint32_t lst[kRc];
+  const Blk b = blk_ctx(a, lst, false);
   double beta[K], dba[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    beta[k] = c.live ? a.beta[c.F * K + k] : 0.0;
-    dba[k] = c.live ? a.dba[c.F * K + k] : 0.0;
+    beta[k] = b.live ? a.beta[b.F * K + k] : 0.0;
+    dba[k] = b.live ? a.dba[b.F * K + k] : 0.0;
   }
-  double acc[NV];
-  acc[0] = acc[1] = 1e300;
-#pragma unroll
-  for (int i = 2; i < NV; ++i) acc[i] = 0.0;
-  if (__syncthreads_or(c.live))
-    for (uint32_t t0 = c.r0; t0 < c.r1; t0 += 64) {
-      const uint32_t nr = min(64u, c.r1 - t0);
-      stage_rows<K>(a, c, t0, nr, xs);
-      stage_counts(a, c.slot, c.g, t0, cws);
-      __syncthreads();
-      // the state of the wave's next row is loaded before this row's work (software prefetch)
-      StateRing ring;
-      ring.load(a, c, cws, t0, nr, c.wave, 0);
-      for (int rr = c.wave; rr < 64; rr += 4) {
-        const uint32_t cu = ring.cu[0];
-        const double xv = ring.x[0], zv = ring.z[0], wv = ring.w[0];
-        ring.load(a, c, cws, t0, nr, rr + 4, 0);
-        if (!cu || !c.live) continue;
-        double xr[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) xr[k] = xs[rr * kXs + k];
-        const Affine f = affine_row<K>(xv, zv, wv, (double)cu, xr, xs[rr * kXs + kXs - 1], beta, dba);
-        if (f.dxa != 0.0) acc[0] = fmin(acc[0], (f.dxa < 0.0 ? -f.xv : f.sv) / f.dxa);
-        if (f.dza < 0.0) acc[1] = fmin(acc[1], -f.zv / f.dza);
-        if (f.dwa < 0.0) acc[1] = fmin(acc[1], -f.wv / f.dwa);
-        acc[2] += f.xv * f.dza + f.sv * f.dwa;
-        acc[3] += f.zv * f.dxa - f.wv * f.dxa;
-        acc[4] += f.dxa * f.dza - f.dxa * f.dwa;
-        const double q0 = f.q * (f.r - f.dxa * (f.dwa * f.is + f.dza * f.ix));
-        const double q1 = f.q * (f.ix - f.is);
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-          acc[5 + k] += q0 * xr[k];
-          acc[5 + K + k] += q1 * xr[k];
-        }
-      }
-      __syncthreads();
+  double acc[5] = {1e300, 1e300, 0.0, 0.0, 0.0};
+  mm_d4 m0 = {0.0, 0.0, 0.0, 0.0}, m1 = {0.0, 0.0, 0.0, 0.0};
+  __syncthreads();  // lst
+  state_walk<K>(a, b, lst, xs, [&](double xv, double zv, double wv, bool valid, double c, const double* xr, uint32_t) {
+    double q0 = 0.0, q1 = 0.0;
+    if (valid) {
+      const Affine f = affine_row<K>(xv, zv, wv, c, xr, beta, dba);
+      if (f.dxa != 0.0) acc[0] = fmin(acc[0], (f.dxa < 0.0 ? -f.xv : f.sv) / f.dxa);
+      if (f.dza < 0.0) acc[1] = fmin(acc[1], -f.zv / f.dza);
+      if (f.dwa < 0.0) acc[1] = fmin(acc[1], -f.wv / f.dwa);
+      acc[2] += f.xv * f.dza + f.sv * f.dwa;
+      acc[3] += f.zv * f.dxa - f.wv * f.dxa;
+      acc[4] += f.dxa * f.dza - f.dxa * f.dwa;
+      q0 = f.q * (f.r - f.dxa * (f.dwa * f.is + f.dza * f.ix));
+      q1 = f.q * (f.ix - f.is);
     }
-  waves_reduce<NV>(acc, red, c.wave, c.lane, 2);
-  if (c.wave == 0) {
-    double* P = a.partial + (((size_t)c.slot * (a.nch[0] + a.nch[1]) + c.gch) * a.S_pad + c.s) * NV;
+    const double bx = xr[b.fl];  // B: row rl, column fl (zero past K)
+    m0 = __builtin_amdgcn_mfma_f64_16x16x4f64(q0, bx, m0, 0, 0, 0);
+    m1 = __builtin_amdgcn_mfma_f64_16x16x4f64(q1, bx, m1, 0, 0, 0);
+  });
+  double* P = a.partial + ((size_t)b.slot * (a.nch[0] + a.nch[1]) + b.gch) * a.S_pad * NV;
+  const size_t fw = (size_t)b.fb * 64 + b.wave * 16;
+  if (b.fl < K)
 #pragma unroll
-    for (int i = 0; i < NV; ++i) P[i] = acc[i];
-  }
+    for (int r = 0; r < 4; ++r) {
+      const size_t fit = fw + b.rl + 4 * r;
+      P[fit * NV + 5 + b.fl] = m0[r];
+      P[fit * NV + 5 + K + b.fl] = m1[r];
+    }
+  acc[0] = rows_min(acc[0]);
+  acc[1] = rows_min(acc[1]);
+#pragma unroll
+  for (int i = 2; i < 5; ++i) acc[i] = rows_sum(acc[i]);
+  if (b.rl == 0)
+#pragma unroll
+    for (int i = 0; i < 5; ++i) P[(fw + b.fl) * NV + i] = acc[i];
 }
 
 // Corrector direction (stored for the next assemble) and its step-length bounds.
 template <int K>
 __global__ __launch_bounds__(256, 2) void mm_final_kernel(const MmArgs a) {
-  __shared__ double xs[64 * kXs];
-  __shared__ double red[64 * 3];
-  __shared__ uint32_t cws[16];
-  const PassCtx c = pass_ctx(a);
+  __shared__ __attribute__((aligned(16))) double xs[2][kSub * kXs];
+  __shared__ uint32_t lst[kRc];
+  const Blk b = blk_ctx(a, lst, false);
   double beta[K], dba[K], db[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    beta[k] = c.live ? a.beta[c.F * K + k] : 0.0;
-    dba[k] = c.live ? a.dba[c.F * K + k] : 0.0;
-    db[k] = c.live ? a.db[c.F * K + k] : 0.0;
+    beta[k] = b.live ? a.beta[b.F * K + k] : 0.0;
+    dba[k] = b.live ? a.dba[b.F * K + k] : 0.0;
+    db[k] = b.live ? a.db[b.F * K + k] : 0.0;
   }
-  const double sigmu = c.live ? a.fs[c.F * kFs + FS_SIGMU] : 0.0;
+  const double sigmu = b.live ? a.fs[b.F * kFs + FS_SIGMU] : 0.0;
   double acc[2] = {1e300, 1e300};
-  if (__syncthreads_or(c.live))
-    for (uint32_t t0 = c.r0; t0 < c.r1; t0 += 64) {
-      const uint32_t nr = min(64u, c.r1 - t0);
-      stage_rows<K>(a, c, t0, nr, xs);
-      stage_counts(a, c.slot, c.g, t0, cws);
-      __syncthreads();
-      // the state of the wave's next row is loaded before this row's work (software prefetch)
-      StateRing ring;
-      ring.load(a, c, cws, t0, nr, c.wave, 0);
-      for (int rr = c.wave; rr < 64; rr += 4) {
-        const uint32_t cu = ring.cu[0];
-        const double xv = ring.x[0], zv = ring.z[0], wv = ring.w[0];
-        ring.load(a, c, cws, t0, nr, rr + 4, 0);
-        if (!cu || !c.live) continue;
-        double xr[K];
+  __syncthreads();  // lst
+  state_walk<K>(a, b, lst, xs, [&](double xv, double zv, double wv, bool valid, double c, const double* xr, uint32_t e) {
+    if (!valid) return;
+    const Affine f = affine_row<K>(xv, zv, wv, c, xr, beta, dba);
+    const double rho = f.r - f.dxa * (f.dwa * f.is + f.dza * f.ix) + sigmu * (f.ix - f.is);
+    double xd = 0.0;
 #pragma unroll
-        for (int k = 0; k < K; ++k) xr[k] = xs[rr * kXs + k];
-        const Affine f = affine_row<K>(xv, zv, wv, (double)cu, xr, xs[rr * kXs + kXs - 1], beta, dba);
-        const double rho = f.r - f.dxa * (f.dwa * f.is + f.dza * f.ix) + sigmu * (f.ix - f.is);
-        double xd = 0.0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) xd += xr[k] * db[k];
-        const double dx = f.q * (rho - xd);
-        const double rxz = sigmu - f.xv * f.zv - f.dxa * f.dza;
-        const double rsw = sigmu - f.sv * f.wv + f.dxa * f.dwa;
-        const double dz = (rxz - f.zv * dx) * f.ix;
-        const double dw = (rsw + f.wv * dx) * f.is;
-        const size_t si = c.sb + (size_t)(t0 + rr) * a.S_pad;
-        a.dx[si] = dx;
-        a.dz[si] = dz;
-        a.dw[si] = dw;
-        if (dx != 0.0) acc[0] = fmin(acc[0], (dx < 0.0 ? -f.xv : f.sv) / dx);
-        if (dz < 0.0) acc[1] = fmin(acc[1], -f.zv / dz);
-        if (dw < 0.0) acc[1] = fmin(acc[1], -f.wv / dw);
-      }
-      __syncthreads();
-    }
-  waves_reduce<2>(acc, red, c.wave, c.lane, 2);
-  if (c.wave == 0) {
-    double* P = a.partial + (((size_t)c.slot * (a.nch[0] + a.nch[1]) + c.gch) * a.S_pad + c.s) * 2;
+    for (int k = 0; k < K; ++k) xd += xr[k] * db[k];
+    const double dx = f.q * (rho - xd);
+    const double rxz = sigmu - f.xv * f.zv - f.dxa * f.dza;
+    const double rsw = sigmu - f.sv * f.wv + f.dxa * f.dwa;
+    const double dz = (rxz - f.zv * dx) * f.ix;
+    const double dw = (rsw + f.wv * dx) * f.is;
+    const size_t si = b.sb + (size_t)(b.r0 + (lst[e] >> 8)) * a.S_pad;
+    a.dx[si] = dx;
+    a.dz[si] = dz;
+    a.dw[si] = dw;
+    if (dx != 0.0) acc[0] = fmin(acc[0], (dx < 0.0 ? -f.xv : f.sv) / dx);
+    if (dz < 0.0) acc[1] = fmin(acc[1], -f.zv / dz);
+    if (dw < 0.0) acc[1] = fmin(acc[1], -f.wv / dw);
+  });
+  acc[0] = rows_min(acc[0]);
+  acc[1] = rows_min(acc[1]);
+  if (b.rl == 0) {
+    double* P = a.partial + (((size_t)b.slot * (a.nch[0] + a.nch[1]) + b.gch) * a.S_pad + b.s) * 2;
     P[0] = acc[0];
     P[1] = acc[1];
   }
@@ -869,7 +842,10 @@ __global__ __launch_bounds__(256) void mm_finish_kernel(const MmArgs a, int K, i
 template <int K>
 struct Kernels {
   static void assemble(const MmArgs& a, dim3 grid, int mode, hipStream_t s) {
-    hipLaunchKernelGGL(mm_assemble_mfma_kernel<K>, grid, dim3(256), 0, s, a, mode);
+    if (mode == 2)
+      hipLaunchKernelGGL((mm_assemble_mfma_kernel<K, true>), grid, dim3(256), 0, s, a, mode);
+    else
+      hipLaunchKernelGGL((mm_assemble_mfma_kernel<K, false>), grid, dim3(256), 0, s, a, mode);
   }
   static void affine(const MmArgs& a, dim3 grid, hipStream_t s) {
     hipLaunchKernelGGL(mm_affine_kernel<K>, grid, dim3(256), 0, s, a);
@@ -904,13 +880,15 @@ struct Buffers {
   double *x = nullptr, *z = nullptr, *w = nullptr, *dx = nullptr, *dz = nullptr, *dw = nullptr;
   double *beta = nullptr, *dba = nullptr, *db = nullptr, *L = nullptr, *fs = nullptr;
   double *partial = nullptr, *red = nullptr, *quant = nullptr, *rows = nullptr;
-  uint32_t *fstat = nullptr, *active = nullptr, *tprefix = nullptr, *lane_of = nullptr;
+  uint32_t *fstat = nullptr, *active = nullptr, *tprefix = nullptr, *lane_of = nullptr, *rowlist = nullptr,
+           *nrows = nullptr;
   unsigned long long* active_rows = nullptr;
   uint8_t* ok = nullptr;
   ~Buffers() {
     for (void* p : {(void*)x, (void*)z, (void*)w, (void*)dx, (void*)dz, (void*)dw, (void*)beta, (void*)dba, (void*)db,
                     (void*)L, (void*)fs, (void*)partial, (void*)red, (void*)quant, (void*)rows, (void*)fstat,
-                    (void*)active, (void*)active_rows, (void*)tprefix, (void*)lane_of, (void*)ok})
+                    (void*)active, (void*)active_rows, (void*)tprefix, (void*)lane_of, (void*)rowlist, (void*)nrows,
+                    (void*)ok})
       (void)hipFree(p);
   }
 };
@@ -940,7 +918,9 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, MmS
     return hipGetLastError();
   };
   const size_t lds_solve = sizeof(double) * ((size_t)K * K + K);
-  // start: weighted OLS per (slot, group)
+  // row lists, then the start: weighted OLS per (slot, group)
+  hipLaunchKernelGGL(mm_rows_kernel, dim3(nch, 1, a.n_rb), dim3(256), 0, s, a);
+  MM_OK(hipGetLastError());
   MM_OK(hipMemsetAsync(a.active_rows, 0, sizeof(unsigned long long), s));
   pass(K, 0, a, dim3(nch, 1, a.n_rb), 0, s);
   MM_OK(hipGetLastError());
@@ -1061,6 +1041,8 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   MM_OK(hipMalloc(&b.fs, sizeof(double) * fits * kFs));
   MM_OK(hipMalloc(&b.fstat, sizeof(uint32_t) * fits));
   MM_OK(hipMalloc(&b.lane_of, sizeof(uint32_t) * fits));
+  MM_OK(hipMalloc(&b.rowlist, sizeof(uint32_t) * (size_t)rb_cap * (nch0 + nch1) * kRc));
+  MM_OK(hipMalloc(&b.nrows, sizeof(uint32_t) * (size_t)rb_cap * (nch0 + nch1)));
   MM_OK(hipMalloc(&b.partial, sizeof(double) * (size_t)rb_cap * (nch0 + nch1) * S_pad * nv_max));
   MM_OK(hipMalloc(&b.red, sizeof(double) * fits * nv_max));
   MM_OK(hipMalloc(&b.active, sizeof(uint32_t)));
@@ -1103,6 +1085,8 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   a.active_rows = b.active_rows;
   a.tprefix = b.tprefix;
   a.lane_of = b.lane_of;
+  a.rowlist = b.rowlist;
+  a.nrows = b.nrows;
   a.key0 = (uint32_t)seed;
   a.key1 = (uint32_t)(seed >> 32);
   a.n_q = n_q;
