@@ -124,7 +124,10 @@ def bench_mm(args, world, rank, local, dist):
     t0 = time.perf_counter()
     asm_ms, fit_rows, iters, last = 0.0, 0.0, 0, None
     for i in range(args.steps):
+        ts = time.perf_counter()
         rows, ok, t = step(args.warmup + i)
+        print(f"mm step {i}: {time.perf_counter() - ts:.3f} s, assemble {t['mm_assemble_ms']:.1f} ms, "
+              f"{t['mm_iterations']} iterations", file=sys.stderr, flush=True)
         asm_ms += t["mm_assemble_ms"]
         fit_rows += t["mm_fit_rows"]
         iters = max(iters, t["mm_iterations"])
@@ -153,7 +156,7 @@ def bench_mm(args, world, rank, local, dist):
                    "rows": args.rows, "predictors": args.preds, "simulations": args.sims,
                    "replicates_per_gpu_per_step": R, "parallelism": f"replicates sharded x{world}, RCCL all-gather"},
         "roofline": {"bound": "hbm", "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": gbps / HBM_PEAK_GBPS, "traffic": None, "kernel": "mm_assemble_kernel<16>",
+                     "frac": gbps / HBM_PEAK_GBPS, "traffic": None, "kernel": "mm_assemble_mfma_kernel<16, true>",
                      "assemble_ms": asm_ms, "live_fit_rows": fit_rows, "bytes_per_fit_row": bytes_row,
                      "tflops": fit_rows * flops_row / (asm_ms * 1e-3) / 1e12, "max_ipm_iterations": iters},
     }

@@ -1471,6 +1471,7 @@ void ob_panel_destroy(ob_panel* p) {
   (void)hipFree(p->d_rows_tmp);
   (void)hipFree(p->d_ok_tmp);
   for (hipEvent_t e : p->seg_events) (void)hipEventDestroy(e);
+  if (p->mm_ws_free) p->mm_ws_free(p->mm_ws);
   delete p;
 }
 

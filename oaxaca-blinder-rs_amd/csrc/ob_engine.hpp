@@ -65,6 +65,8 @@ struct ob_panel {
   uint32_t* d_hactive = nullptr;  // Heckman: replicates still iterating
   size_t cap_hgamma = 0, cap_hflags = 0, cap_hpartial = 0;
   size_t cap_m1 = 0, cap_partial = 0, cap_gram = 0, cap_chunks = 0, cap_counts = 0;
+  void* mm_ws = nullptr;  // Machado-Mata workspace (ob_mm.hip), freed by mm_ws_free
+  void (*mm_ws_free)(void*) = nullptr;
   std::vector<hipEvent_t> seg_events;  // 6 per segment of the last boot run
   ob_timing timing = {};
   bool timing_pending = false;

@@ -876,6 +876,8 @@ void pass(int K, int which, const MmArgs& a, dim3 grid, int mode, hipStream_t s)
   }
 }
 
+// MM workspace, kept on the panel between calls and grown on demand (the IPM state alone is
+// tens of GB: allocating and freeing it per call cost more than the passes at configs[4]).
 struct Buffers {
   double *x = nullptr, *z = nullptr, *w = nullptr, *dx = nullptr, *dz = nullptr, *dw = nullptr;
   double *beta = nullptr, *dba = nullptr, *db = nullptr, *L = nullptr, *fs = nullptr;
@@ -884,14 +886,34 @@ struct Buffers {
            *nrows = nullptr;
   unsigned long long* active_rows = nullptr;
   uint8_t* ok = nullptr;
+  size_t cap[23] = {};
+  void** slot(int i) {
+    void** v[23] = {(void**)&x, (void**)&z, (void**)&w, (void**)&dx, (void**)&dz, (void**)&dw, (void**)&beta,
+                    (void**)&dba, (void**)&db, (void**)&L, (void**)&fs, (void**)&partial, (void**)&red,
+                    (void**)&quant, (void**)&rows, (void**)&fstat, (void**)&active, (void**)&active_rows,
+                    (void**)&tprefix, (void**)&lane_of, (void**)&rowlist, (void**)&nrows, (void**)&ok};
+    return v[i];
+  }
+  // bytes[i] for slot i; reallocates the slots that are too small
+  hipError_t reserve(const size_t (&bytes)[23]) {
+    for (int i = 0; i < 23; ++i) {
+      if (bytes[i] <= cap[i]) continue;
+      void** q = slot(i);
+      (void)hipFree(*q);
+      *q = nullptr;
+      cap[i] = 0;
+      const hipError_t e = hipMalloc(q, bytes[i]);
+      if (e != hipSuccess) return e;
+      cap[i] = bytes[i];
+    }
+    return hipSuccess;
+  }
   ~Buffers() {
-    for (void* p : {(void*)x, (void*)z, (void*)w, (void*)dx, (void*)dz, (void*)dw, (void*)beta, (void*)dba, (void*)db,
-                    (void*)L, (void*)fs, (void*)partial, (void*)red, (void*)quant, (void*)rows, (void*)fstat,
-                    (void*)active, (void*)active_rows, (void*)tprefix, (void*)lane_of, (void*)rowlist, (void*)nrows,
-                    (void*)ok})
-      (void)hipFree(p);
+    for (int i = 0; i < 23; ++i) (void)hipFree(*slot(i));
   }
 };
+
+void free_workspace(void* b) { delete static_cast<Buffers*>(b); }
 
 // OB_MM_TRACE=1: per-iteration active fits and the final fit statuses on stderr.
 bool trace() {
@@ -900,7 +922,7 @@ bool trace() {
 }
 
 struct MmStats {
-  double assemble_ms = 0.0, fit_rows = 0.0;
+  double assemble_ms = 0.0, fit_rows = 0.0, sync_ms = 0.0;
   int iterations = 0;
   hipEvent_t ev[2] = {nullptr, nullptr};
 };
@@ -955,7 +977,9 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, MmS
     unsigned long long arows = 0;
     MM_OK(hipMemcpyAsync(&active, a.active, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     MM_OK(hipMemcpyAsync(&arows, a.active_rows, sizeof(arows), hipMemcpyDeviceToHost, s));
+    const auto ts = std::chrono::steady_clock::now();
     MM_OK(hipStreamSynchronize(s));
+    st.sync_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
     float ms = 0.f;
     MM_OK(hipEventElapsedTime(&ms, st.ev[0], st.ev[1]));
     st.assemble_ms += ms;
@@ -1031,27 +1055,21 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   const uint32_t rb_cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({want, 256, (48ull << 30) / state_per_rep}));
   const size_t fits = (size_t)rb_cap * 2 * S_pad;
   const int nv_max = K * (K + 1) / 2 + K + 2 > 5 + 2 * K ? K * (K + 1) / 2 + K + 2 : 5 + 2 * K;
-  Buffers b;
+  if (!p->mm_ws) {
+    p->mm_ws = new Buffers();
+    p->mm_ws_free = free_workspace;
+  }
+  Buffers& b = *static_cast<Buffers*>(p->mm_ws);
   const size_t st_elems = (size_t)rb_cap * rep_rows * S_pad;
-  for (double** q : {&b.x, &b.z, &b.w, &b.dx, &b.dz, &b.dw}) MM_OK(hipMalloc(q, sizeof(double) * st_elems));
-  MM_OK(hipMalloc(&b.beta, sizeof(double) * fits * K));
-  MM_OK(hipMalloc(&b.dba, sizeof(double) * fits * K));
-  MM_OK(hipMalloc(&b.db, sizeof(double) * fits * K));
-  MM_OK(hipMalloc(&b.L, sizeof(double) * fits * K * K));
-  MM_OK(hipMalloc(&b.fs, sizeof(double) * fits * kFs));
-  MM_OK(hipMalloc(&b.fstat, sizeof(uint32_t) * fits));
-  MM_OK(hipMalloc(&b.lane_of, sizeof(uint32_t) * fits));
-  MM_OK(hipMalloc(&b.rowlist, sizeof(uint32_t) * (size_t)rb_cap * (nch0 + nch1) * kRc));
-  MM_OK(hipMalloc(&b.nrows, sizeof(uint32_t) * (size_t)rb_cap * (nch0 + nch1)));
-  MM_OK(hipMalloc(&b.partial, sizeof(double) * (size_t)rb_cap * (nch0 + nch1) * S_pad * nv_max));
-  MM_OK(hipMalloc(&b.red, sizeof(double) * fits * nv_max));
-  MM_OK(hipMalloc(&b.active, sizeof(uint32_t)));
-  MM_OK(hipMalloc(&b.active_rows, sizeof(unsigned long long)));
-  MM_OK(hipMalloc(&b.quant, sizeof(double) * n_q));
-  MM_OK(hipMalloc(&b.rows, sizeof(double) * rb_cap * 3 * n_q));
-  MM_OK(hipMalloc(&b.ok, rb_cap));
   const uint32_t nt1 = (p->n[1] + OB_TILE_ROWS - 1) / OB_TILE_ROWS;
-  MM_OK(hipMalloc(&b.tprefix, sizeof(uint32_t) * rb_cap * 2 * (p->ntiles[0] + 1 + nt1 + 1)));
+  const size_t d8 = sizeof(double), u4 = sizeof(uint32_t);
+  const size_t need[23] = {d8 * st_elems, d8 * st_elems, d8 * st_elems, d8 * st_elems, d8 * st_elems,
+                           d8 * st_elems, d8 * fits * K, d8 * fits * K, d8 * fits * K, d8 * fits * K * K,
+                           d8 * fits * kFs, d8 * (size_t)rb_cap * (nch0 + nch1) * S_pad * nv_max,
+                           d8 * fits * nv_max, d8 * n_q, d8 * rb_cap * 3 * n_q, u4 * fits, u4,
+                           sizeof(unsigned long long), u4 * rb_cap * 2 * (p->ntiles[0] + 1 + nt1 + 1), u4 * fits,
+                           u4 * (size_t)rb_cap * (nch0 + nch1) * kRc, u4 * (size_t)rb_cap * (nch0 + nch1), rb_cap};
+  MM_OK(b.reserve(need));
   MM_OK(hipMemcpy(b.quant, quantiles, sizeof(double) * n_q, hipMemcpyHostToDevice));
 
   MmArgs a{};
@@ -1138,6 +1156,9 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   p->timing.mm_fit_rows = st.fit_rows;
   p->timing.mm_iterations = st.iterations;
   p->timing.mm_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  if (trace())
+    fprintf(stderr, "[mm] call: %.1f ms, %.1f ms waiting in per-iteration syncs, assemble %.1f ms\n", p->timing.mm_ms,
+            st.sync_ms, st.assemble_ms);
   if (max_iters) *max_iters = st.iterations;
   return OB_OK;
 }
