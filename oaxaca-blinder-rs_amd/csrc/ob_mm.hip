@@ -153,7 +153,7 @@ struct Blk {
   uint32_t g, gch, slot, fb, r0, n_ent;
   int wave, lane, fl, rl, s;
   size_t F, sb;  // fit index; state index of (fit, group row 0)
-  bool live, wave_live;
+  bool live, wave_live, any;  // any: some fit of the block is live (else the block exits)
   const double* X;
   int64_t ld;
 };
@@ -178,7 +178,8 @@ __device__ __forceinline__ Blk blk_ctx(const MmArgs& a, uint32_t* lst, bool all_
   b.ld = a.ld[b.g];
   b.sb = ((size_t)b.slot * a.rep_rows + (b.g ? a.n[0] : 0u)) * a.S_pad + b.s;
   const size_t li = (size_t)b.slot * (a.nch[0] + a.nch[1]) + b.gch;
-  b.n_ent = a.nrows[li];
+  b.any = __syncthreads_or(b.live) != 0;
+  b.n_ent = b.any ? a.nrows[li] : 0u;
   const uint32_t* L = a.rowlist + li * kRc;
   for (uint32_t i = threadIdx.x; i < b.n_ent; i += 256) lst[i] = L[i];
   return b;
@@ -237,6 +238,7 @@ __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a
   __shared__ __attribute__((aligned(16))) double xs[2][kSub * kXs];
   __shared__ uint32_t lst[kRc];
   const Blk b = blk_ctx(a, lst, mode == 0);
+  if (!b.any) return;  // partials of dead fits are never reduced
   double beta[K];
   double tau = 0.0, ap = 0.0, ad = 0.0, delta = 0.0;
 #pragma unroll
@@ -447,6 +449,7 @@ __global__ __launch_bounds__(256, 2) void mm_affine_kernel(const MmArgs a) {
   __shared__ __attribute__((aligned(16))) double xs[2][kSub * kXs];
   __shared__ uint32_t lst[kRc];
   const Blk b = blk_ctx(a, lst, false);
+  if (!b.any) return;  // partials of dead fits are never reduced
   double beta[K], dba[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -497,6 +500,7 @@ __global__ __launch_bounds__(256, 2) void mm_final_kernel(const MmArgs a) {
   __shared__ __attribute__((aligned(16))) double xs[2][kSub * kXs];
   __shared__ uint32_t lst[kRc];
   const Blk b = blk_ctx(a, lst, false);
+  if (!b.any) return;  // partials of dead fits are never reduced
   double beta[K], dba[K], db[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -537,7 +541,7 @@ __global__ __launch_bounds__(256, 2) void mm_final_kernel(const MmArgs a) {
 }
 
 // Chunk partials -> per-fit values, chunks in a fixed order; the first n_min values are minima.
-__global__ __launch_bounds__(256) void mm_reduce_kernel(const MmArgs a, int nv, int n_min) {
+__global__ __launch_bounds__(256) void mm_reduce_kernel(const MmArgs a, int nv, int n_min, int skip_dead) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   const size_t per_slot = (size_t)2 * a.S_pad * nv;
   if (i >= (size_t)a.n_rb * per_slot) return;
@@ -548,6 +552,7 @@ __global__ __launch_bounds__(256) void mm_reduce_kernel(const MmArgs a, int nv, 
   const uint32_t c0 = g ? a.nch[0] : 0u, nc = a.nch[g];
   const size_t stride = (size_t)a.S_pad * nv;
   const double* P = a.partial + ((size_t)slot * (a.nch[0] + a.nch[1]) + c0) * stride + sv;
+  if (skip_dead && (a.fstat[((size_t)slot * 2 + g) * a.S_pad + sv / nv] & (kDone | kFailed))) return;
   const bool is_min = (int)(sv % nv) < n_min;
   double v = is_min ? 1e300 : 0.0;
   for (uint32_t c = 0; c < nc; ++c) v = is_min ? fmin(v, P[c * stride]) : v + P[c * stride];
@@ -577,7 +582,7 @@ __global__ __launch_bounds__(64) void mm_start_kernel(const MmArgs a, int K) {
     double bv = 0.0;
     for (int k = 0; k < K; ++k) bv += v[k] * R[NP + k];
     const double ssr = fmax(R[NP + K] - bv, 0.0), sc = R[0];
-    delta = 0.1 * (1.0 + sqrt(ssr / sc));  // dual start offset (tools/qr_ipm_proto.py)
+    delta = ssr / sc;  // residual mean square; mm_shift_kernel makes the per-fit dual offset
   }
   for (int s = lane; s < a.S_pad; s += 64) {
     const size_t F = ((size_t)slot * 2 + g) * a.S_pad + s;
@@ -631,6 +636,97 @@ __global__ __launch_bounds__(256) void mm_order_kernel(const MmArgs a, int m2) {
   for (int j = threadIdx.x; j < a.S; j += blockDim.x) {
     a.fs[(base + j) * kFs + FS_TAU] = key[j];
     a.lane_of[base + val[j]] = (uint32_t)j;
+  }
+}
+
+// Per-fit start (block per (slot, group)): the intercept of the OLS start moves to the fit's
+// tau-quantile of the OLS residuals, and the dual offset shrinks to 0.01 (1 + rms of the shifted
+// residual). At n = 250k this takes the extreme quantiles from ~85 to ~30 iterations and leaves the
+// middle unchanged (tools/qr_ipm_proto.py --start). The quantile is a count-weighted one over
+// kShiftSamples list entries taken at a fixed stride of the replicate's nonzero-count rows, so it
+// is a function of the replicate alone.
+constexpr int kShiftSamples = 4096;
+constexpr double kDeltaScale = 0.01;
+__global__ __launch_bounds__(1024) void mm_shift_kernel(const MmArgs a, int K) {
+  __shared__ double key[kShiftSamples];
+  __shared__ double wt[kShiftSamples];
+  __shared__ uint32_t pre[1024 + 1];
+  __shared__ double beta[16];
+  const uint32_t slot = blockIdx.x >> 1, g = blockIdx.x & 1;
+  const uint32_t nch = a.nch[0] + a.nch[1], c0 = g ? a.nch[0] : 0u, ncg = a.nch[g];
+  const size_t F0 = fit_index(a, slot, g, 0);
+  if (a.fstat[F0] & kFailed) return;  // no OLS start for this group: every fit failed already
+  const size_t li0 = (size_t)slot * nch + c0;
+  // inclusive prefix of the chunk list lengths (ncg <= 1024 chunks of kRc rows: n_g < 2^21)
+  for (uint32_t c = threadIdx.x; c < ncg; c += blockDim.x) pre[c + 1] = a.nrows[li0 + c];
+  if (threadIdx.x == 0) pre[0] = 0;
+  if (threadIdx.x < (unsigned)K) beta[threadIdx.x] = a.beta[F0 * K + threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (uint32_t c = 1; c <= ncg; ++c) pre[c] += pre[c - 1];
+  __syncthreads();
+  const uint32_t tot = pre[ncg];
+  const int m = (int)min<uint32_t>(tot, (uint32_t)kShiftSamples);
+  for (int j = threadIdx.x; j < kShiftSamples; j += blockDim.x) {
+    double r = INFINITY, c = 0.0;
+    if (j < m) {
+      const uint32_t e = (uint32_t)(((uint64_t)j * tot) / (uint32_t)m);
+      uint32_t lo = 0, hi = ncg;  // chunk with pre[lo] <= e < pre[lo + 1]
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pre[mid] <= e) lo = mid;
+        else hi = mid;
+      }
+      const uint32_t ent = a.rowlist[(li0 + lo) * kRc + (e - pre[lo])];
+      const uint32_t row = lo * kRc + (ent >> 8);
+      const double* X = a.cols[g];
+      double xb = beta[0];
+      for (int k = 1; k < K; ++k) xb += X[(size_t)(k - 1) * a.ld[g] + row] * beta[k];
+      r = X[(size_t)a.p * a.ld[g] + row] - xb;
+      c = (double)(ent & 255u);
+    }
+    key[j] = r;
+    wt[j] = c;
+  }
+  __syncthreads();
+  for (int k = 2; k <= kShiftSamples; k <<= 1)  // bitonic sort by residual, weights along
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < kShiftSamples; i += blockDim.x) {
+        const int l = i ^ j;
+        if (l > i) {
+          const bool up = (i & k) == 0;
+          const double x = key[i], y = key[l];
+          if ((x > y) == up) {
+            key[i] = y;
+            key[l] = x;
+            const double t = wt[i];
+            wt[i] = wt[l];
+            wt[l] = t;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  if (threadIdx.x == 0)  // inclusive prefix of the weights (in place, serial: 4096 adds once per batch)
+    for (int i = 1; i < m; ++i) wt[i] += wt[i - 1];
+  __syncthreads();
+  const double W = m ? wt[m - 1] : 0.0;
+  for (int s = threadIdx.x; s < a.S; s += blockDim.x) {
+    const size_t F = F0 + s;
+    double* f = a.fs + F * kFs;
+    double q = 0.0;
+    if (m) {
+      const double target = f[FS_TAU] * W;
+      int lo = 0, hi = m - 1;  // first i with wt[i] >= target
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (wt[mid] >= target) hi = mid;
+        else lo = mid + 1;
+      }
+      q = key[lo];
+    }
+    a.beta[F * K] = beta[0] + q;
+    f[FS_DELTA] = kDeltaScale * (1.0 + sqrt(f[FS_DELTA] + q * q));
   }
 }
 
@@ -934,9 +1030,10 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, MmS
   const int nv1 = NP + K + 2, nv2 = 5 + 2 * K;
   const size_t n_fits = (size_t)a.n_rb * 2 * a.S_pad;
   const dim3 grid(nch, a.S_pad / 64, a.n_rb);
-  auto reduce = [&](int nv, int n_min) -> hipError_t {
+  auto reduce = [&](int nv, int n_min, int skip_dead = 1) -> hipError_t {
     const size_t tot = n_fits * nv;
-    hipLaunchKernelGGL(mm_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, a, nv, n_min);
+    hipLaunchKernelGGL(mm_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, a, nv, n_min,
+                       skip_dead);
     return hipGetLastError();
   };
   const size_t lds_solve = sizeof(double) * ((size_t)K * K + K);
@@ -946,7 +1043,7 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, MmS
   MM_OK(hipMemsetAsync(a.active_rows, 0, sizeof(unsigned long long), s));
   pass(K, 0, a, dim3(nch, 1, a.n_rb), 0, s);
   MM_OK(hipGetLastError());
-  MM_OK(reduce(nv1, 0));
+  MM_OK(reduce(nv1, 0, 0));  // the OLS sums sit in fit 0 (the statuses are not set yet)
   hipLaunchKernelGGL(mm_start_kernel, dim3(a.n_rb * 2), dim3(64), lds_solve, s, a, K);
   MM_OK(hipGetLastError());
   int m2 = 1;
@@ -954,6 +1051,8 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, MmS
   const size_t lds_ord = (size_t)m2 * (sizeof(double) + sizeof(uint32_t));
   MM_OK(hipFuncSetAttribute((const void*)mm_order_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_ord));
   hipLaunchKernelGGL(mm_order_kernel, dim3(a.n_rb * 2), dim3(256), lds_ord, s, a, m2);
+  MM_OK(hipGetLastError());
+  hipLaunchKernelGGL(mm_shift_kernel, dim3(a.n_rb * 2), dim3(1024), 0, s, a, K);
   MM_OK(hipGetLastError());
   int it = 0;
   uint64_t live_rows = 0;  // first assemble: every fit of a group whose OLS start exists (mm_start_kernel)
@@ -1049,6 +1148,8 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   const int S_pad = (sims + 63) / 64 * 64;
   const size_t rep_rows = (size_t)p->n[0] + p->n[1];
   const uint32_t nch0 = (p->n[0] + kRc - 1) / kRc, nch1 = (p->n[1] + kRc - 1) / kRc;
+  if (nch0 > 1024 || nch1 > 1024)  // mm_shift_kernel's chunk prefix
+    return ob::fail(OB_E_UNSUPPORTED, "Machado-Mata groups take at most %u rows", 1024u * kRc);
   // replicate slots per batch: IPM state (6 f64 per fit and row) within 48 GB
   const size_t state_per_rep = 6 * rep_rows * S_pad * sizeof(double);
   const uint64_t want = std::max<uint64_t>(n_reps, 1);

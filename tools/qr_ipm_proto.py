@@ -3,15 +3,18 @@ on the bounded dual LP  max y'x  s.t.  X'x = (1 - tau) X'c,  0 <= x <= c  (c = r
 whose equality multipliers are the QR coefficients. Pass structure mirrors the kernels:
   assemble (M = X'QX, X'q r), affine step + corrector right-hand sides, final step lengths.
 Design aid only (compared here with scipy HiGHS); the oracle does not use it.
-usage: python tools/qr_ipm_proto.py
+usage: python tools/qr_ipm_proto.py [--start]   (--start: iteration counts of the OLS start vs the
+shifted start of mm_shift_kernel at n = 250k, the configs[4] group size)
 """
+import sys
+
 import numpy as np
 from scipy.optimize import linprog
 
 NO_RP = True  # the kernels assume A x = b (feasible start, A dx = 0 steps)
 
 
-def qr_ipm(X, y, c, tau, tol=1e-12, max_iter=100, eta=0.99995):
+def qr_ipm(X, y, c, tau, tol=1e-12, max_iter=100, eta=0.99995, shift=True):
     act = c > 0
     X, y, c = X[act], y[act], c[act].astype(float)
     n, K = X.shape
@@ -21,7 +24,14 @@ def qr_ipm(X, y, c, tau, tol=1e-12, max_iter=100, eta=0.99995):
     G = (X.T * c) @ X
     beta = np.linalg.solve(G, X.T @ (c * y))
     r = y - X @ beta
-    dlt = 0.1 * (1.0 + np.sqrt((c * r * r).sum() / c.sum()))  # from the OLS Gram on the GPU
+    if shift:  # mm_shift_kernel: intercept to the tau-quantile of the OLS residuals (count-weighted)
+        o = np.argsort(r)
+        cw = np.cumsum(c[o])
+        beta[0] += r[o][np.searchsorted(cw, tau * cw[-1])]
+        r = y - X @ beta
+        dlt = 0.01 * (1.0 + np.sqrt((c * r * r).sum() / c.sum()))
+    else:  # the plain OLS start
+        dlt = 0.1 * (1.0 + np.sqrt((c * r * r).sum() / c.sum()))
     z = np.maximum(-r, 0.0) + dlt
     w = np.maximum(r, 0.0) + dlt
     for it in range(1, max_iter + 1):
@@ -99,5 +109,17 @@ def main():
     print("worst", worst, "iterations median", np.median(its), "max", max(its))
 
 
+def start_study():
+    sys.path.insert(0, __file__.rsplit("/", 2)[0])
+    import bench
+
+    d = bench.synthetic(500000, 15, False)
+    X = np.column_stack([np.ones(250000), d["xa"]])
+    c = np.random.default_rng(3).multinomial(250000, np.ones(250000) / 250000)
+    for tau in (0.01, 0.05, 0.2, 0.5, 0.8, 0.95, 0.99):
+        its = [qr_ipm(X, d["ya"], c, tau, max_iter=300, shift=sh)[1] for sh in (False, True)]
+        print(f"tau={tau:.2f} iterations: OLS start {its[0]}, shifted start {its[1]}", flush=True)
+
+
 if __name__ == "__main__":
-    main()
+    start_study() if "--start" in sys.argv else main()
