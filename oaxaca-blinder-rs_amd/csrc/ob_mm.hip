@@ -66,8 +66,8 @@ struct MmArgs {
   uint32_t nb_rep, rep_pad;
   uint32_t nch[2];
   size_t rep_rows;         // n0 + n1: state rows per replicate
-  double *x, *z, *w, *dx, *dz, *dw;  // [slot][row (A then B)][S_pad]
-  double *beta, *dba, *db;           // [fit][K]
+  double *x, *z, *w;                 // [slot][row (A then B)][S_pad]
+  double *beta, *bprev, *dba, *db;   // [fit][K]; bprev: beta the last directions were taken at
   double* L;                         // [fit][K*K]
   double* fs;                        // [fit][kFs]
   uint32_t* fstat;                   // [fit]
@@ -226,9 +226,76 @@ __device__ __forceinline__ double rows_min(double v) {
   return fmin(v, __shfl_xor(v, 32));
 }
 
+// Per-fit vectors as MFMA B fragments: f[kb] = v[fit][4 kb + rl] (zero past K or for dead lanes).
+template <int K>
+__device__ __forceinline__ void bfrag(const double* v, const Blk& b, bool on, double (&f)[(K + 3) / 4]) {
+#pragma unroll
+  for (int kb = 0; kb < (K + 3) / 4; ++kb) {
+    const int k = 4 * kb + b.rl;
+    f[kb] = (on && k < K) ? v[b.F * K + k] : 0.0;
+  }
+}
+
+// x_i . v for the 16 rows of step group G (steps 4G..4G+3 of a sub-tile) against each lane's fit,
+// on f64 MFMA: A = the staged rows (m = row 16G + fl, k), B = the fragments (k, n = fit). D element
+// i is this lane's row of step 4G + i (row 16G + rl + 4i), the (fit, row) pair the step holds.
+template <int K, int NV>
+__device__ __forceinline__ void group_dots(const double* X, int G, const Blk& b,
+                                           const double (&f)[NV][(K + 3) / 4], mm_d4 (&d)[NV]) {
+#pragma unroll
+  for (int v = 0; v < NV; ++v) d[v] = (mm_d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int kb = 0; kb < (K + 3) / 4; ++kb) {
+    const double av = X[(16 * G + b.fl) * kXs + 4 * kb + b.rl];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) d[v] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, f[v][kb], d[v], 0, 0, 0);
+  }
+}
+
+// Per-row affine direction from the current state (shared by mm_affine, mm_final and the step
+// replay of mm_assemble).
+struct Affine {
+  double xv, zv, wv, sv, ix, is, q, r, dxa, dza, dwa;  // ix = 1/x, is = 1/s (divisions shared)
+};
+
+// xb = x_i . beta, xd = x_i . dba (group_dots).
+__device__ __forceinline__ Affine affine_row(double xv, double zv, double wv, double c, double y, double xb,
+                                             double xd) {
+  Affine f;
+  f.xv = xv;
+  f.zv = zv;
+  f.wv = wv;
+  f.sv = c - f.xv;
+  f.r = y - xb;
+  f.ix = 1.0 / f.xv;
+  f.is = 1.0 / f.sv;
+  f.q = 1.0 / (f.zv * f.ix + f.wv * f.is);
+  f.dxa = f.q * (f.r - xd);
+  f.dza = -f.zv - f.zv * f.dxa * f.ix;
+  f.dwa = -f.wv + f.wv * f.dxa * f.is;
+  return f;
+}
+
+// Per-row corrector direction (mm_final for the step bounds; mm_assemble replays it to take the
+// step, so the direction is never stored). xd = x_i . db (group_dots).
+struct Corrector {
+  double dx, dz, dw;
+};
+__device__ __forceinline__ Corrector corrector_row(const Affine& f, double xd, double sigmu) {
+  Corrector o;
+  const double rho = f.r - f.dxa * (f.dwa * f.is + f.dza * f.ix) + sigmu * (f.ix - f.is);
+  o.dx = f.q * (rho - xd);
+  const double rxz = sigmu - f.xv * f.zv - f.dxa * f.dza;
+  const double rsw = sigmu - f.sv * f.wv + f.dxa * f.dwa;
+  o.dz = (rxz - f.zv * o.dx) * f.ix;
+  o.dw = (rsw + f.wv * o.dx) * f.is;
+  return o;
+}
+
 // mm_assemble: mode 0: weighted OLS of the replicate (q = c, rho = y) -> M, X'Cy, sum c y^2, n_act;
-// mode 1: start point (x = (1 - tau) c, z/w from the OLS residual) + assemble; mode 2 (STEP): apply
-// the last step (x += ap dx, z += ad dz, w += ad dw) + assemble. M = X'QX and X'Q r on f64 MFMA:
+// mode 1: start point (x = (1 - tau) c, z/w from the OLS residual) + assemble; mode 2 (STEP): replay
+// the last corrector direction from (bprev, dba, db, sigma mu) and take the step (x += ap dx,
+// z += ad dz, w += ad dw) + assemble. Only x, z, w cross HBM. M = X'QX and X'Q r on f64 MFMA:
 // column block cb < NCB has B = x_i x_j of pair columns cb*16.. (ob_pair_index order), block NCB
 // has A = q r and B = x.
 template <int K, bool STEP>
@@ -239,15 +306,21 @@ __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a
   __shared__ uint32_t lst[kRc];
   const Blk b = blk_ctx(a, lst, mode == 0);
   if (!b.any) return;  // partials of dead fits are never reduced
-  double beta[K];
-  double tau = 0.0, ap = 0.0, ad = 0.0, delta = 0.0;
-#pragma unroll
-  for (int k = 0; k < K; ++k) beta[k] = (b.live && mode) ? a.beta[b.F * K + k] : 0.0;
+  constexpr int NDOT = STEP ? 3 : 1;  // x_i . (bprev, dba, db) or x_i . beta
+  double fb[NDOT][(K + 3) / 4];
+  bfrag<K>(STEP ? a.bprev : a.beta, b, b.live && mode, fb[0]);
+  if (STEP) {
+    bfrag<K>(a.dba, b, b.live, fb[NDOT > 1 ? 1 : 0]);
+    bfrag<K>(a.db, b, b.live, fb[NDOT > 2 ? 2 : 0]);
+  }
+  mm_d4 dots[NDOT];
+  double tau = 0.0, ap = 0.0, ad = 0.0, delta = 0.0, sigmu = 0.0;
   if (b.live && mode) {
     tau = a.fs[b.F * kFs + FS_TAU];
     ap = a.fs[b.F * kFs + FS_AP];
     ad = a.fs[b.F * kFs + FS_AD];
     delta = a.fs[b.F * kFs + FS_DELTA];
+    sigmu = a.fs[b.F * kFs + FS_SIGMU];
   }
   // B-operand columns (i, j) of this lane (n = fl) per pair block, packed i | j << 8; kXzero
   // past the last pair
@@ -275,16 +348,13 @@ __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a
     double stg[kStage];
     xs_load<K>(a, b, lst, 0, stg);
     xs_store(xs[0], stg);
-    double rx[kRingA], rz[kRingA], rw[kRingA], rdx[kRingA], rdz[kRingA], rdw[kRingA];
+    double rx[kRingA], rz[kRingA], rw[kRingA];
     auto load = [&](int k, uint32_t e) {
       if (STEP) {
         const size_t si = state_at(a, b, lst, e);
         rx[k] = a.x[si];
         rz[k] = a.z[si];
         rw[k] = a.w[si];
-        rdx[k] = a.dx[si];
-        rdz[k] = a.dz[si];
-        rdw[k] = a.dw[si];
       }
     };
 #pragma unroll
@@ -294,8 +364,9 @@ __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a
       const double* X = xs[t & 1];
       xs_load<K>(a, b, lst, t + 1, stg);
       auto step = [&](int j) {
+          if ((j & 3) == 0 && mode) group_dots<K, NDOT>(X, j >> 2, b, fb, dots);
           const int k = j % kRingA;
-          const double cx = rx[k], cz = rz[k], cw = rw[k], cdx = rdx[k], cdz = rdz[k], cdw = rdw[k];
+          const double cx = rx[k], cz = rz[k], cw = rw[k];
           const uint32_t e = t * kSub + 4 * j + b.rl;
           load(k, e + 4 * kRingA);
           const bool valid = e < b.n_ent && b.live;
@@ -310,19 +381,20 @@ __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a
               gap += c * y * y;
               obj += 1.0;
             } else {
-              double xb = 0.0;
-#pragma unroll
-              for (int k2 = 0; k2 < K; ++k2) xb += xr[k2] * beta[k2];
-              const double r = y - xb;
-              double xv, zv, wv;
+              double xv, zv, wv, r;
               if (!STEP) {
+                r = y - dots[0][j & 3];
                 xv = (1.0 - tau) * c;
                 zv = fmax(-r, 0.0) + delta;
                 wv = fmax(r, 0.0) + delta;
               } else {
-                xv = cx + ap * cdx;
-                zv = cz + ad * cdz;
-                wv = cw + ad * cdw;
+                const Affine f = affine_row(cx, cz, cw, c, y, dots[0][j & 3], dots[NDOT > 1 ? 1 : 0][j & 3]);
+                const double xdb = dots[NDOT > 2 ? 2 : 0][j & 3];
+                const Corrector d = corrector_row(f, xdb, sigmu);
+                xv = cx + ap * d.dx;
+                zv = cz + ad * d.dz;
+                wv = cw + ad * d.dw;
+                r = f.r - ad * xdb;  // y - x_i . (bprev + ad db)
               }
               const size_t si = b.sb + (size_t)(b.r0 + (lst[e] >> 8)) * a.S_pad;
               a.x[si] = xv;
@@ -371,40 +443,13 @@ __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a
   }
 }
 
-// Per-row affine direction from the current state (shared by mm_affine / mm_final).
-struct Affine {
-  double xv, zv, wv, sv, ix, is, q, r, dxa, dza, dwa;  // ix = 1/x, is = 1/s (divisions shared)
-};
-
-template <int K>
-__device__ __forceinline__ Affine affine_row(double xv, double zv, double wv, double c, const double* xr,
-                                             const double (&beta)[K], const double (&dba)[K]) {
-  Affine f;
-  f.xv = xv;
-  f.zv = zv;
-  f.wv = wv;
-  f.sv = c - f.xv;
-  double xb = 0.0, xd = 0.0;
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    xb += xr[k] * beta[k];
-    xd += xr[k] * dba[k];
-  }
-  f.r = xr[kXy] - xb;
-  f.ix = 1.0 / f.xv;
-  f.is = 1.0 / f.sv;
-  f.q = 1.0 / (f.zv * f.ix + f.wv * f.is);
-  f.dxa = f.q * (f.r - xd);
-  f.dza = -f.zv - f.zv * f.dxa * f.ix;
-  f.dwa = -f.wv + f.wv * f.dxa * f.is;
-  return f;
-}
-
 // The affine / final passes share the walk: state (x, z, w) streamed kRing steps ahead, the
-// design values from the double-buffered sub-tiles. body(j-th step's state, valid, count, xr, e).
-template <int K, typename Body>
+// design values from the double-buffered sub-tiles, x_i . v for the fragments fb on MFMA once per
+// 4 steps. body(j-th step's state, valid, count, xr, dots).
+template <int K, int NDOT, typename Body>
 __device__ __forceinline__ void state_walk(const MmArgs& a, const Blk& b, const uint32_t* lst, double (*xs)[kSub * kXs],
-                                           Body&& body) {
+                                           const double (&fb)[NDOT][(K + 3) / 4], Body&& body) {
+  mm_d4 dots[NDOT];
   const uint32_t nsub = (b.n_ent + kSub - 1) / kSub;
   if (!__syncthreads_or(b.live) || !nsub) return;
   double stg[kStage];
@@ -424,12 +469,16 @@ __device__ __forceinline__ void state_walk(const MmArgs& a, const Blk& b, const 
     const double* X = xs[t & 1];
     xs_load<K>(a, b, lst, t + 1, stg);
     auto step = [&](int j) {
+      if ((j & 3) == 0) group_dots<K, NDOT>(X, j >> 2, b, fb, dots);
       const int k = j % kRing;
       const double xv = rx[k], zv = rz[k], wv = rw[k];
       const uint32_t e = t * kSub + 4 * j + b.rl;
       load(k, e + 4 * kRing);
       const bool valid = e < b.n_ent && b.live;
-      body(xv, zv, wv, valid, valid ? (double)(lst[e] & 255u) : 1.0, X + (4 * j + b.rl) * kXs, e);
+      double dv[NDOT];
+#pragma unroll
+      for (int v = 0; v < NDOT; ++v) dv[v] = dots[v][j & 3];
+      body(xv, zv, wv, valid, valid ? (double)(lst[e] & 255u) : 1.0, X + (4 * j + b.rl) * kXs, dv);
     };
     if (b.wave_live)
 #pragma unroll
@@ -450,19 +499,17 @@ __global__ __launch_bounds__(256, 2) void mm_affine_kernel(const MmArgs a) {
   __shared__ uint32_t lst[kRc];
   const Blk b = blk_ctx(a, lst, false);
   if (!b.any) return;  // partials of dead fits are never reduced
-  double beta[K], dba[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    beta[k] = b.live ? a.beta[b.F * K + k] : 0.0;
-    dba[k] = b.live ? a.dba[b.F * K + k] : 0.0;
-  }
+  double fb[2][(K + 3) / 4];
+  bfrag<K>(a.beta, b, b.live, fb[0]);
+  bfrag<K>(a.dba, b, b.live, fb[1]);
   double acc[5] = {1e300, 1e300, 0.0, 0.0, 0.0};
   mm_d4 m0 = {0.0, 0.0, 0.0, 0.0}, m1 = {0.0, 0.0, 0.0, 0.0};
   __syncthreads();  // lst
-  state_walk<K>(a, b, lst, xs, [&](double xv, double zv, double wv, bool valid, double c, const double* xr, uint32_t) {
+  state_walk<K, 2>(a, b, lst, xs, fb, [&](double xv, double zv, double wv, bool valid, double c, const double* xr,
+                                          const double (&dv)[2]) {
     double q0 = 0.0, q1 = 0.0;
     if (valid) {
-      const Affine f = affine_row<K>(xv, zv, wv, c, xr, beta, dba);
+      const Affine f = affine_row(xv, zv, wv, c, xr[kXy], dv[0], dv[1]);
       if (f.dxa != 0.0) acc[0] = fmin(acc[0], (f.dxa < 0.0 ? -f.xv : f.sv) / f.dxa);
       if (f.dza < 0.0) acc[1] = fmin(acc[1], -f.zv / f.dza);
       if (f.dwa < 0.0) acc[1] = fmin(acc[1], -f.wv / f.dwa);
@@ -494,39 +541,26 @@ __global__ __launch_bounds__(256, 2) void mm_affine_kernel(const MmArgs a) {
     for (int i = 0; i < 5; ++i) P[(fw + b.fl) * NV + i] = acc[i];
 }
 
-// Corrector direction (stored for the next assemble) and its step-length bounds.
+// Step-length bounds of the corrector direction (the next assemble replays the direction).
 template <int K>
 __global__ __launch_bounds__(256, 2) void mm_final_kernel(const MmArgs a) {
   __shared__ __attribute__((aligned(16))) double xs[2][kSub * kXs];
   __shared__ uint32_t lst[kRc];
   const Blk b = blk_ctx(a, lst, false);
   if (!b.any) return;  // partials of dead fits are never reduced
-  double beta[K], dba[K], db[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    beta[k] = b.live ? a.beta[b.F * K + k] : 0.0;
-    dba[k] = b.live ? a.dba[b.F * K + k] : 0.0;
-    db[k] = b.live ? a.db[b.F * K + k] : 0.0;
-  }
+  double fb[3][(K + 3) / 4];
+  bfrag<K>(a.beta, b, b.live, fb[0]);
+  bfrag<K>(a.dba, b, b.live, fb[1]);
+  bfrag<K>(a.db, b, b.live, fb[2]);
   const double sigmu = b.live ? a.fs[b.F * kFs + FS_SIGMU] : 0.0;
   double acc[2] = {1e300, 1e300};
   __syncthreads();  // lst
-  state_walk<K>(a, b, lst, xs, [&](double xv, double zv, double wv, bool valid, double c, const double* xr, uint32_t e) {
+  state_walk<K, 3>(a, b, lst, xs, fb, [&](double xv, double zv, double wv, bool valid, double c, const double* xr,
+                                          const double (&dv)[3]) {
     if (!valid) return;
-    const Affine f = affine_row<K>(xv, zv, wv, c, xr, beta, dba);
-    const double rho = f.r - f.dxa * (f.dwa * f.is + f.dza * f.ix) + sigmu * (f.ix - f.is);
-    double xd = 0.0;
-#pragma unroll
-    for (int k = 0; k < K; ++k) xd += xr[k] * db[k];
-    const double dx = f.q * (rho - xd);
-    const double rxz = sigmu - f.xv * f.zv - f.dxa * f.dza;
-    const double rsw = sigmu - f.sv * f.wv + f.dxa * f.dwa;
-    const double dz = (rxz - f.zv * dx) * f.ix;
-    const double dw = (rsw + f.wv * dx) * f.is;
-    const size_t si = b.sb + (size_t)(b.r0 + (lst[e] >> 8)) * a.S_pad;
-    a.dx[si] = dx;
-    a.dz[si] = dz;
-    a.dw[si] = dw;
+    const Affine f = affine_row(xv, zv, wv, c, xr[kXy], dv[0], dv[1]);
+    const Corrector d = corrector_row(f, dv[2], sigmu);
+    const double dx = d.dx, dz = d.dz, dw = d.dw;
     if (dx != 0.0) acc[0] = fmin(acc[0], (dx < 0.0 ? -f.xv : f.sv) / dx);
     if (dz < 0.0) acc[1] = fmin(acc[1], -f.zv / dz);
     if (dw < 0.0) acc[1] = fmin(acc[1], -f.wv / dw);
@@ -801,7 +835,10 @@ __global__ __launch_bounds__(256) void mm_step_kernel(const MmArgs a, int K, siz
   if (F >= n_fits || (a.fstat[F] & (kDone | kFailed))) return;
   const double* R = a.red + F * 2;
   const double ap = fmin(1.0, kEta * R[0]), ad = fmin(1.0, kEta * R[1]);
-  for (int k = 0; k < K; ++k) a.beta[F * K + k] += ad * a.db[F * K + k];
+  for (int k = 0; k < K; ++k) {
+    a.bprev[F * K + k] = a.beta[F * K + k];
+    a.beta[F * K + k] += ad * a.db[F * K + k];
+  }
   a.fs[F * kFs + FS_AP] = ap;
   a.fs[F * kFs + FS_AD] = ad;
 }
@@ -975,24 +1012,25 @@ void pass(int K, int which, const MmArgs& a, dim3 grid, int mode, hipStream_t s)
 // MM workspace, kept on the panel between calls and grown on demand (the IPM state alone is
 // tens of GB: allocating and freeing it per call cost more than the passes at configs[4]).
 struct Buffers {
-  double *x = nullptr, *z = nullptr, *w = nullptr, *dx = nullptr, *dz = nullptr, *dw = nullptr;
-  double *beta = nullptr, *dba = nullptr, *db = nullptr, *L = nullptr, *fs = nullptr;
+  double *x = nullptr, *z = nullptr, *w = nullptr;
+  double *beta = nullptr, *bprev = nullptr, *dba = nullptr, *db = nullptr, *L = nullptr, *fs = nullptr;
   double *partial = nullptr, *red = nullptr, *quant = nullptr, *rows = nullptr;
   uint32_t *fstat = nullptr, *active = nullptr, *tprefix = nullptr, *lane_of = nullptr, *rowlist = nullptr,
            *nrows = nullptr;
   unsigned long long* active_rows = nullptr;
   uint8_t* ok = nullptr;
-  size_t cap[23] = {};
+  static constexpr int kSlots = 21;
+  size_t cap[kSlots] = {};
   void** slot(int i) {
-    void** v[23] = {(void**)&x, (void**)&z, (void**)&w, (void**)&dx, (void**)&dz, (void**)&dw, (void**)&beta,
+    void** v[kSlots] = {(void**)&x, (void**)&z, (void**)&w, (void**)&beta, (void**)&bprev,
                     (void**)&dba, (void**)&db, (void**)&L, (void**)&fs, (void**)&partial, (void**)&red,
                     (void**)&quant, (void**)&rows, (void**)&fstat, (void**)&active, (void**)&active_rows,
                     (void**)&tprefix, (void**)&lane_of, (void**)&rowlist, (void**)&nrows, (void**)&ok};
     return v[i];
   }
   // bytes[i] for slot i; reallocates the slots that are too small
-  hipError_t reserve(const size_t (&bytes)[23]) {
-    for (int i = 0; i < 23; ++i) {
+  hipError_t reserve(const size_t (&bytes)[kSlots]) {
+    for (int i = 0; i < kSlots; ++i) {
       if (bytes[i] <= cap[i]) continue;
       void** q = slot(i);
       (void)hipFree(*q);
@@ -1005,7 +1043,7 @@ struct Buffers {
     return hipSuccess;
   }
   ~Buffers() {
-    for (int i = 0; i < 23; ++i) (void)hipFree(*slot(i));
+    for (int i = 0; i < kSlots; ++i) (void)hipFree(*slot(i));
   }
 };
 
@@ -1150,8 +1188,8 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   const uint32_t nch0 = (p->n[0] + kRc - 1) / kRc, nch1 = (p->n[1] + kRc - 1) / kRc;
   if (nch0 > 1024 || nch1 > 1024)  // mm_shift_kernel's chunk prefix
     return ob::fail(OB_E_UNSUPPORTED, "Machado-Mata groups take at most %u rows", 1024u * kRc);
-  // replicate slots per batch: IPM state (6 f64 per fit and row) within 48 GB
-  const size_t state_per_rep = 6 * rep_rows * S_pad * sizeof(double);
+  // replicate slots per batch: IPM state (x, z, w: 3 f64 per fit and row) within 48 GB
+  const size_t state_per_rep = 3 * rep_rows * S_pad * sizeof(double);
   const uint64_t want = std::max<uint64_t>(n_reps, 1);
   const uint32_t rb_cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({want, 256, (48ull << 30) / state_per_rep}));
   const size_t fits = (size_t)rb_cap * 2 * S_pad;
@@ -1164,8 +1202,8 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   const size_t st_elems = (size_t)rb_cap * rep_rows * S_pad;
   const uint32_t nt1 = (p->n[1] + OB_TILE_ROWS - 1) / OB_TILE_ROWS;
   const size_t d8 = sizeof(double), u4 = sizeof(uint32_t);
-  const size_t need[23] = {d8 * st_elems, d8 * st_elems, d8 * st_elems, d8 * st_elems, d8 * st_elems,
-                           d8 * st_elems, d8 * fits * K, d8 * fits * K, d8 * fits * K, d8 * fits * K * K,
+  const size_t need[Buffers::kSlots] = {d8 * st_elems, d8 * st_elems, d8 * st_elems, d8 * fits * K,
+                           d8 * fits * K, d8 * fits * K, d8 * fits * K, d8 * fits * K * K,
                            d8 * fits * kFs, d8 * (size_t)rb_cap * (nch0 + nch1) * S_pad * nv_max,
                            d8 * fits * nv_max, d8 * n_q, d8 * rb_cap * 3 * n_q, u4 * fits, u4,
                            sizeof(unsigned long long), u4 * rb_cap * 2 * (p->ntiles[0] + 1 + nt1 + 1), u4 * fits,
@@ -1189,10 +1227,8 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   a.x = b.x;
   a.z = b.z;
   a.w = b.w;
-  a.dx = b.dx;
-  a.dz = b.dz;
-  a.dw = b.dw;
   a.beta = b.beta;
+  a.bprev = b.bprev;
   a.dba = b.dba;
   a.db = b.db;
   a.L = b.L;
