@@ -143,8 +143,8 @@ def bench_mm(args, world, rank, local, dist):
     if rank != 0:
         return
     k = args.preds + 1
-    bytes_row = 72.0  # mm_assemble per live (fit, row): x, z, w, dx, dz, dw read, x, z, w written
-    flops_row = 2.0 * (k * (k + 1) / 2 + 2 * k)  # X'QX pairs, X'Q r, X beta
+    bytes_row = 48.0  # mm_assemble per live (fit, row): x, z, w read, x, z, w written (direction replayed)
+    flops_row = 2.0 * (k * (k + 1) / 2 + 4 * k)  # X'QX pairs, X'Q r, x.bprev, x.dba, x.db
     gbps = fit_rows * bytes_row / (asm_ms * 1e-3) / 1e9
     value = world * R * args.steps / elapsed
     out = {

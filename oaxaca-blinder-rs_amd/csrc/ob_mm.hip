@@ -493,7 +493,7 @@ __device__ __forceinline__ void state_walk(const MmArgs& a, const Blk& b, const 
 
 // [0] primal step bound, [1] dual step bound, [2..4] mu_aff terms, then X'q rho0, X'q rho1.
 template <int K>
-__global__ __launch_bounds__(256, 2) void mm_affine_kernel(const MmArgs a) {
+__global__ __launch_bounds__(256, 3) void mm_affine_kernel(const MmArgs a) {
   constexpr int NV = 5 + 2 * K;
   __shared__ __attribute__((aligned(16))) double xs[2][kSub * kXs];
   __shared__ uint32_t lst[kRc];
