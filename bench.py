@@ -167,6 +167,127 @@ def bench_mm(args, world, rank, local, dist):
     print(json.dumps(out), flush=True)
 
 
+def heckman_frame(rows, preds, seed=20260425):
+    """configs[1]'s wage panel plus a selection equation (builder .heckman_selection): s = 1[0.3 +
+    0.5 z1 - 0.4 z2 + 0.2 x4 + u > 0], outcomes kept on unselected rows (tests/test_gpu_heckman.py's
+    design at scale). Returns (frame, predictor names, selection predictor names)."""
+    d = synthetic(rows, preds, False)
+    rng = np.random.default_rng(seed)
+    x = np.vstack([d["xa"], d["xb"]])
+    n = x.shape[0]
+    z1, z2 = rng.normal(size=n), rng.normal(size=n)
+    s = (0.3 + 0.5 * z1 - 0.4 * z2 + 0.2 * x[:, 3] + rng.normal(size=n) > 0).astype(np.float64)
+    names = [f"x{j + 1}" for j in range(preds)]
+    frame = {"y": np.concatenate([d["ya"], d["yb"]]),
+             "g": np.array(["M"] * len(d["ya"]) + ["F"] * len(d["yb"]), dtype=object), "s": s, "z1": z1, "z2": z2}
+    frame.update({nm: np.ascontiguousarray(x[:, j]) for j, nm in enumerate(names)})
+    return frame, names, ["z1", "z2", "x4"]
+
+
+def bench_heckman(args, world, rank, local, dist):
+    """Heckman two-step bootstrap (estimation.rs:114-260) on configs[1]'s panel: per replicate the
+    probit of s on [1, z1, z2, x4] by Fisher scoring, the IMR sums and the IMR-augmented solve."""
+    import torch
+
+    ob = importlib.import_module("oaxaca-blinder-rs_amd")
+    frame, names, zs = heckman_frame(args.rows, args.preds)
+    b = (ob.OaxacaBuilder(frame, "y", "g", "F").predictors(names).heckman_selection("s", zs)
+         .bootstrap_reps(args.reps).seed(0x0B5EED).device(local))
+    pr = b.prepare()
+    B, dev = args.reps, torch.device("cuda", local)
+    rows = torch.empty((B, pr.row_len), dtype=torch.float64, device=dev)
+    ok = torch.empty(B, dtype=torch.uint8, device=dev)
+
+    def step(i):
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        pr.boot_device((i * world + rank) * B, B, rows.data_ptr(), ok.data_ptr(), stream)
+        if dist:
+            g = torch.empty((world * B, pr.row_len), dtype=torch.float64, device=dev)
+            dist.all_gather_into_tensor(g, rows)
+        pr.sync()
+        return pr.timing()
+
+    for i in range(args.warmup):
+        step(i)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    tm_sum = {"gram_ms": 0.0, "heckman_ms": 0.0, "level1_ms": 0.0, "counts_ms": 0.0}
+    iters = 0
+    for i in range(args.steps):
+        tm = step(args.warmup + i)
+        for k_ in tm_sum:
+            tm_sum[k_] += tm[k_]
+        iters = max(iters, tm["probit_iterations"])
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    tt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    elapsed = float(tt[0])
+    if rank != 0:
+        pr.close()
+        return
+    k = args.preds + 1  # selected-row X'X, X'y: the extended Gram with weight column [s == 1]
+    flops_rep = 2.0 * args.rows * (k * (k + 1) / 2 + k)
+    gram_launch_ms = tm_sum["gram_ms"] / args.steps
+    achieved = flops_rep * B / (gram_launch_ms * 1e-3) / 1e12
+    okh = ok.cpu().numpy()
+    out = {
+        "metric": "Heckman two-step bootstrap replicates/sec (configs[1] panel + selection equation)",
+        "value": world * B * args.steps / elapsed, "unit": "replicates/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (SURVEY.md §8d wage panel + s = 1[0.3 + 0.5 z1 - 0.4 z2 + 0.2 x4 + u > 0])",
+        "config": {"workload": "heckman_selection(s, [z1, z2, x4]), GroupA reference coefficients",
+                   "rows": args.rows, "predictors": args.preds, "selection_predictors": len(zs),
+                   "replicates_per_gpu_per_step": B, "parallelism": f"replicates sharded x{world}"},
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": F64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / F64_MFMA_PEAK_TFLOPS, "traffic": None, "kernel": "ob_gram_kernel",
+                     "avg_launch_ms": gram_launch_ms, "flops_per_replicate": flops_rep},
+        "breakdown_ms_per_step": {k_: v / args.steps for k_, v in tm_sum.items()},
+        "dominant": {"phase": "probit Fisher scoring + IMR sums (ob_probit_kernel, ob_heck_sums_kernel)",
+                     "share_of_step": tm_sum["heckman_ms"] / (elapsed * 1e3),
+                     "bound": "f64 VALU: erfc, exp and a division per live (replicate, row) per iteration"},
+        "max_probit_iterations": iters,
+        "cpu_baseline": None,
+        "check": {"ok_replicates": int(okh.sum()), "explained_mean": float(rows[:, 0].mean().item())},
+    }
+    if world == 1 and args.cpu_seconds > 0:
+        out["cpu_baseline"] = cpu_baseline_heckman(frame, names, zs, args.cpu_seconds)
+    pr.close()
+    print(json.dumps(out), flush=True)
+
+
+def cpu_baseline_heckman(frame, names, zs, target_s):
+    """The oracle's heckman_single_pass (probit.rs / heckman.rs restated in numpy, one thread) on
+    whole resampled replicates of the same panel, as many as fit in target_s."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    ia = np.flatnonzero(frame["g"] == "M")
+    ib = np.flatnonzero(frame["g"] == "F")
+    groups = []
+    for rows in (ia, ib):
+        x = np.column_stack([np.ones(len(rows))] + [frame[nm][rows] for nm in names])
+        z = np.column_stack([np.ones(len(rows))] + [frame[nm][rows] for nm in zs])
+        groups.append(dict(x=x, y=frame["y"][rows], w=None, zsel=z, s=frame["s"][rows]))
+    n, t0 = 0, time.perf_counter()
+    while n == 0 or time.perf_counter() - t0 < target_s:
+        take = []
+        for gi, g in enumerate(groups):
+            idx = O.resample_indices(0x0B5EED, 100000 + n, gi, len(g["y"]))
+            take.append({k_: (None if v is None else v[idx]) for k_, v in g.items()})
+        O.heckman_single_pass(take[0], take[1], 0, False)
+        n += 1
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "replicates/s", "cores": 1, "kind": "port",
+            "sample": f"{n} replicates of the same panel through oracle.heckman_single_pass (numpy, 1 thread), "
+                      f"{dt:.1f} s"}
+
+
 def load_traffic(rows, preds, reps):
     """HBM bytes per ob_gram_kernel launch from the committed rocprofv3 PMC summary."""
     path = os.path.join(ROOT, "profiles", "pmc_gram.json")
@@ -199,8 +320,13 @@ def main():
                     help="configs[4]: Machado-Mata (defaults 500k rows x 15 predictors, 1000 simulations, "
                          "2 replicates per GPU per step); reports MM replicates/s")
     ap.add_argument("--sims", type=int, default=1000, help="--mm: quantile regressions per group per replicate")
+    ap.add_argument("--heckman", action="store_true",
+                    help="Heckman two-step bootstrap on configs[1]'s panel plus a selection equation "
+                         "(2000 replicates per GPU per step); reports Heckman replicates/s")
     args = ap.parse_args()
     taus = [float(t) for t in args.taus.split(",") if t.strip()]
+    if args.heckman and "--reps" not in set(a.split("=")[0] for a in sys.argv[1:]):
+        args.reps = 2000
     if args.mm:
         explicit = set(a.split("=")[0] for a in sys.argv[1:])
         if "--rows" not in explicit:
@@ -223,8 +349,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(local)
-    if args.mm:
-        bench_mm(args, world, rank, local, dist)
+    if args.mm or args.heckman:
+        (bench_mm if args.mm else bench_heckman)(args, world, rank, local, dist)
         if dist:
             dist.destroy_process_group()
         return

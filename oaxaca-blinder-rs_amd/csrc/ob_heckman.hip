@@ -90,10 +90,22 @@ __device__ __forceinline__ void block_sum(double (&acc)[N], double* red, const L
     for (int i = 0; i < N; ++i) acc[i] = red[l.lane * (N + 1) + i] + acc[i];
 }
 
+// The wave's 64-row sub-tile of `ncol` consecutive panel columns (from `src`) -> LDS [col][64]: one
+// coalesced load per column instead of a scalar load per row and column; the wave then reads its
+// rows at uniform LDS addresses. Wave-local (LDS operations of one wave complete in order).
+__device__ __forceinline__ void wave_stage(double* stg, const double* src, int64_t ld, uint32_t r0, uint32_t nr,
+                                           int ncol, int lane) {
+  __builtin_amdgcn_wave_barrier();
+  for (int c = 0; c < ncol; ++c) stg[c * 64 + lane] = (uint32_t)lane < nr ? src[(size_t)c * ld + r0 + lane] : 0.0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 template <int KS>
 __global__ __launch_bounds__(kHB) void ob_probit_kernel(const ob_heck_seg a) {
   constexpr int NH = KS * (KS + 1) / 2, NP = NH + KS;
   __shared__ double red[64 * (NP + 1)];
+  __shared__ double stage[4 * KS * 64];  // per wave: s, z_1..z_{KS-1} of its sub-tile
   const Lanes l = lanes(a);
   const size_t st = (size_t)l.g * a.rep_pad + l.rep;
   const bool act = l.rep < a.n_reps && !(a.hflags[st] & kDone);
@@ -107,12 +119,13 @@ __global__ __launch_bounds__(kHB) void ob_probit_kernel(const ob_heck_seg a) {
   const double* X = a.cols[l.g];
   const int64_t ld = a.ld[l.g];
   const uint32_t n = a.n[l.g];
-  const double* S = X + (size_t)(a.p + 2) * ld;
-  const double* Z = X + (size_t)(a.p + 3) * ld;
+  const double* SZ = X + (size_t)(a.p + 2) * ld;  // s, then z_1..z_{KS-1}: consecutive columns
+  double* stg = stage + l.wave * (KS * 64);
   for (uint32_t tile = l.t0; tile < l.t1; ++tile) {
     const uint32_t r0 = tile * OB_TILE_ROWS + l.wave * 64;
     if (r0 >= n) break;
     const uint32_t nr = min(64u, n - r0);
+    wave_stage(stg, SZ, ld, r0, nr, KS, l.lane);
     const uint32_t* cw = count_row(a, l, tile);
     uint32_t word = 0;
     for (uint32_t ri = 0; ri < nr; ++ri) {
@@ -120,17 +133,16 @@ __global__ __launch_bounds__(kHB) void ob_probit_kernel(const ob_heck_seg a) {
       const uint32_t cu = (word >> ((ri & 3) * 8)) & 255u;
       if (!act || cu == 0) continue;
       const double c = (double)cu;
-      const size_t row = r0 + ri;
       double z[KS];
       z[0] = 1.0;
 #pragma unroll
-      for (int j = 1; j < KS; ++j) z[j] = Z[(size_t)(j - 1) * ld + row];
+      for (int j = 1; j < KS; ++j) z[j] = stg[j * 64 + ri];
       double zg = 0.0;
 #pragma unroll
       for (int j = 0; j < KS; ++j) zg += z[j] * gam[j];
       const double phi = npdf(zg);
       const double bp = clamp_phi(ncdf(zg));
-      const double lam = S[row] > 0.5 ? phi / bp : -phi / (1.0 - bp);  // probit.rs:66-70
+      const double lam = stg[ri] > 0.5 ? phi / bp : -phi / (1.0 - bp);  // probit.rs:66-70
       const double sw = sqrt(phi * phi / (bp * (1.0 - bp)));           // probit.rs:75-76
       const double cwt = c * (sw * sw), cl = c * lam;
       int e = 0;
@@ -304,9 +316,13 @@ __global__ __launch_bounds__(64) void ob_probit_step_kernel(const ob_heck_seg a)
     atomicAdd(a.active, 1u);
 }
 
+// Staged columns per row of the sums kernel: x_1..x_p, y, [s == 1], s, z_1..z_{ks-1}, (w).
+__host__ __device__ inline int heck_sums_cols(int p, int ks, int weighted) { return p + 2 + ks + (weighted ? 1 : 0); }
+
 template <int NB>
 __global__ __launch_bounds__(kHB) void ob_heck_sums_kernel(const ob_heck_seg a) {
-  __shared__ double red[64 * (NB + 1)];
+  extern __shared__ __attribute__((aligned(16))) double hsm[];
+  double* red = hsm;  // [64][NB + 1], then the waves' staged sub-tiles
   const Lanes l = lanes(a);
   const bool act = l.rep < a.n_reps;
   if (!__syncthreads_or(act)) return;
@@ -321,14 +337,13 @@ __global__ __launch_bounds__(kHB) void ob_heck_sums_kernel(const ob_heck_seg a) 
   const double* X = a.cols[l.g];
   const int64_t ld = a.ld[l.g];
   const uint32_t n = a.n[l.g];
-  const double* Y = X + (size_t)a.p * ld;
-  const double* IND = X + (size_t)(a.p + 1) * ld;
-  const double* Z = X + (size_t)(a.p + 3) * ld;
-  const double* W = a.weighted ? X + (size_t)(a.p + 2 + ks) * ld : nullptr;
+  const int ncol = heck_sums_cols(a.p, ks, a.weighted), cy = a.p, cind = a.p + 1, cz = a.p + 2, cw8 = a.p + 2 + ks;
+  double* stg = hsm + 64 * (NB + 1) + l.wave * (ncol * 64);
   for (uint32_t tile = l.t0; tile < l.t1; ++tile) {
     const uint32_t r0 = tile * OB_TILE_ROWS + l.wave * 64;
     if (r0 >= n) break;
     const uint32_t nr = min(64u, n - r0);
+    wave_stage(stg, X, ld, r0, nr, ncol, l.lane);
     const uint32_t* cw = count_row(a, l, tile);
     uint32_t word = 0;
     for (uint32_t ri = 0; ri < nr; ++ri) {
@@ -336,21 +351,20 @@ __global__ __launch_bounds__(kHB) void ob_heck_sums_kernel(const ob_heck_seg a) 
       const uint32_t cu = (word >> ((ri & 3) * 8)) & 255u;
       if (!act || cu == 0) continue;
       const double c = (double)cu;
-      const size_t row = r0 + ri;
       double z[ob::kHeckMaxKs];
       z[0] = 1.0;
 #pragma unroll
-      for (int j = 1; j < ob::kHeckMaxKs; ++j) z[j] = j < ks ? Z[(size_t)(j - 1) * ld + row] : 0.0;
+      for (int j = 1; j < ob::kHeckMaxKs; ++j) z[j] = j < ks ? stg[(cz + j) * 64 + ri] : 0.0;
       double zg = 0.0;
 #pragma unroll
       for (int j = 0; j < ob::kHeckMaxKs; ++j)
         if (j < ks) zg += z[j] * gam[j];
 #pragma unroll
       for (int j = 0; j < ob::kHeckMaxKs; ++j) acc[5 + j] += c * z[j];  // selection means (all rows)
-      const double y = Y[row], w = W ? W[row] : 1.0;
+      const double y = stg[cy * 64 + ri], w = a.weighted ? stg[cw8 * 64 + ri] : 1.0;
       acc[3] += c * w * y;  // total gap (builder.rs:676-684, all rows)
       acc[4] += c * w;
-      if (IND[row] == 1.0) {  // heckman.rs:56-69: lambda = phi / Phi, 0 when Phi < 1e-10
+      if (stg[cind * 64 + ri] == 1.0) {  // heckman.rs:56-69: lambda = phi / Phi, 0 when Phi < 1e-10
         const double bp = ncdf(zg);
         const double lam = bp < 1e-10 ? 0.0 : npdf(zg) / bp;
         const double cl = c * lam;
@@ -360,7 +374,7 @@ __global__ __launch_bounds__(kHB) void ob_heck_sums_kernel(const ob_heck_seg a) 
         acc[13] += cl;
 #pragma unroll
         for (int j = 1; j < NB - 13; ++j)
-          if (j < K) acc[13 + j] += cl * X[(size_t)(j - 1) * ld + row];
+          if (j < K) acc[13 + j] += cl * stg[(j - 1) * 64 + ri];
       }
     }
   }
@@ -553,10 +567,19 @@ int heckman_segment(const ob_heck_seg& a, hipStream_t s, int* iters) {
   }
   if (iters) *iters = it;
   const dim3 grid(a.n_chunks, a.rep_pad / 64);
-  if (heck_sums_len(a.p + 1) <= 32)
-    hipLaunchKernelGGL(ob_heck_sums_kernel<32>, grid, dim3(kHB), 0, s, a);
+  const int nhs = heck_sums_len(a.p + 1);
+  const int nb = nhs <= 32 ? 32 : (nhs <= 40 ? 40 : 64);
+  const size_t lds_sums =
+      sizeof(double) * (64 * (size_t)(nb + 1) + 4 * 64 * (size_t)heck_sums_cols(a.p, a.ks, a.weighted));
+  const void* fn = nb == 32 ? (const void*)ob_heck_sums_kernel<32>
+                            : (nb == 40 ? (const void*)ob_heck_sums_kernel<40> : (const void*)ob_heck_sums_kernel<64>);
+  HK_OK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sums));
+  if (nb == 32)
+    hipLaunchKernelGGL(ob_heck_sums_kernel<32>, grid, dim3(kHB), lds_sums, s, a);
+  else if (nb == 40)
+    hipLaunchKernelGGL(ob_heck_sums_kernel<40>, grid, dim3(kHB), lds_sums, s, a);
   else
-    hipLaunchKernelGGL(ob_heck_sums_kernel<64>, grid, dim3(kHB), 0, s, a);
+    hipLaunchKernelGGL(ob_heck_sums_kernel<64>, grid, dim3(kHB), lds_sums, s, a);
   HK_OK(hipGetLastError());
   const size_t lds = heck_solve_lds(a);
   HK_OK(hipFuncSetAttribute((const void*)ob_heck_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
