@@ -5,7 +5,7 @@ Workload = BASELINE.json configs[1]: a 1,000,000-row two-group panel (500k/500k)
 predictors, two-fold WLS decomposition (builder default reference coefficients GroupA), 10,000
 bootstrap replicates per GPU per step. One step = one full bootstrap run with the panel already
 resident in HBM: OBRS-1 resampling + Gram + solves + OB terms for every replicate (HIP), the
-RCCL all-gather of the per-replicate rows over xGMI (N > 1), and the SE/p/CI aggregation of
+RCCL all-gather of the per-replicate component columns over xGMI (N > 1), and the SE/p/CI aggregation of
 every reported component on rank 0 (builder.rs:841-930). Replicates are sharded across ranks
 (weak scaling: each rank runs its own 10,000 replicate ids per step).
 
@@ -366,23 +366,26 @@ def main():
     dev = torch.device("cuda", local)
     rows = torch.empty((ny * B, rl), dtype=torch.float64, device=dev)
     ok = torch.empty(ny * B, dtype=torch.uint8, device=dev)
-    all_rows = torch.empty((world * ny * B, rl), dtype=torch.float64, device=dev) if world > 1 else rows
-    all_ok = torch.empty(world * ny * B, dtype=torch.uint8, device=dev) if world > 1 else ok
     kd = panel.k + panel.n_base
-    stat_cols = np.arange(6 + 2 * kd, dtype=np.int32)  # every reported component (+ total_gap)
+    ns = 6 + 2 * kd  # every reported component (+ total_gap): the only columns the aggregation reads
+    stat_cols = np.arange(ns, dtype=np.int32)
+    part = torch.empty((ny * B, ns), dtype=torch.float64, device=dev)
+    all_part = torch.empty((world * ny * B, ns), dtype=torch.float64, device=dev) if world > 1 else part
+    all_ok = torch.empty(world * ny * B, dtype=torch.uint8, device=dev) if world > 1 else ok
     seed = 0x0B5EED
 
     def step(i):
         stream = torch.cuda.current_stream(dev).cuda_stream
         first = (i * world + rank) * B
         panel.boot_device(seed, first, B, rows.data_ptr(), ok.data_ptr(), args.ref, stream=stream)
+        part.copy_(rows[:, :ns])  # the component columns only: 48 of 153 f64 per replicate at K = 21
         if world > 1:
-            dist.all_gather_into_tensor(all_rows, rows)
+            dist.all_gather_into_tensor(all_part, part)
             dist.all_gather_into_tensor(all_ok, ok)
         if rank == 0:  # per outcome: that outcome's block of every rank, in replicate order
-            h_rows = all_rows.cpu().numpy().reshape(world, ny, B, rl)
+            h_rows = all_part.cpu().numpy().reshape(world, ny, B, ns)
             h_ok = all_ok.cpu().numpy().reshape(world, ny, B)
-            stats = [ob.aggregate(np.ascontiguousarray(h_rows[:, t].reshape(-1, rl)),
+            stats = [ob.aggregate(np.ascontiguousarray(h_rows[:, t].reshape(-1, ns)),
                                   np.ascontiguousarray(h_ok[:, t].reshape(-1)), stat_cols) for t in range(ny)][0]
         else:
             torch.cuda.current_stream(dev).synchronize()
