@@ -252,6 +252,15 @@ __device__ __forceinline__ void group_dots(const double* X, int G, const Blk& b,
   }
 }
 
+// 1/v within ~1 ulp without the IEEE division sequence (div_scale / div_fmas / div_fixup):
+// v_rcp_f64 and two Newton steps. The operands are normal numbers (interior iterates, nonzero
+// direction components), so the scaling that sequence guards against is never needed.
+__device__ __forceinline__ double mm_rcp(double v) {
+  double r = __builtin_amdgcn_rcp(v);
+  r = fma(fma(-v, r, 1.0), r, r);
+  return fma(fma(-v, r, 1.0), r, r);
+}
+
 // Per-row affine direction from the current state (shared by mm_affine, mm_final and the step
 // replay of mm_assemble).
 struct Affine {
@@ -267,9 +276,9 @@ __device__ __forceinline__ Affine affine_row(double xv, double zv, double wv, do
   f.wv = wv;
   f.sv = c - f.xv;
   f.r = y - xb;
-  f.ix = 1.0 / f.xv;
-  f.is = 1.0 / f.sv;
-  f.q = 1.0 / (f.zv * f.ix + f.wv * f.is);
+  f.ix = mm_rcp(f.xv);
+  f.is = mm_rcp(f.sv);
+  f.q = mm_rcp(f.zv * f.ix + f.wv * f.is);
   f.dxa = f.q * (f.r - xd);
   f.dza = -f.zv - f.zv * f.dxa * f.ix;
   f.dwa = -f.wv + f.wv * f.dxa * f.is;
@@ -401,7 +410,7 @@ __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a
               a.z[si] = zv;
               a.w[si] = wv;
               const double sv = c - xv;
-              q = xv * sv / (zv * sv + wv * xv);  // 1 / (z/x + w/s)
+              q = xv * sv * mm_rcp(zv * sv + wv * xv);  // 1 / (z/x + w/s)
               qr = q * r;                          // rho_aff = r_d + w - z = y - X beta
               gap += xv * zv + sv * wv;
               obj += y * xv;
@@ -510,9 +519,9 @@ __global__ __launch_bounds__(256, 3) void mm_affine_kernel(const MmArgs a) {
     double q0 = 0.0, q1 = 0.0;
     if (valid) {
       const Affine f = affine_row(xv, zv, wv, c, xr[kXy], dv[0], dv[1]);
-      if (f.dxa != 0.0) acc[0] = fmin(acc[0], (f.dxa < 0.0 ? -f.xv : f.sv) / f.dxa);
-      if (f.dza < 0.0) acc[1] = fmin(acc[1], -f.zv / f.dza);
-      if (f.dwa < 0.0) acc[1] = fmin(acc[1], -f.wv / f.dwa);
+      if (f.dxa != 0.0) acc[0] = fmin(acc[0], (f.dxa < 0.0 ? -f.xv : f.sv) * mm_rcp(f.dxa));
+      if (f.dza < 0.0) acc[1] = fmin(acc[1], -f.zv * mm_rcp(f.dza));
+      if (f.dwa < 0.0) acc[1] = fmin(acc[1], -f.wv * mm_rcp(f.dwa));
       acc[2] += f.xv * f.dza + f.sv * f.dwa;
       acc[3] += f.zv * f.dxa - f.wv * f.dxa;
       acc[4] += f.dxa * f.dza - f.dxa * f.dwa;
@@ -561,9 +570,9 @@ __global__ __launch_bounds__(256, 2) void mm_final_kernel(const MmArgs a) {
     const Affine f = affine_row(xv, zv, wv, c, xr[kXy], dv[0], dv[1]);
     const Corrector d = corrector_row(f, dv[2], sigmu);
     const double dx = d.dx, dz = d.dz, dw = d.dw;
-    if (dx != 0.0) acc[0] = fmin(acc[0], (dx < 0.0 ? -f.xv : f.sv) / dx);
-    if (dz < 0.0) acc[1] = fmin(acc[1], -f.zv / dz);
-    if (dw < 0.0) acc[1] = fmin(acc[1], -f.wv / dw);
+    if (dx != 0.0) acc[0] = fmin(acc[0], (dx < 0.0 ? -f.xv : f.sv) * mm_rcp(dx));
+    if (dz < 0.0) acc[1] = fmin(acc[1], -f.zv * mm_rcp(dz));
+    if (dw < 0.0) acc[1] = fmin(acc[1], -f.wv * mm_rcp(dw));
   });
   acc[0] = rows_min(acc[0]);
   acc[1] = rows_min(acc[1]);
