@@ -42,8 +42,17 @@ constexpr uint32_t kDone = 1u, kFailed = 2u;
   } while (0)
 
 // statrs Normal(0, 1): pdf = exp(-z^2 / 2) / sqrt(2 pi), cdf = erfc(-z / sqrt 2) / 2.
-__device__ __forceinline__ double npdf(double z) { return exp(-0.5 * z * z) / 2.5066282746310002; }
-__device__ __forceinline__ double ncdf(double z) { return 0.5 * erfc(-z / 1.4142135623730951); }
+// (The constant divisions are multiplications by the reciprocals: a last-bit difference.)
+__device__ __forceinline__ double npdf(double z) { return exp(-0.5 * z * z) * 0.3989422804014327; }
+__device__ __forceinline__ double ncdf(double z) { return 0.5 * erfc(-z * 0.7071067811865476); }
+
+// 1/v within ~1 ulp: v_rcp_f64 and two Newton steps instead of the IEEE division sequence (the
+// operands are normal numbers: clamped probabilities).
+__device__ __forceinline__ double hk_rcp(double v) {
+  double r = __builtin_amdgcn_rcp(v);
+  r = fma(fma(-v, r, 1.0), r, r);
+  return fma(fma(-v, r, 1.0), r, r);
+}
 
 // f64::clamp: NaN stays NaN.
 __device__ __forceinline__ double clamp_phi(double v) {
@@ -142,9 +151,9 @@ __global__ __launch_bounds__(kHB) void ob_probit_kernel(const ob_heck_seg a) {
       for (int j = 0; j < KS; ++j) zg += z[j] * gam[j];
       const double phi = npdf(zg);
       const double bp = clamp_phi(ncdf(zg));
-      const double lam = stg[ri] > 0.5 ? phi / bp : -phi / (1.0 - bp);  // probit.rs:66-70
-      const double sw = sqrt(phi * phi / (bp * (1.0 - bp)));           // probit.rs:75-76
-      const double cwt = c * (sw * sw), cl = c * lam;
+      const double ib = hk_rcp(bp), iq = hk_rcp(1.0 - bp);
+      const double lam = stg[ri] > 0.5 ? phi * ib : -phi * iq;  // probit.rs:66-70
+      const double cwt = c * (phi * phi * ib * iq), cl = c * lam;  // sqrt_w^2 of probit.rs:75-76
       int e = 0;
 #pragma unroll
       for (int j = 0; j < KS; ++j) {
@@ -366,7 +375,7 @@ __global__ __launch_bounds__(kHB) void ob_heck_sums_kernel(const ob_heck_seg a) 
       acc[4] += c * w;
       if (stg[cind * 64 + ri] == 1.0) {  // heckman.rs:56-69: lambda = phi / Phi, 0 when Phi < 1e-10
         const double bp = ncdf(zg);
-        const double lam = bp < 1e-10 ? 0.0 : npdf(zg) / bp;
+        const double lam = bp < 1e-10 ? 0.0 : npdf(zg) * hk_rcp(bp);
         const double cl = c * lam;
         acc[0] += cl * y;
         acc[1] += cl * lam;
