@@ -113,7 +113,7 @@ constexpr int kXs = 18;     // LDS stride of a staged row: [1, x_1..x_p, 0.., y 
 constexpr int kXy = 16, kXzero = 17;
 constexpr int kSub = 64;    // list rows per staged sub-tile (16 wave steps of 4 rows)
 constexpr int kRing = 4;    // wave steps of state in flight (affine / final)
-constexpr int kRingA = 2;   // the same for the assemble pass (6 state values per step)
+constexpr int kRingA = 4;   // the same for the assemble pass (its fragments sit in LDS to make room)
 constexpr int kStoreAt = 4; // step after which the next sub-tile's staged values are written
 constexpr int kStage = (kSub * kXs + 255) / 256;  // staging values per thread
 typedef double mm_d4 __attribute__((ext_vector_type(4)));
@@ -252,6 +252,25 @@ __device__ __forceinline__ void group_dots(const double* X, int G, const Blk& b,
   }
 }
 
+// group_dots with the fragments read from LDS ([vector][fit of the block][K + 1], odd stride).
+template <int K, int NV>
+__device__ __forceinline__ void group_dots_lds(const double* X, int G, const Blk& b, const double* fbl,
+                                               mm_d4 (&d)[NV]) {
+#pragma unroll
+  for (int v = 0; v < NV; ++v) d[v] = (mm_d4){0.0, 0.0, 0.0, 0.0};
+  const int fit = b.wave * 16 + b.fl;
+#pragma unroll
+  for (int kb = 0; kb < (K + 3) / 4; ++kb) {
+    const double av = X[(16 * G + b.fl) * kXs + 4 * kb + b.rl];
+    const int k = 4 * kb + b.rl;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const double bv = k < K ? fbl[(v * 64 + fit) * (K + 1) + k] : 0.0;
+      d[v] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, d[v], 0, 0, 0);
+    }
+  }
+}
+
 // 1/v within ~1 ulp without the IEEE division sequence (div_scale / div_fmas / div_fixup):
 // v_rcp_f64 and two Newton steps. The operands are normal numbers (interior iterates, nonzero
 // direction components), so the scaling that sequence guards against is never needed.
@@ -316,11 +335,14 @@ __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a
   const Blk b = blk_ctx(a, lst, mode == 0);
   if (!b.any) return;  // partials of dead fits are never reduced
   constexpr int NDOT = STEP ? 3 : 1;  // x_i . (bprev, dba, db) or x_i . beta
-  double fb[NDOT][(K + 3) / 4];
-  bfrag<K>(STEP ? a.bprev : a.beta, b, b.live && mode, fb[0]);
-  if (STEP) {
-    bfrag<K>(a.dba, b, b.live, fb[NDOT > 1 ? 1 : 0]);
-    bfrag<K>(a.db, b, b.live, fb[NDOT > 2 ? 2 : 0]);
+  // the per-fit vectors live in LDS (registers go to a deeper state prefetch): [vector][fit][K + 1]
+  __shared__ double fbl[NDOT * 64 * (K + 1)];
+  {
+    const double* src[3] = {STEP ? a.bprev : a.beta, a.dba, a.db};
+    const int fit = b.wave * 16 + b.fl;
+#pragma unroll
+    for (int v = 0; v < NDOT; ++v)
+      for (int k = b.rl; k < K; k += 4) fbl[(v * 64 + fit) * (K + 1) + k] = (b.live && mode) ? src[v][b.F * K + k] : 0.0;
   }
   mm_d4 dots[NDOT];
   double tau = 0.0, ap = 0.0, ad = 0.0, delta = 0.0, sigmu = 0.0;
@@ -373,7 +395,7 @@ __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a
       const double* X = xs[t & 1];
       xs_load<K>(a, b, lst, t + 1, stg);
       auto step = [&](int j) {
-          if ((j & 3) == 0 && mode) group_dots<K, NDOT>(X, j >> 2, b, fb, dots);
+          if ((j & 3) == 0 && mode) group_dots_lds<K, NDOT>(X, j >> 2, b, fbl, dots);
           const int k = j % kRingA;
           const double cx = rx[k], cz = rz[k], cw = rw[k];
           const uint32_t e = t * kSub + 4 * j + b.rl;
