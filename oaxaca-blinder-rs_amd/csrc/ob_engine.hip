@@ -38,6 +38,7 @@ constexpr int kBlock = 256;
 constexpr int kCntStride = OB_TILE_ROWS / 4 + 1;  // u32 words per replicate row of the u8 count image (+1 pad)
 constexpr uint64_t kSegReps = 16384;
 constexpr uint64_t kCountBudget = 24ull << 30;  // bytes of level-2 count images per segment
+constexpr int64_t kMaxGroupRows = (160 * 1024 / 4) * (int64_t)OB_TILE_ROWS;  // 40960 tiles: the 160 KB LDS histogram
 constexpr size_t kSegEvents = 6;
 constexpr int kColStride = 96;  // doubles per staged column: 64 rows rotated by (c mod 32), wrap duplicated
 
@@ -1331,7 +1332,8 @@ int ob_panel_create(ob_ctx* ctx, const ob_panel_desc* d, ob_panel** out) {
         return ob::fail(OB_E_INVALID, "missing selection column pointer");
   }
   for (int g = 0; g < 2; ++g) {
-    if (gd[g]->n < 0 || gd[g]->n > 16000000) return ob::fail(OB_E_UNSUPPORTED, "group rows must be in [0, 16e6]");
+    if (gd[g]->n < 0 || gd[g]->n > kMaxGroupRows)  // level 1 keeps one u32 per 256-row tile in LDS
+      return ob::fail(OB_E_UNSUPPORTED, "group rows must be in [0, %lld]", (long long)kMaxGroupRows);
     if (gd[g]->n > 0 && ((d->p > 0 && !gd[g]->x) || !gd[g]->y || (d->weighted && !gd[g]->w)))
       return ob::fail(OB_E_INVALID, "missing column pointer");
     if (gd[g]->ldx < gd[g]->n) return ob::fail(OB_E_INVALID, "ldx < n");
@@ -1507,7 +1509,7 @@ int ob_boot_run_device(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t 
   if (!valid_ref(ref_mode)) return ob::fail(OB_E_INVALID, "unknown reference coefficients %d", ref_mode);
   if (p->n[0] == 0 || p->n[1] == 0)
     return ob::fail(OB_E_GROUP, "%sOne group has no data", ob::error_prefix(OB_E_GROUP));
-  if (p->ntiles[0] > 40000 || p->ntiles[1] > 40000)
+  if (p->ntiles[0] > kMaxGroupRows / OB_TILE_ROWS || p->ntiles[1] > kMaxGroupRows / OB_TILE_ROWS)
     return ob::fail(OB_E_UNSUPPORTED, "group too large for the LDS level-1 histogram");
   return ob::engine_boot(p, seed, first_rep, n_reps, ref_mode, d_rows, d_ok,
                          reinterpret_cast<hipStream_t>(hip_stream));

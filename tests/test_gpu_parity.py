@@ -423,3 +423,25 @@ def test_full_size_panel_properties(ob, O):
     se_gap = rows[:, 5].std(ddof=1)
     sd = np.sqrt((d["ya"].var() + d["yb"].var()) / 2)
     assert 0.5 < se_gap / (sd * np.sqrt(2 / 500_000)) < 2.0
+
+
+def test_largest_group_and_the_limit(ob, O, N):
+    """n_g = 10,485,760 rows (40,960 tiles: level 1's LDS histogram at its 160 KB) runs, and its
+    bootstrap rows match the oracle's reference algorithm; one more row is refused up front."""
+    n = 40960 * 256
+    rng = np.random.default_rng(3)
+    x = rng.normal(size=(n, 1))
+    y = 1.0 + 0.5 * x[:, 0] + rng.normal(size=n)
+    xb, yb = x[:4096] + 0.1, y[:4096] - 0.2
+    panel = ob.Panel(x, y, xb, yb)
+    try:
+        rows, ok = panel.boot(SEED, 0, 2, 0)
+    finally:
+        panel.close()
+    cfg = O.PassConfig(2, 1, 0, False)
+    orows, ook = O.boot_ref(cfg, O.with_intercept(x), y, None, O.with_intercept(xb), yb, None, SEED, 0, 2,
+                            threads=8, full=False)
+    assert ok.all() and ook.all() and close(rows, orows, abs(orows[0, 5]))[0]
+    with pytest.raises(N.OaxacaError) as e:
+        ob.Panel(np.zeros((n + 1, 1)), np.zeros(n + 1), xb, yb)
+    assert e.value.code == N.OB_E_UNSUPPORTED
