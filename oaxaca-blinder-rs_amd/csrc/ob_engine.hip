@@ -58,7 +58,7 @@ struct GramArgs {
   int k1, c_first, e, ncb, n_cg;
   uint32_t nb_rep;
   const uint32_t* chunks;  // [chunk][3] = (group, first tile, end tile)
-  const uint32_t* m1;      // [tile (group 0 then group 1)][rep_pad]
+  const uint32_t* m1;      // [replicate][tile (group 0 then group 1)]
   uint32_t tiles0;
   uint32_t rep_pad;
   uint32_t n_reps;
@@ -73,40 +73,153 @@ struct GramArgs {
 };
 
 // ---------------------------------------------------------------------------------------------
-// Level 1: tile counts m_j for one (replicate, group) from n_g draws (OBRS-1, ob_spec.h).
+// Level 1: tile counts m_j for one (replicate, group) by fair-bit splitting (OBRS-1, ob_spec.h;
+// oracle orc_level1_counts). Level l of the dyadic tile tree lives in LDS buffer (D - l) & 1.
+// Levels l < 8 have at most 2^l nodes and give each 256 >> l threads (popcounts summed by LDS
+// atomics); deeper levels give a thread whole nodes. T <= 256 tiles ("small") keeps the tile
+// level and the running counts in LDS; larger T sends the last split straight to m1, the
+// thread that owns node k of level D-1 owning tiles 2k, 2k+1 in every round, so later rounds
+// add to m1 without atomics. The <= 256 direct draws finish with atomics (LDS or global).
 // ---------------------------------------------------------------------------------------------
+static_assert(kBlock == 256, "level 1 maps 256 threads onto the top tree levels");
+__host__ __device__ inline uint32_t l1_depth(uint32_t ntiles) { return ntiles > 1 ? 32u - __builtin_clz(ntiles - 1) : 0u; }
+__host__ __device__ inline bool l1_small(uint32_t ntiles) { return ntiles <= 256u; }
+__host__ __device__ inline uint32_t l1_buf0_words(uint32_t ntiles) { return l1_small(ntiles) ? 256u : (ntiles + 3) / 4; }
+__host__ __device__ inline uint32_t l1_lds_words(uint32_t ntiles) {
+  return l1_small(ntiles) ? 256u + 128u + 256u : (ntiles + 3) / 4 + (ntiles + 1) / 2;
+}
+
 __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t n1, uint32_t tiles0,
-                                                           uint32_t first_rep, uint32_t rep_pad,
+                                                           uint32_t first_rep, uint32_t stride,
                                                            uint32_t key0, uint32_t key1, uint32_t* m1) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t hist[];
-  const uint32_t g = blockIdx.y;
-  const uint32_t rl = blockIdx.x;
-  const uint32_t rep = first_rep + rl;
+  extern __shared__ __attribute__((aligned(16))) uint32_t l1s[];
+  __shared__ uint32_t s_rej, s_tail, s_acc;
+  const uint32_t g = blockIdx.y, rl = blockIdx.x, rep = first_rep + rl, tid = threadIdx.x;
   const uint32_t n = g ? n1 : n0;
-  const uint32_t ntiles = (n + OB_TILE_ROWS - 1) >> OB_TILE_SHIFT;
-  for (uint32_t i = threadIdx.x; i < ntiles; i += kBlock) hist[i] = 0;
-  __syncthreads();
-  const uint32_t ncalls = (n + 3) >> 2, thresh = (0u - n) % n;
-  for (uint32_t p = threadIdx.x; p < ncalls; p += kBlock) {
-    const ob_u32x4 u = ob_philox(p, rep, g, OB_TAG_L1, key0, key1);
-    const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-    for (uint32_t h = 0; h < 4; ++h) {
-      const uint32_t d = 4 * p + h;
-      if (d < n) {
-        uint64_t m = (uint64_t)wd[h] * n;
-        for (uint32_t j = 0; (uint32_t)m < thresh; ++j) {  // Lemire rejection, p < n / 2^32
-          const ob_u32x4 r = ob_philox(d, rep, g, OB_TAG_RETRY + (j >> 2), key0, key1);
-          const uint32_t rw[4] = {r.x, r.y, r.z, r.w};
-          m = (uint64_t)rw[j & 3] * n;
+  if (n == 0) return;
+  const uint32_t T = (n + OB_TILE_ROWS - 1) >> OB_TILE_SHIFT, D = l1_depth(T);
+  const uint32_t tail = n - (T - 1) * OB_TILE_ROWS;
+  const bool small = l1_small(T), partial = tail < OB_TILE_ROWS;
+  uint32_t* buf[2] = {l1s, l1s + l1_buf0_words(T)};
+  uint32_t* mt = l1s + 256u + 128u;  // small: running tile counts
+  uint32_t* mcol = m1 + (size_t)rl * stride + (g ? tiles0 : 0u);  // [rep][tile]: one row per block
+  const uint32_t tail_owner = ((T - 1) >> 1) & (kBlock - 1);
+  if (small && tid < T) mt[tid] = 0;
+  uint32_t todo = n;
+  for (uint32_t round = 0;; ++round) {
+    if (tid == 0) {
+      buf[D & 1][0] = todo;
+      s_rej = 0;
+      s_tail = 0;
+      s_acc = 0;
+    }
+    __syncthreads();
+    uint32_t rej = 0;
+    // large T, round r: tile t of the last split gets c (tail tile: parked for acceptance)
+    auto emit = [&](uint32_t t, uint32_t c) {
+      if (partial && t == T - 1) s_tail = c;
+      else if (round == 0) mcol[t] = c;
+      else if (c) mcol[t] += c;
+    };
+    for (uint32_t l = 0; l < D; ++l) {
+      const uint32_t* cur = buf[(D - l) & 1];
+      uint32_t* nxt = buf[(D - l - 1) & 1];
+      const uint32_t span = 1u << (D - l - 1);  // tiles per child
+      const uint32_t nodes = (T + 2 * span - 1) / (2 * span), nnext = (T + span - 1) / span;
+      const uint32_t tag = OB_TAG_L1T + (round << 5) + l;
+      if (l < 8) {  // nodes <= 2^l: 256 >> l threads per node; never the large last level
+        const uint32_t sh = 8 - l, k = tid >> sh, j = tid & ((1u << sh) - 1);
+        if (j == 0 && k < nodes) nxt[2 * k] = 0;
+        __syncthreads();
+        if (k < nodes) {
+          const uint32_t c = cur[k];
+          uint32_t left = 0;
+          for (uint32_t q = j; 128 * q < c; q += 1u << sh) left += ob_l1_split_bits(q, c, rep, (k << 1) | g, tag, key0, key1);
+          if (left) atomicAdd(&nxt[2 * k], left);
         }
-        atomicAdd(&hist[(uint32_t)(m >> 32) >> OB_TILE_SHIFT], 1u);
+        __syncthreads();
+        if (j == 0 && k < nodes) {
+          const uint32_t c = cur[k], right = c - nxt[2 * k];
+          if (2 * k + 1 < nnext) nxt[2 * k + 1] = right;
+          else rej += right;
+        }
+        __syncthreads();
+      } else {
+        const bool to_m1 = l + 1 == D && !small;
+        for (uint32_t k = tid; k < nodes; k += kBlock) {
+          const uint32_t c = cur[k];
+          uint32_t left = 0;
+          for (uint32_t q = 0; 128 * q < c; ++q) left += ob_l1_split_bits(q, c, rep, (k << 1) | g, tag, key0, key1);
+          const uint32_t right = c - left;
+          if (to_m1) {
+            emit(2 * k, left);
+            if (2 * k + 1 < T) emit(2 * k + 1, right);
+            else rej += right;
+          } else {
+            nxt[2 * k] = left;
+            if (2 * k + 1 < nnext) nxt[2 * k + 1] = right;
+            else rej += right;
+          }
+        }
+        __syncthreads();
       }
     }
+    if (small) {  // tile level D is buf[0]
+      const uint32_t* tl = buf[0];
+      if (tid < T) {
+        if (partial && tid == T - 1) s_tail = tl[tid];
+        else mt[tid] += tl[tid];
+      }
+      __syncthreads();
+    }
+    if (partial && tid < 64) {  // the tail tile accepts draw i iff its byte < tail
+      const uint32_t c = s_tail;
+      uint32_t acc = 0;
+      for (uint32_t q = tid; 16 * q < c; q += 64) {
+        const ob_u32x4 u = ob_philox(q, rep, g, OB_TAG_L1S + round, key0, key1);
+        const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
+        const uint32_t m = min(16u, c - 16 * q);
+#pragma unroll
+        for (uint32_t i = 0; i < 16; ++i) acc += (i < m && ((wd[i >> 2] >> (8 * (i & 3))) & 0xFFu) < tail) ? 1u : 0u;
+      }
+      if (acc) atomicAdd(&s_acc, acc);
+    }
+    __syncthreads();
+    if (partial) {
+      const uint32_t a = s_acc;
+      if (tid == 0) rej += s_tail - a;
+      if (small) {
+        if (tid == 0) mt[T - 1] += a;
+      } else if (tid == tail_owner) {
+        if (round == 0) mcol[T - 1] = a;
+        else if (a) mcol[T - 1] += a;
+      }
+    }
+    if (rej) atomicAdd(&s_rej, rej);
+    __syncthreads();
+    todo = s_rej;
+    __syncthreads();
+    if (todo <= OB_L1_DIRECT) break;
   }
+  if (!small) __threadfence();
   __syncthreads();
-  const uint32_t toff = g ? tiles0 : 0;
-  for (uint32_t i = threadIdx.x; i < ntiles; i += kBlock) m1[(size_t)(toff + i) * rep_pad + rl] = hist[i];
+  if (tid < todo) {  // direct draws: Lemire over [0, n)
+    const uint32_t thresh = (0u - n) % n;
+    uint64_t x;
+    for (uint32_t j = 0;; ++j) {
+      const ob_u32x4 u = ob_philox(tid, rep, g, OB_TAG_L1D + (j >> 2), key0, key1);
+      const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
+      x = (uint64_t)wd[j & 3] * n;
+      if ((uint32_t)x >= thresh) break;
+    }
+    const uint32_t t = (uint32_t)(x >> 32) >> OB_TILE_SHIFT;
+    if (small) atomicAdd(&mt[t], 1u);
+    else atomicAdd(&mcol[t], 1u);
+  }
+  if (small) {
+    __syncthreads();
+    if (tid < T) mcol[tid] = mt[tid];
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -285,7 +398,7 @@ __device__ __forceinline__ void check_counts(const GramArgs& a, uint32_t* cnt, c
 
 __device__ __forceinline__ uint32_t level1_count(const GramArgs& a, const Work& w, uint32_t tile, uint32_t r) {
   const uint32_t rep = w.rep0 + r;
-  return rep < a.n_reps ? a.m1[(size_t)(w.g ? a.tiles0 + tile : tile) * a.rep_pad + rep] : 0u;
+  return rep < a.n_reps ? a.m1[(size_t)rep * a.tiles_total + (w.g ? a.tiles0 + tile : tile)] : 0u;
 }
 
 __device__ __forceinline__ void publish_counts(const Work& w, uint32_t tile, uint32_t m, uint32_t* mc, uint32_t* cum,
@@ -1081,7 +1194,7 @@ int engine_point_estimate(ob_panel* p, int ref_mode, double* row, double* resid_
 }
 
 // OBRS-1 resample counts for replicates [first_rep, first_rep + n_reps) without the Gram: level-1
-// tile counts into d_m1 ([tile][rep_pad]) and the level-2 count images into d_counts (the
+// tile counts into d_m1 ([replicate][tile]) and the level-2 count images into d_counts (the
 // ob_engine.hpp layout, replicate batches of 64). Used by the Machado-Mata driver (ob_mm.hip).
 int engine_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_reps, hipStream_t s,
                   uint32_t* nb_rep, uint32_t* rep_pad) {
@@ -1095,10 +1208,10 @@ int engine_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_rep
   OB_TRY(ensure_buf(&p->d_counts, p->cap_counts, (size_t)tiles * pl.nb_rep * 4 * kCimgWords));
   HIP_OK(hipMemsetAsync(p->d_flags, 0, sizeof(uint32_t), s));
   const uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
-  const size_t lds_l1 = sizeof(uint32_t) * std::max(p->ntiles[0], p->ntiles[1]);
+  const size_t lds_l1 = sizeof(uint32_t) * std::max(l1_lds_words(p->ntiles[0]), l1_lds_words(p->ntiles[1]));
   HIP_OK(hipFuncSetAttribute((const void*)ob_level1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_l1));
   hipLaunchKernelGGL(ob_level1_kernel, dim3(n_reps, 2), dim3(kBlock), lds_l1, s, p->n[0], p->n[1], p->ntiles[0],
-                     (uint32_t)first_rep, pl.rep_pad, key0, key1, p->d_m1);
+                     (uint32_t)first_rep, tiles, key0, key1, p->d_m1);
   HIP_OK(hipGetLastError());
   GramArgs ga = gram_args(p, pl);
   ga.m1 = p->d_m1;
@@ -1144,7 +1257,7 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   HIP_OK(hipStreamSynchronize(s));  // the host vector dies with this call
   HIP_OK(hipMemsetAsync(p->d_flags, 0, sizeof(uint32_t), s));
 
-  const size_t lds_l1 = sizeof(uint32_t) * std::max(p->ntiles[0], p->ntiles[1]);
+  const size_t lds_l1 = sizeof(uint32_t) * std::max(l1_lds_words(p->ntiles[0]), l1_lds_words(p->ntiles[1]));
   HIP_OK(hipFuncSetAttribute((const void*)ob_level1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_l1));
   HIP_OK(hipFuncSetAttribute((const void*)ob_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)solve_lds_bytes(p)));
@@ -1174,7 +1287,7 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     const bool timed = true;
     if (timed) HIP_OK(hipEventRecord(ev[0], s));
     hipLaunchKernelGGL(ob_level1_kernel, dim3(ns, 2), dim3(kBlock), lds_l1, s, p->n[0], p->n[1], p->ntiles[0], frep,
-                       plx.rep_pad, key0, key1, p->d_m1);
+                       tiles, key0, key1, p->d_m1);
     HIP_OK(hipGetLastError());
     if (timed) HIP_OK(hipEventRecord(ev[1], s));
     GramArgs ga = gram_args(p, plx);

@@ -49,7 +49,7 @@ struct ob_panel {
   int row_len = 0;
 
   // workspace, sized for `cap_reps` replicates per segment
-  uint32_t* d_m1 = nullptr;      // [tile][rep_pad]
+  uint32_t* d_m1 = nullptr;      // [replicate][tile]
   uint32_t* d_counts = nullptr;  // level-2 count images [tile][batch][sub-tile][17 x 64]
   double* d_partial = nullptr;   // [chunk][rep_pad][e_pad]
   double* d_gram = nullptr;      // [rep_pad][2][e_pad]

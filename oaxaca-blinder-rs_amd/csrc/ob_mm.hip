@@ -62,7 +62,7 @@ struct MmArgs {
   uint32_t rep0;           // MM-1 replicate id of slot 0 (OB_MM_POINT_REP: every row once)
   uint32_t seg0;           // slot 0's position in the count-image segment
   const uint32_t* counts;  // level-2 count images (ob_engine.hpp layout); null for the point
-  const uint32_t* m1;      // level-1 tile counts [tile][rep_pad]
+  const uint32_t* m1;      // level-1 tile counts [replicate][tile]
   uint32_t nb_rep, rep_pad;
   uint32_t nch[2];
   size_t rep_rows;         // n0 + n1: state rows per replicate
@@ -952,7 +952,7 @@ __global__ __launch_bounds__(256) void mm_finish_kernel(const MmArgs a, int K, i
     uint32_t s = 0;
     for (uint32_t t = 0; t < nt[g]; ++t) {
       pre[g][t] = s;
-      s += a.m1[(size_t)((g ? a.tiles0 : 0u) + t) * a.rep_pad + pos];
+      s += a.m1[(size_t)pos * (a.tiles0 + nt[1]) + (g ? a.tiles0 : 0u) + t];
     }
     pre[g][nt[g]] = s;
   }

@@ -6,10 +6,13 @@
 // draws per group, unseeded. OBRS-1 produces the same distribution (an exact multinomial with
 // cell probability 1/n_g) from a counter-based stream so that replicate r is reproducible from
 // (seed, r) alone on any GPU count:
-//   level 1: n_g draws, four per Philox call (words x,y,z,w of call p -> draws 4p..4p+3), each an
-//            exact uniform idx on [0, n_g) by Lemire's multiply-and-reject on the 32-bit word
-//            (reject iff low32(x n_g) < 2^32 mod n_g; draw d retries on its own stream
-//            {d, rep, g, OB_TAG_RETRY + (j >> 2)}, word j & 3); tile = idx / OB_TILE_ROWS -> m_j
+//   level 1: the tile counts m_j of n_g uniform row draws, by fair-bit splitting (no per-draw
+//            index): over the dyadic tree of 2^D >= T tiles a node holding c draws sends
+//            popcount(first c bits of its stream) left and the rest right
+//            (ob_l1_split_bits); children past the last tile and draws a partial last tile
+//            rejects (byte >= its rows) are drawn again in further rounds, the last <= 256 by
+//            Lemire's multiply-and-reject over [0, n_g). DESIGN.md §3, oracle
+//            orc_level1_counts.
 //   level 2: m_j draws inside tile j (S_j rows). Full tiles (S_j = OB_TILE_ROWS = 2^8): Philox
 //            call p yields draws 16p..16p+15, draw 16p + 4i + b = byte b (LSB first) of output
 //            word i (exactly uniform, independent). The partial last tile: call p yields draws
@@ -27,9 +30,11 @@
 
 #define OB_TILE_ROWS 256u
 #define OB_TILE_SHIFT 8u
-#define OB_TAG_L1 0x4F425231u /* "OBR1" */
-#define OB_TAG_L2 0x4F425232u /* "OBR2" */
-#define OB_TAG_RETRY 0x52455452u /* "RETR" */
+#define OB_TAG_L1T 0x4C310000u /* "L1" + (round << 5) + level: split bits of node k, {q, rep, 2k | g} */
+#define OB_TAG_L1S 0x4C530000u /* "LS" + round: partial-tile acceptance bytes, {q, rep, g} */
+#define OB_TAG_L1D 0x4C440000u /* "LD" + (j >> 2): direct draw r, attempt j, {r, rep, g} */
+#define OB_L1_DIRECT 256u      /* rejected draws at most this many are drawn directly */
+#define OB_TAG_L2 0x4F425232u  /* "OBR2" */
 
 struct ob_u32x4 {
   uint32_t x, y, z, w;
@@ -52,6 +57,21 @@ OB_HD ob_u32x4 ob_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uin
   }
   ob_u32x4 o = {c0, c1, c2, c3};
   return o;
+}
+
+// Fair bits [128 q, min(c, 128 q + 128)) of a level-1 node stream, counted: bit b of the stream
+// is bit (b & 31) of word ((b >> 5) & 3) of Philox({b >> 7, rep, c2, tag}).
+OB_HD uint32_t ob_l1_split_bits(uint32_t q, uint32_t c, uint32_t rep, uint32_t c2, uint32_t tag, uint32_t k0,
+                                uint32_t k1) {
+  const ob_u32x4 u = ob_philox(q, rep, c2, tag, k0, k1);
+  const uint32_t r = c - 128u * q;
+  const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
+  uint32_t s = 0;
+  for (uint32_t i = 0; i < 4; ++i) {
+    const uint32_t nb = r > 32u * i ? r - 32u * i : 0u;
+    s += (uint32_t)__builtin_popcount(nb >= 32u ? wd[i] : (wd[i] & ((1u << nb) - 1u)));
+  }
+  return s;
 }
 
 // floor(u * s / 2^64), s < 2^32.

@@ -29,9 +29,7 @@
 /* builder.rs:822-827, i.e. n_g i.i.d. uniform draws with replacement per group).            */
 /* ------------------------------------------------------------------------------------------ */
 #define ORC_TILE 256u
-#define ORC_TAG_L1 0x4F425231u /* "OBR1" */
 #define ORC_TAG_L2 0x4F425232u /* "OBR2" */
-#define ORC_TAG_RETRY 0x52455452u /* "RETR" (+ j >> 2) */
 
 /* Philox4x32-10 (Salmon et al., SC'11; Random123 reference constants). */
 void orc_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
@@ -60,34 +58,95 @@ static inline uint64_t orc_draw_u64(const uint32_t w[4], int odd) {
     return odd ? (((uint64_t)w[3] << 32) | w[2]) : (((uint64_t)w[1] << 32) | w[0]);
 }
 
-/* Level 1 row index of draw d (exact uniform on [0, n), Lemire's multiply-and-reject on a
- * 32-bit word x): m = x * n; reject iff low32(m) < (2^32 - n) mod n; accept -> high32(m).
- * A rejected draw d takes its retries from its own stream: retry j is word (j & 3) of
- * Philox({d, rep, g, ORC_TAG_RETRY + (j >> 2)}). Rejection probability < n / 2^32. */
-static inline uint32_t orc_level1_index(uint32_t x, uint32_t d, uint32_t rep, uint32_t g, uint32_t n,
-                                        uint32_t thresh, const uint32_t key[2]) {
-    uint64_t m = (uint64_t)x * n;
-    for (uint32_t j = 0; (uint32_t)m < thresh; ++j) {
-        uint32_t ctr[4] = {d, rep, g, ORC_TAG_RETRY + (j >> 2)}, w[4];
+/* Level 1 (OBRS-1): the tile counts m of n i.i.d. uniform row draws over [0, n),
+ * drawn by fair-bit splitting instead of one index per draw. T = ceil(n / 256) tiles, D =
+ * ceil(log2 T); the dyadic tree over 2^D tiles (rows [0, 2^(D+8))) has node (l, k) = tiles
+ * [k 2^(D-l), (k+1) 2^(D-l)). A round with c_0 draws at the root splits every node (l < D) with
+ * count c into its left child L = popcount of bits [0, c) of the node's bit stream and its right
+ * child c - L: bit b is bit (b & 31) of word ((b >> 5) & 3) of
+ * Philox({b >> 7, rep, (k << 1) | g, ORC_TAG_L1T + (round << 5) + l}). A child starting at tile
+ * >= T is padding: its draws are rejected. At the tiles, a partial last tile (S = n - 256 (T-1)
+ * < 256 rows) accepts draw i iff byte (i & 3) of word ((i >> 2) & 3) of
+ * Philox({i >> 4, rep, g, ORC_TAG_L1S + round}) is < S. Rejected draws R start the next round
+ * while R > 256; the last R <= 256 are direct: draw r is Lemire's multiply-and-reject on word
+ * (j & 3) of Philox({r, rep, g, ORC_TAG_L1D + (j >> 2)}), attempt j. Each fair split is a
+ * Binomial(c, 1/2), so the accepted draws are i.i.d. uniform over the valid rows. */
+#define ORC_TAG_L1T 0x4C310000u /* "L1" + (round << 5) + level */
+#define ORC_TAG_L1S 0x4C530000u /* "LS" + round */
+#define ORC_TAG_L1D 0x4C440000u /* "LD" + (j >> 2) */
+#define ORC_L1_DIRECT 256u
+
+static uint32_t orc_split_left(uint32_t c, uint32_t rep, uint32_t g, uint32_t k, uint32_t tag, const uint32_t key[2]) {
+    uint32_t left = 0;
+    for (uint32_t q = 0; 128u * q < c; ++q) {
+        uint32_t ctr[4] = {q, rep, (k << 1) | g, tag}, w[4];
         orc_philox4x32_10(ctr, key, w);
-        m = (uint64_t)w[j & 3] * n;
+        uint32_t r = c - 128u * q;
+        for (uint32_t i = 0; i < 4; ++i) {
+            uint32_t nb = r > 32u * i ? r - 32u * i : 0u;
+            uint32_t mask = nb >= 32u ? 0xFFFFFFFFu : ((1u << nb) - 1u);
+            left += (uint32_t)__builtin_popcount(w[i] & mask);
+        }
     }
-    return (uint32_t)(m >> 32);
+    return left;
 }
 
-/* Level 1: multinomial tile counts m[tile] for (seed, rep, group) from n draws over [0,n):
- * Philox call p = {p, rep, g, ORC_TAG_L1} gives draws 4p..4p+3 from its words x, y, z, w. */
 void orc_level1_counts(uint64_t seed, uint32_t rep, uint32_t g, uint32_t n, uint32_t* m) {
     uint32_t ntiles = (n + ORC_TILE - 1) / ORC_TILE;
+    if (ntiles == 0) return;
     memset(m, 0, sizeof(uint32_t) * ntiles);
     uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
-    uint32_t thresh = (0u - n) % n;
-    for (uint32_t p = 0; 4u * p < n; ++p) {
-        uint32_t ctr[4] = {p, rep, g, ORC_TAG_L1}, w[4];
-        orc_philox4x32_10(ctr, key, w);
-        for (uint32_t h = 0; h < 4 && 4u * p + h < n; ++h)
-            m[orc_level1_index(w[h], 4u * p + h, rep, g, n, thresh, key) / ORC_TILE]++;
+    uint32_t depth = 0;
+    while ((1u << depth) < ntiles) ++depth;
+    const uint32_t tail = n - (ntiles - 1) * ORC_TILE; /* rows of the last tile */
+    uint32_t* cur = (uint32_t*)malloc(sizeof(uint32_t) * ntiles);
+    uint32_t* nxt = (uint32_t*)malloc(sizeof(uint32_t) * ntiles);
+    uint32_t todo = n;
+    for (uint32_t round = 0; round == 0 || todo > ORC_L1_DIRECT; ++round) {
+        uint32_t rejected = 0, nodes = 1;
+        cur[0] = todo;
+        for (uint32_t l = 0; l < depth; ++l) {
+            uint32_t span = 1u << (depth - l - 1); /* tiles per child */
+            uint32_t nnext = (ntiles + span - 1) / span;
+            for (uint32_t k = 0; k < nodes; ++k) {
+                uint32_t c = cur[k], left = c ? orc_split_left(c, rep, g, k, ORC_TAG_L1T + (round << 5) + l, key) : 0;
+                nxt[2 * k] = left;
+                if (2 * k + 1 < nnext) nxt[2 * k + 1] = c - left;
+                else rejected += c - left;
+            }
+            nodes = nnext;
+            uint32_t* t = cur; cur = nxt; nxt = t;
+        }
+        for (uint32_t t = 0; t < ntiles; ++t) {
+            uint32_t c = cur[t];
+            if (t == ntiles - 1 && tail < ORC_TILE) {
+                uint32_t acc = 0;
+                for (uint32_t q = 0; 16u * q < c; ++q) {
+                    uint32_t ctr[4] = {q, rep, g, ORC_TAG_L1S + round}, w[4];
+                    orc_philox4x32_10(ctr, key, w);
+                    for (uint32_t i = 0; i < 16 && 16u * q + i < c; ++i)
+                        acc += ((w[i >> 2] >> (8u * (i & 3u))) & 0xFFu) < tail;
+                }
+                rejected += c - acc;
+                c = acc;
+            }
+            m[t] += c;
+        }
+        todo = rejected;
     }
+    const uint32_t thresh = (0u - n) % n;
+    for (uint32_t r = 0; r < todo; ++r) {
+        uint64_t x = 0;
+        for (uint32_t j = 0;; ++j) {
+            uint32_t ctr[4] = {r, rep, g, ORC_TAG_L1D + (j >> 2)}, w[4];
+            orc_philox4x32_10(ctr, key, w);
+            x = (uint64_t)w[j & 3] * n;
+            if ((uint32_t)x >= thresh) break;
+        }
+        m[(uint32_t)(x >> 32) / ORC_TILE]++;
+    }
+    free(cur);
+    free(nxt);
 }
 
 /* Full OBRS-1 index list for (seed, rep, group): tiles ascending, draws in q order. */
