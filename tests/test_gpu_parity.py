@@ -426,7 +426,7 @@ def test_full_size_panel_properties(ob, O):
 
 
 def test_largest_group_and_the_limit(ob, O, N):
-    """n_g = 10,485,760 rows (40,960 tiles: level 1's LDS histogram at its 160 KB) runs, and its
+    """n_g = 10,485,760 rows (40,960 tiles, D = 16, 37.5 % of round 0 padding) runs, and its
     bootstrap rows match the oracle's reference algorithm; one more row is refused up front."""
     n = 40960 * 256
     rng = np.random.default_rng(3)
@@ -445,3 +445,24 @@ def test_largest_group_and_the_limit(ob, O, N):
     with pytest.raises(N.OaxacaError) as e:
         ob.Panel(np.zeros((n + 1, 1)), np.zeros(n + 1), xb, yb)
     assert e.value.code == N.OB_E_UNSUPPORTED
+
+
+@pytest.mark.parametrize("na,nb", [(65536, 256), (65537, 300), (131372, 1000), (200000, 70000), (257, 65535)])
+def test_level1_tree_shapes_match_oracle(ob, O, na, nb):
+    """Level 1's fair-bit tree at its shape edges: 256 tiles (the largest LDS-only
+    tree, no padding), 257 tiles (first m1-direct tree, half of round 0 rejected, 1-row tail),
+    one tile, partial tails, several rejection rounds and the direct draws; rows vs the oracle."""
+    rng = np.random.default_rng(na + nb)
+    xa = rng.normal(size=(na, 1))
+    ya = 1.0 + 0.5 * xa[:, 0] + rng.normal(size=na)
+    xb = rng.normal(size=(nb, 1)) + 0.1
+    yb = 0.8 + 0.4 * xb[:, 0] + rng.normal(size=nb)
+    panel = ob.Panel(xa, ya, xb, yb)
+    try:
+        rows, ok = panel.boot(SEED, 5, 4, 0)
+    finally:
+        panel.close()
+    cfg = O.PassConfig(2, 1, 0, False)
+    orows, ook = O.boot_ref(cfg, O.with_intercept(xa), ya, None, O.with_intercept(xb), yb, None, SEED, 5, 4,
+                            threads=8, full=False)
+    assert ok.all() and ook.all() and close(rows, orows, abs(orows[0, 5]))[0]

@@ -214,6 +214,13 @@ def test_resample_is_multinomial(O):
     assert abs(chi2 - (n - 1)) < 6 * np.sqrt(2 * (n - 1))
     m = O.level1_counts(0xABC, 7, 0, 100_000)
     assert m.sum() == 100_000 and len(m) == (100_000 + 255) // 256
+    # the fair-bit tree's shape edges: one tile, exact powers of two, 257 tiles with a 1-row tail
+    for n in (1, 3, 255, 256, 257, 512, 65536, 65537, 131372):
+        for rep in range(3):
+            m = O.level1_counts(0x5EED, rep, 1, n)
+            assert m.sum() == n and len(m) == (n + 255) // 256
+    tail = np.array([O.level1_counts(0x5EED, rep, 0, 257)[-1] for rep in range(400)])
+    assert abs(tail.mean() - 1.0) < 0.25  # a 1-row tail tile: E m = 257 / 257
 
 
 # --- Heckman two-step (heckman.rs, estimation.rs:114-260, math/probit.rs) ---------------------
