@@ -396,9 +396,10 @@ __device__ __forceinline__ void check_counts(const GramArgs& a, uint32_t* cnt, c
   if (part == 0 && sum != mc[r]) atomicOr(a.flags, 1u);
 }
 
-__device__ __forceinline__ uint32_t level1_count(const GramArgs& a, const Work& w, uint32_t tile, uint32_t r) {
-  const uint32_t rep = w.rep0 + r;
-  return rep < a.n_reps ? a.m1[(size_t)rep * a.tiles_total + (w.g ? a.tiles0 + tile : tile)] : 0u;
+// Level-1 count of global tile tt (group 0's tiles, then group 1's) for batch replicate r.
+__device__ __forceinline__ uint32_t level1_count(const GramArgs& a, uint32_t rep0, uint32_t tt, uint32_t r) {
+  const uint32_t rep = rep0 + r;
+  return rep < a.n_reps ? a.m1[(size_t)rep * a.tiles_total + tt] : 0u;
 }
 
 __device__ __forceinline__ void publish_counts(const Work& w, uint32_t tile, uint32_t m, uint32_t* mc, uint32_t* cum,
@@ -413,11 +414,6 @@ __device__ __forceinline__ void publish_counts(const Work& w, uint32_t tile, uin
   }
   cum[lane + 1] = v;
   if (lane == 0) cum[0] = 0;
-}
-
-__device__ __forceinline__ void tile_counts(const GramArgs& a, const Work& w, uint32_t tile, uint32_t* mc,
-                                            uint32_t* cum, int lane) {
-  publish_counts(w, tile, level1_count(a, w, tile, lane), mc, cum, lane);
 }
 
 template <int CB>
@@ -456,12 +452,17 @@ __global__ __launch_bounds__(kBlock) void ob_count_kernel(const GramArgs a) {
   w.rep0 = w.rb * 64;
   const uint32_t tt0 = blockIdx.x * kCntTilesPerBlock;
   const uint32_t tt1 = min(a.tiles_total, tt0 + kCntTilesPerBlock);
+  // wave 0 loads tile tt+1's level-1 counts while the block draws tile tt
+  uint32_t m_next = (wave == 0 && tt0 < tt1) ? level1_count(a, w.rep0, tt0, lane) : 0u;
   for (uint32_t tt = tt0; tt < tt1; ++tt) {
     w.g = tt >= a.tiles0 ? 1u : 0u;
     w.n = w.g ? a.n1 : a.n0;
     const uint32_t tile = tt - (w.g ? a.tiles0 : 0u);
     for (int i = tid; i < 64 * kCntStride; i += kBlock) img[i] = 0u;
-    if (wave == 0) tile_counts(a, w, tile, mc, cum, lane);
+    if (wave == 0) {
+      publish_counts(w, tile, m_next, mc, cum, lane);
+      if (tt + 1 < tt1) m_next = level1_count(a, w.rep0, tt + 1, lane);
+    }
     __syncthreads();
     level2_draws(a, w, tile, img, mc, cum, 0, 1, wave, 4, lane);
     __syncthreads();
