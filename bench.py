@@ -17,6 +17,7 @@ Rank 0 prints one JSON line (contract in the task brief); see DESIGN.md §5 for 
 from __future__ import annotations
 
 import argparse
+import contextlib
 import importlib
 import json
 import os
@@ -52,6 +53,46 @@ def synthetic(rows, preds, weighted, seed=20260424):
     return out
 
 
+@contextlib.contextmanager
+def stdout_to_stderr():
+    """RCCL prints a version banner on stdout when a communicator starts; the bench's stdout must
+    carry only its one JSON line, so fd 1 points at stderr while communicators are created."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        yield
+    finally:
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
+def host_cores():
+    """Threads the CPU baselines use: the box's CPU share (OMP_NUM_THREADS, which the GPU box sets
+    to its per-GPU share), else every core this process may run on."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    try:
+        return max(1, int(env)) if env else len(os.sched_getaffinity(0))
+    except ValueError:
+        return len(os.sched_getaffinity(0))
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_info(threads):
+    return {"cores": threads, "cpu_model": cpu_model(), "host_cpus_visible": len(os.sched_getaffinity(0))}
+
+
 def cpu_baseline(d, preds, weighted, ref, target_s, threads):
     """The oracle's reference-algorithm bootstrap (gather every column, full X^T W X, Cholesky,
     solve, residuals, sigma^2, inverse -- builder.rs:816-839 + ols.rs:44-144) on host cores."""
@@ -68,30 +109,33 @@ def cpu_baseline(d, preds, weighted, ref, target_s, threads):
     t0 = time.perf_counter()
     _, ok = O.boot_ref(*args, 1000, n, threads=threads, full=True)
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "replicates/s", "cores": threads, "kind": "port",
+    return {"value": n / dt, "unit": "replicates/s", **host_info(threads), "kind": "port",
             "sample": f"{n} replicates of the same {d['ya'].size + d['yb'].size}-row x {preds}-predictor "
                       f"{'WLS' if weighted else 'OLS'} panel, oracle/ob_oracle.c orc_boot_ref (full=1), "
                       f"{threads} threads, {dt:.1f} s"}
 
 
-def cpu_baseline_mm(d, sims, target_s):
-    """The oracle's QR (HiGHS exact LP, one group's full design) timed on host cores; an MM
-    replicate is 2 x sims such fits (quantile_decomposition.rs:221-229), so replicates/s =
-    fits/s / (2 sims). The reference's own solver (Clarabel IPM) is not runnable here."""
+def cpu_baseline_mm(d, sims, target_s, threads, min_fits=8):
+    """The oracle's QR (HiGHS exact LP, one group's full design) timed on host cores, at least
+    min_fits fits spread over a thread pool; an MM replicate is 2 x sims such fits
+    (quantile_decomposition.rs:221-229), so replicates/s = fits/s / (2 sims). The reference's own
+    solver (Clarabel IPM) is not runnable here."""
+    from concurrent.futures import ThreadPoolExecutor
+
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
     x = O.with_intercept(d["xa"])
     c = np.ones(len(d["ya"]), dtype=np.int64)
-    t0, n = time.perf_counter(), 0
-    while True:
-        O.qr_exact(x, d["ya"], c, 0.1 + 0.8 * ((n * 0.618) % 1.0))
-        n += 1
-        if time.perf_counter() - t0 > target_s:
-            break
+    taus = [0.1 + 0.8 * ((i * 0.618) % 1.0) for i in range(max(min_fits, threads))]
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        list(ex.map(lambda t: O.qr_exact(x, d["ya"], c, t), taus))
     dt = time.perf_counter() - t0
-    return {"value": n / dt / (2 * sims), "unit": "replicates/s", "cores": 1, "kind": "port",
-            "sample": f"{n} HiGHS QR fits of group A ({len(d['ya'])} rows x {x.shape[1]} columns), {dt:.1f} s; "
+    n = len(taus)
+    return {"value": n / dt / (2 * sims), "unit": "replicates/s", **host_info(threads), "kind": "port",
+            "sample": f"{n} HiGHS QR fits of group A ({len(d['ya'])} rows x {x.shape[1]} columns) on {threads} "
+                      f"threads, {dt:.1f} s ({dt / n * threads:.1f} s per fit per thread); "
                       f"replicates/s = fits/s / {2 * sims}"}
 
 
@@ -160,8 +204,8 @@ def bench_mm(args, world, rank, local, dist):
                      "assemble_ms": asm_ms, "live_fit_rows": fit_rows, "bytes_per_fit_row": bytes_row,
                      "tflops": fit_rows * flops_row / (asm_ms * 1e-3) / 1e12, "max_ipm_iterations": iters},
     }
-    out["cpu_baseline"] = cpu_baseline_mm(d, args.sims, args.cpu_seconds) if world == 1 and args.cpu_seconds > 0 \
-        else None
+    out["cpu_baseline"] = cpu_baseline_mm(d, args.sims, args.cpu_seconds, args.cpu_threads) \
+        if world == 1 and args.cpu_seconds > 0 else None
     rows, ok = last
     out["check"] = {"ok_replicates": int(ok.sum()), "q50_gap_mean": float(np.nanmean(rows[:, 6]))}
     print(json.dumps(out), flush=True)
@@ -256,14 +300,17 @@ def bench_heckman(args, world, rank, local, dist):
         "check": {"ok_replicates": int(okh.sum()), "explained_mean": float(rows[:, 0].mean().item())},
     }
     if world == 1 and args.cpu_seconds > 0:
-        out["cpu_baseline"] = cpu_baseline_heckman(frame, names, zs, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline_heckman(frame, names, zs, args.cpu_seconds, args.cpu_threads)
     pr.close()
     print(json.dumps(out), flush=True)
 
 
-def cpu_baseline_heckman(frame, names, zs, target_s):
-    """The oracle's heckman_single_pass (probit.rs / heckman.rs restated in numpy, one thread) on
-    whole resampled replicates of the same panel, as many as fit in target_s."""
+def cpu_baseline_heckman(frame, names, zs, target_s, threads):
+    """The oracle's heckman_single_pass (probit.rs / heckman.rs restated in numpy) on whole
+    resampled replicates of the same panel, one replicate per task over a thread pool (numpy
+    releases the GIL in its array kernels), as many rounds as fit in target_s."""
+    from concurrent.futures import ThreadPoolExecutor
+
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
@@ -274,18 +321,23 @@ def cpu_baseline_heckman(frame, names, zs, target_s):
         x = np.column_stack([np.ones(len(rows))] + [frame[nm][rows] for nm in names])
         z = np.column_stack([np.ones(len(rows))] + [frame[nm][rows] for nm in zs])
         groups.append(dict(x=x, y=frame["y"][rows], w=None, zsel=z, s=frame["s"][rows]))
-    n, t0 = 0, time.perf_counter()
-    while n == 0 or time.perf_counter() - t0 < target_s:
+
+    def one(rep):
         take = []
         for gi, g in enumerate(groups):
-            idx = O.resample_indices(0x0B5EED, 100000 + n, gi, len(g["y"]))
+            idx = O.resample_indices(0x0B5EED, 100000 + rep, gi, len(g["y"]))
             take.append({k_: (None if v is None else v[idx]) for k_, v in g.items()})
         O.heckman_single_pass(take[0], take[1], 0, False)
-        n += 1
+
+    n, t0 = 0, time.perf_counter()
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        while n == 0 or time.perf_counter() - t0 < target_s:
+            list(ex.map(one, range(n, n + threads)))
+            n += threads
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "replicates/s", "cores": 1, "kind": "port",
-            "sample": f"{n} replicates of the same panel through oracle.heckman_single_pass (numpy, 1 thread), "
-                      f"{dt:.1f} s"}
+    return {"value": n / dt, "unit": "replicates/s", **host_info(threads), "kind": "port",
+            "sample": f"{n} replicates of the same panel through oracle.heckman_single_pass (numpy), "
+                      f"{threads} threads, {dt:.1f} s"}
 
 
 def load_traffic(rows, preds, reps):
@@ -306,13 +358,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--reps", type=int, default=10000, help="replicates per GPU per step")
+    ap.add_argument("--reps", type=int, default=10000,
+                    help="replicates per GPU per step (weak scaling), or per step in total with --strong")
+    ap.add_argument("--strong", action="store_true",
+                    help="configs[2]: --reps replicates per step in total, sharded over the GPUs (strong scaling)")
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--preds", type=int, default=20)
     ap.add_argument("--ref", type=int, default=0, help="ReferenceCoefficients (0 = GroupA)")
     ap.add_argument("--unweighted", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="0 disables the CPU baseline leg")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: the box's CPU share (host_cores())")
     ap.add_argument("--taus", type=str, default="",
                     help="configs[3]: comma-separated RIF quantiles sharing one bootstrap (e.g. 0.1,0.5,0.9); "
                          "reports replicate-quantiles/s instead of the headline metric")
@@ -339,54 +394,58 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.cpu_threads <= 0:
+        args.cpu_threads = host_cores()
     import torch
 
+    torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    if "RANK" in os.environ or world > 1:  # launched by torch.distributed.run (world 1 included)
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
+        with stdout_to_stderr():
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     if args.mm or args.heckman:
         (bench_mm if args.mm else bench_heckman)(args, world, rank, local, dist)
         if dist:
             dist.destroy_process_group()
         return
     ob = importlib.import_module("oaxaca-blinder-rs_amd")
+    N = ob._native
     weighted = not args.unweighted
     d = synthetic(args.rows, args.preds, weighted)
     ya, yb = d["ya"], d["yb"]
     if taus:  # builder.rs:711-757: each group's outcome replaced by its RIF, one column per tau
         ya = np.column_stack([ob.rif(d["ya"], t) for t in taus])
         yb = np.column_stack([ob.rif(d["yb"], t) for t in taus])
-    panel = ob.Panel(d["xa"], ya, d["xb"], yb, d["wa"], d["wb"], device=local)
-    B, rl, ny = args.reps, panel.row_len, panel.n_y
+    # the engine's own RCCL communicator (ob_ctx_create_rank): every step's rows are all-gathered
+    # by ob_boot_run_sharded_device inside the timed loop, at N = 1 too
+    with stdout_to_stderr():
+        uid = [N.unique_id() if rank == 0 else None]
+        if dist is not None and world > 1:
+            dist.broadcast_object_list(uid, src=0)
+        ctx = N.rank_context(local, rank, world, uid[0])
+    panel = ob.Panel(d["xa"], ya, d["xb"], yb, d["wa"], d["wb"], ctx=ctx)
+    # weak: every rank runs --reps replicates per step; strong (configs[2]): --reps in total
+    total = args.reps if args.strong else args.reps * world
+    per_rank = -(-total // world)
+    rl, ny = panel.row_len, panel.n_y
     dev = torch.device("cuda", local)
-    rows = torch.empty((ny * B, rl), dtype=torch.float64, device=dev)
-    ok = torch.empty(ny * B, dtype=torch.uint8, device=dev)
+    rows = torch.empty((ny * total, rl), dtype=torch.float64, device=dev)
+    ok = torch.empty(ny * total, dtype=torch.uint8, device=dev)
     kd = panel.k + panel.n_base
     ns = 6 + 2 * kd  # every reported component (+ total_gap): the only columns the aggregation reads
     stat_cols = np.arange(ns, dtype=np.int32)
-    part = torch.empty((ny * B, ns), dtype=torch.float64, device=dev)
-    all_part = torch.empty((world * ny * B, ns), dtype=torch.float64, device=dev) if world > 1 else part
-    all_ok = torch.empty(world * ny * B, dtype=torch.uint8, device=dev) if world > 1 else ok
     seed = 0x0B5EED
 
     def step(i):
         stream = torch.cuda.current_stream(dev).cuda_stream
-        first = (i * world + rank) * B
-        panel.boot_device(seed, first, B, rows.data_ptr(), ok.data_ptr(), args.ref, stream=stream)
-        part.copy_(rows[:, :ns])  # the component columns only: 48 of 153 f64 per replicate at K = 21
-        if world > 1:
-            dist.all_gather_into_tensor(all_part, part)
-            dist.all_gather_into_tensor(all_ok, ok)
-        if rank == 0:  # per outcome: that outcome's block of every rank, in replicate order
-            h_rows = all_part.cpu().numpy().reshape(world, ny, B, ns)
-            h_ok = all_ok.cpu().numpy().reshape(world, ny, B)
-            stats = [ob.aggregate(np.ascontiguousarray(h_rows[:, t].reshape(-1, ns)),
-                                  np.ascontiguousarray(h_ok[:, t].reshape(-1)), stat_cols) for t in range(ny)][0]
+        panel.boot_sharded_device(seed, i * total, total, rows.data_ptr(), ok.data_ptr(), args.ref, stream=stream)
+        if rank == 0:  # per outcome: builder.rs:841-930 over that outcome's block, in replicate order
+            h_rows = rows[:, :ns].cpu().numpy().reshape(ny, total, ns)
+            h_ok = ok.cpu().numpy().reshape(ny, total)
+            stats = [ob.aggregate(np.ascontiguousarray(h_rows[t]), np.ascontiguousarray(h_ok[t]), stat_cols)
+                     for t in range(ny)][0]
         else:
             torch.cuda.current_stream(dev).synchronize()
             stats = None
@@ -399,31 +458,32 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    gram_ms = 0.0
+    sums = {"gram_ms": 0.0, "level1_ms": 0.0, "counts_ms": 0.0, "reduce_ms": 0.0, "solve_ms": 0.0, "gather_ms": 0.0}
     launches = 0
     stats = None
     for i in range(args.steps):
         stats, tm = step(args.warmup + i)
-        gram_ms += tm["gram_ms"]
+        for k_ in sums:
+            sums[k_] += tm[k_]
         launches += tm["gram_launches"]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed, gram_ms / max(launches, 1)], dtype=torch.float64, device=dev)
-    if dist:
+    t = torch.tensor([elapsed, sums["gram_ms"] / max(launches, 1)], dtype=torch.float64, device=dev)
+    if dist and world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, gram_launch_ms = float(t[0]), float(t[1])
 
     if rank == 0:
-        total_reps = world * B * args.steps
-        value = total_reps / elapsed
+        value = total * args.steps / elapsed
         k = args.preds + 1
         flops_rep = 2.0 * args.rows * (k * (k + 1) / 2 + ny * k)  # SURVEY.md §8d (X^T W X + one X^T W y per outcome)
         bytes_rep = args.rows * (args.preds + (2 if weighted else 1)) * 8.0
-        reps_per_launch = B / max(launches / args.steps, 1)
-        achieved = flops_rep * reps_per_launch / (gram_launch_ms * 1e-3) / 1e12
-        traffic = load_traffic(args.rows, args.preds, B) if not taus else None
+        reps_per_launch = min(per_rank, 16384) if launches else 0
+        achieved = flops_rep * reps_per_launch / (gram_launch_ms * 1e-3) / 1e12 if gram_launch_ms else 0.0
+        traffic = load_traffic(args.rows, args.preds, per_rank) if not taus else None
+        mode = "strong" if args.strong else "weak"
         out = {
             "metric": "bootstrap replicates/sec on 1M-row×20-pred panel at 1/2/4/8 MI355X" if not taus else
                       "RIF bootstrap replicate-quantiles/sec (configs[3], quantiles share each resample)",
@@ -434,14 +494,16 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": mode,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (SURVEY.md §8d wage panel, numpy seed 20260424; OBRS-1 bootstrap seed 0x0B5EED)",
-            "config": {"workload": "configs[1]: two-fold WLS bootstrap, GroupA reference coefficients" if not taus
-                       else f"configs[3]: RIF decomposition at tau={taus}, two-fold WLS, GroupA",
+            "config": {"workload": ("configs[1]: two-fold WLS bootstrap, GroupA reference coefficients" if not args.strong
+                                    else f"configs[2]: {total} replicates per step in total, sharded over {world} GPU(s)")
+                       if not taus else f"configs[3]: RIF decomposition at tau={taus}, two-fold WLS, GroupA",
                        "rows": args.rows, "predictors": args.preds, "weighted": weighted,
-                       "replicates_per_gpu_per_step": B, "parallelism": f"replicates sharded x{world}, RCCL all-gather"},
+                       "replicates_per_step": total, "replicates_per_gpu_per_step": per_rank,
+                       "parallelism": f"replicates sharded x{world}, engine RCCL all-gather (ob_boot_run_sharded_device)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": F64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": achieved / F64_MFMA_PEAK_TFLOPS, "traffic": traffic,
                          "kernel": "ob_gram_kernel", "avg_launch_ms": gram_launch_ms,
@@ -449,14 +511,16 @@ def main():
             "gather_equivalent": {"algorithmic_bytes_per_replicate": bytes_rep,
                                   "GBps": bytes_rep * value / world / 1e9,
                                   "frac_of_hbm_peak": bytes_rep * value / world / 1e9 / HBM_PEAK_GBPS},
+            "breakdown_ms_per_step_rank0": {k_: v / args.steps for k_, v in sums.items()},
         }
         if world == 1 and args.cpu_seconds > 0 and not taus:
             out["cpu_baseline"] = cpu_baseline(d, args.preds, weighted, args.ref, args.cpu_seconds, args.cpu_threads)
         else:
             out["cpu_baseline"] = None
         out["check"] = {"explained_se": float(stats[0][0]), "unexplained_se": float(stats[1][0]),
-                        "ok_replicates": int(all_ok.sum().item()), "quantiles": taus or None}
+                        "ok_replicates": int(ok.sum().item()), "quantiles": taus or None}
         print(json.dumps(out), flush=True)
+    panel.close()
     if dist:
         dist.destroy_process_group()
 

@@ -37,6 +37,7 @@ extern "C" {
 #define OB_E_INVALID 8       /* bad argument */
 #define OB_E_UNSUPPORTED 9   /* outside the engine's scope (Heckman selection, sizes over limits) */
 #define OB_E_OVERFLOW 10     /* a resample count exceeded 255 in one row (probability < 1e-500) */
+#define OB_E_RCCL 11         /* RCCL missing or a collective failed (multi-GPU entry points) */
 
 const char* ob_last_error(void);
 const char* ob_version(void);
@@ -158,10 +159,53 @@ typedef struct {
   double mm_fit_rows;        /* ob_mm_run: live (fit, row) pairs those launches processed */
   int32_t mm_iterations;     /* ob_mm_run: most IPM iterations of a batch */
   double mm_ms;              /* ob_mm_run: whole call, host clock */
+  double gather_ms;          /* sharded runs: the RCCL all-gather of the per-replicate rows (HIP events) */
 } ob_timing;
 int ob_panel_last_timing(const ob_panel* panel, ob_timing* out);
 /* Synchronize the stream used by the last *_device call and collect its timings. */
 int ob_panel_sync(ob_panel* panel);
+
+/* ---- multi-GPU: replicates sharded over GPUs, one RCCL all-gather ----------
+ * Replaces the Rayon into_par_iter of builder.rs:816-839 across devices. Replicates are
+ * independent and a replicate's row is a pure function of (seed, replicate id), so the rows are
+ * bitwise the same on 1, 2, 4 or 8 GPUs. Shard of rank r of W over [first_rep, first_rep + n):
+ * per = ceil(n / W) replicates starting at first_rep + r * per (the last shard may be short or
+ * empty). The per-replicate rows of every rank are then all-gathered over RCCL (xGMI), so every
+ * rank ends with all n rows in replicate order; the caller aggregates them (ob_aggregate /
+ * ob_prepared_finish) on one rank.
+ *
+ * One process per GPU (the torchrun / MPI shape): rank 0 calls ob_get_unique_id, sends the 128
+ * bytes to every rank out of band, and each rank calls ob_ctx_create_rank with its GPU. Panels
+ * created in a rank context run sharded through ob_boot_run_sharded[_device]. A plain ob_ctx acts
+ * as rank 0 of 1 (no collective). */
+typedef struct {
+  char internal[128]; /* ncclUniqueId */
+} ob_unique_id;
+int ob_get_unique_id(ob_unique_id* id);
+int ob_ctx_create_rank(int device, int rank, int world, const ob_unique_id* id, ob_ctx** out);
+int ob_ctx_rank(const ob_ctx* ctx, int* rank, int* world);
+/* This rank's shard + the all-gather; rows/ok (host) receive all n_reps rows on every rank
+   (n_y outcome-major blocks as in ob_boot_run). Collective: every rank of the context calls it
+   with the same seed, first_rep, n_reps and ref_mode. */
+int ob_boot_run_sharded(ob_panel* panel, uint64_t seed, uint64_t first_rep, uint64_t n_reps, int ref_mode,
+                        double* rows, uint8_t* ok);
+/* Same into device buffers (n_reps x row_len doubles, n_reps bytes; x n_y) enqueued on hip_stream
+   (NULL = engine stream); ob_panel_sync waits and fills ob_timing.gather_ms. */
+int ob_boot_run_sharded_device(ob_panel* panel, uint64_t seed, uint64_t first_rep, uint64_t n_reps, int ref_mode,
+                               double* d_rows, uint8_t* d_ok, void* hip_stream);
+/* One process driving several GPUs: panels[i] (the same design, each created in an ob_ctx on a
+   distinct device) takes shard i of n_panels; the shards are all-gathered over an RCCL clique of
+   those devices (ncclCommInitAll, cached per device list) and rows/ok (host) receive all n_reps
+   rows. */
+int ob_boot_run_multi(ob_panel* const* panels, int n_panels, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
+                      int ref_mode, double* rows, uint8_t* ok);
+
+/* ---- test hook: the OBRS-1 resample counts themselves (bitwise parity, builder.rs:822-827) ----
+ * For replicates [first_rep, first_rep + n_reps) of `group` (0 = A, 1 = B): level1 receives
+ * n_reps x ceil(n_g / 256) tile counts and row_counts n_reps x n_g per-row draw counts, exactly
+ * as the Gram kernel consumes them. Either output may be NULL. */
+int ob_debug_counts(ob_panel* panel, uint64_t seed, uint64_t first_rep, uint32_t n_reps, int group,
+                    uint32_t* level1, uint8_t* row_counts);
 
 /* ---- inference (host) --------------------------------------------------------------------- */
 /* inference.rs:4-34: out = {std_err, p_value, ci_lower, ci_upper}; n = 0 gives NaNs. */
@@ -230,6 +274,9 @@ int ob_prepared_n_y(const ob_prepared* prep);
 uint64_t ob_prepared_seed(const ob_prepared* prep);
 ob_panel* ob_prepared_panel(ob_prepared* prep);
 int ob_prepared_boot(ob_prepared* prep, uint64_t first_rep, uint64_t n_reps, double* rows, uint8_t* ok);
+/* ob_boot_run_sharded over the prepared panel (its seed and reference coefficients): with a rank
+   context (ob_ctx_create_rank) each rank runs its shard and every rank receives all rows. */
+int ob_prepared_boot_sharded(ob_prepared* prep, uint64_t first_rep, uint64_t n_reps, double* rows, uint8_t* ok);
 int ob_prepared_boot_device(ob_prepared* prep, uint64_t first_rep, uint64_t n_reps, double* d_rows,
                             uint8_t* d_ok, void* hip_stream);
 /* Aggregation of builder.rs:841-950 over the successful rows (ok != 0), in replicate order. */

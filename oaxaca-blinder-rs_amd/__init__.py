@@ -9,12 +9,12 @@ from ._native import OaxacaError
 from .api import (BudgetAdjustment, ComponentResult, DecompositionDetail, OaxacaBlinder, OaxacaBuilder,
                   OaxacaResults, PreparedRun, QuantileDecompositionBuilder, QuantileDecompositionDetail,
                   QuantileDecompositionResults, ReferenceCoefficients, TwoFoldResults, parse_formula)
-from .engine import Panel, aggregate, bootstrap_stats, rif, row_layout
+from .engine import Panel, aggregate, boot_multi, bootstrap_stats, rif, row_layout
 from .frame import Frame, read_csv
 
 __all__ = [
     "OaxacaBuilder", "OaxacaBlinder", "OaxacaResults", "TwoFoldResults", "DecompositionDetail",
     "ComponentResult", "BudgetAdjustment", "ReferenceCoefficients", "OaxacaError", "PreparedRun",
-    "Panel", "Frame", "read_csv", "aggregate", "bootstrap_stats", "rif", "row_layout", "parse_formula",
+    "Panel", "boot_multi", "Frame", "read_csv", "aggregate", "bootstrap_stats", "rif", "row_layout", "parse_formula",
     "QuantileDecompositionBuilder", "QuantileDecompositionDetail", "QuantileDecompositionResults",
 ]

@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(_HERE, "liboaxaca_boot.so")
 
 OB_OK = 0
 OB_E_POLARS, OB_E_COLUMN, OB_E_GROUP, OB_E_LINALG, OB_E_DIAG, OB_E_INSUFFICIENT = 1, 2, 3, 4, 5, 6
-OB_E_HIP, OB_E_INVALID, OB_E_UNSUPPORTED, OB_E_OVERFLOW = 7, 8, 9, 10
+OB_E_HIP, OB_E_INVALID, OB_E_UNSUPPORTED, OB_E_OVERFLOW, OB_E_RCCL = 7, 8, 9, 10, 11
 
 OB_COL_F64, OB_COL_I64, OB_COL_STR = 0, 1, 2
 OB_TABLE_TWO_FOLD, OB_TABLE_DETAILED_EXPLAINED, OB_TABLE_DETAILED_UNEXPLAINED = 0, 1, 2
@@ -37,6 +37,8 @@ EXPORTED = (
     "ob_matrices_dims", "ob_matrices_get", "ob_matrices_name", "ob_matrices_free",
     "ob_mm_run", "ob_quantile_decomposition_run", "ob_qd_results_dims", "ob_qd_results_get",
     "ob_qd_results_n_failed", "ob_qd_results_free",
+    "ob_get_unique_id", "ob_ctx_create_rank", "ob_ctx_rank", "ob_boot_run_sharded", "ob_boot_run_sharded_device",
+    "ob_boot_run_multi", "ob_debug_counts", "ob_prepared_boot_sharded",
 )
 
 
@@ -70,7 +72,11 @@ class ob_timing(C.Structure):
                 ("blocks", C.c_int32), ("counts_ms", C.c_double),
                 ("heckman_ms", C.c_double), ("probit_iterations", C.c_int32),
                 ("mm_assemble_ms", C.c_double), ("mm_fit_rows", C.c_double), ("mm_iterations", C.c_int32),
-                ("mm_ms", C.c_double)]
+                ("mm_ms", C.c_double), ("gather_ms", C.c_double)]
+
+
+class ob_unique_id(C.Structure):
+    _fields_ = [("internal", C.c_uint8 * 128)]  # raw bytes (a c_char array would stop at NUL)
 
 
 class ob_column(C.Structure):
@@ -169,6 +175,14 @@ _SIGS = {
     "ob_qd_results_get": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_char_p), C.POINTER(ob_component)]),
     "ob_qd_results_n_failed": (C.c_int64, [_P]),
     "ob_qd_results_free": (None, [_P]),
+    "ob_get_unique_id": (C.c_int, [C.POINTER(ob_unique_id)]),
+    "ob_ctx_create_rank": (C.c_int, [C.c_int, C.c_int, C.c_int, C.POINTER(ob_unique_id), C.POINTER(_P)]),
+    "ob_ctx_rank": (C.c_int, [_P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "ob_boot_run_sharded": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, _D, _U8]),
+    "ob_boot_run_sharded_device": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, _P, _P, _P]),
+    "ob_boot_run_multi": (C.c_int, [C.POINTER(_P), C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, _D, _U8]),
+    "ob_prepared_boot_sharded": (C.c_int, [_P, C.c_uint64, C.c_uint64, _D, _U8]),
+    "ob_debug_counts": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_int, C.POINTER(C.c_uint32), _U8]),
 }
 
 _lib = None
@@ -216,10 +230,16 @@ def check(rc: int) -> None:
 _ctx_cache: dict = {}
 
 
-def context(device: int | None = None) -> C.c_void_p:
-    """Process-wide ob_ctx for ``device`` (default: LOCAL_RANK or 0)."""
+def resolve_device(device: int | None = None) -> int:
+    """The GPU a ``device=None`` call uses: OB_DEVICE, else LOCAL_RANK, else 0."""
     if device is None:
         device = int(os.environ.get("OB_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+    return int(device)
+
+
+def context(device: int | None = None) -> C.c_void_p:
+    """Process-wide ob_ctx for ``device`` (default: resolve_device())."""
+    device = resolve_device(device)
     with _lib_lock:
         ctx = _ctx_cache.get(device)
     if ctx is None:
@@ -227,6 +247,35 @@ def context(device: int | None = None) -> C.c_void_p:
         check(lib().ob_ctx_create(device, C.byref(ctx)))
         with _lib_lock:
             _ctx_cache[device] = ctx
+    return ctx
+
+
+def unique_id() -> bytes:
+    """ncclGetUniqueId through the engine (rank 0 calls it and broadcasts the 128 bytes)."""
+    u = ob_unique_id()
+    check(lib().ob_get_unique_id(C.byref(u)))
+    return C.string_at(C.addressof(u), C.sizeof(u))
+
+
+_rank_ctx_cache: dict = {}
+
+
+def rank_context(device: int, rank: int, world: int, uid: bytes) -> C.c_void_p:
+    """An ob_ctx that is rank ``rank`` of ``world`` on an RCCL communicator (ob_ctx_create_rank).
+    Cached per (device, rank, world, uid); panels created in it run sharded."""
+    key = (device, rank, world, bytes(uid))
+    with _lib_lock:
+        ctx = _rank_ctx_cache.get(key)
+    if ctx is None:
+        uid = bytes(uid)
+        if len(uid) != C.sizeof(ob_unique_id):
+            raise ValueError("a unique id is 128 bytes")
+        u = ob_unique_id()
+        C.memmove(C.addressof(u), uid, len(uid))
+        ctx = C.c_void_p()
+        check(lib().ob_ctx_create_rank(device, rank, world, C.byref(u), C.byref(ctx)))
+        with _lib_lock:
+            _rank_ctx_cache[key] = ctx
     return ctx
 
 

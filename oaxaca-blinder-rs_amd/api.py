@@ -241,6 +241,7 @@ class OaxacaBuilder:
         self._selection_predictors: list[str] = []
         self._seed: int | None = None
         self._device: int | None = None
+        self._ctx = None  # an explicit ob_ctx (distributed.fit_sharded's rank context)
 
     @classmethod
     def from_formula(cls, dataframe, formula: str, group: str, reference_group: str):
@@ -380,16 +381,18 @@ class OaxacaBuilder:
         cols, ncol, nrow = self._frame.as_c()
         cfg, keep = self._config()
         h = C.c_void_p()
-        N.check(lib.ob_builder_prepare(N.context(self._device), cols, ncol, nrow, C.byref(cfg), C.byref(h)))
-        return PreparedRun(h, self._bootstrap_reps)
+        ctx = self._ctx if self._ctx is not None else N.context(self._device)
+        N.check(lib.ob_builder_prepare(ctx, cols, ncol, nrow, C.byref(cfg), C.byref(h)))
+        return PreparedRun(h, self._bootstrap_reps, N.resolve_device(self._device))
 
 
 class PreparedRun:
     """An ``ob_prepared`` handle: panel resident in HBM + point estimate."""
 
-    def __init__(self, handle, reps: int):
+    def __init__(self, handle, reps: int, device: int = 0):
         self._h = handle
         self.bootstrap_reps = reps
+        self.device = device  # the GPU holding the panel
         self.row_len = N.lib().ob_prepared_row_len(handle)
         self.seed = int(N.lib().ob_prepared_seed(handle))
 
@@ -400,6 +403,17 @@ class PreparedRun:
             N.check(N.lib().ob_prepared_boot(self._h, first_rep, n_reps,
                                              rows.ctypes.data_as(C.POINTER(C.c_double)),
                                              ok.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return rows, ok
+
+    def boot_sharded(self, first_rep: int, n_reps: int):
+        """ob_prepared_boot_sharded: this rank's shard + the engine's RCCL all-gather (a rank
+        context) -> all rows on every rank."""
+        rows = np.empty((n_reps, self.row_len), dtype=np.float64)
+        ok = np.zeros(n_reps, dtype=np.uint8)
+        if n_reps:
+            N.check(N.lib().ob_prepared_boot_sharded(self._h, first_rep, n_reps,
+                                                     rows.ctypes.data_as(C.POINTER(C.c_double)),
+                                                     ok.ctypes.data_as(C.POINTER(C.c_uint8))))
         return rows, ok
 
     def boot_device(self, first_rep: int, n_reps: int, rows_ptr: int, ok_ptr: int, stream: int | None):

@@ -860,6 +860,11 @@ int ob_prepared_boot(ob_prepared* p, uint64_t first_rep, uint64_t n_reps, double
   return ob_boot_run(p->panel, p->seed, first_rep, n_reps, p->ref, rows, ok);
 }
 
+int ob_prepared_boot_sharded(ob_prepared* p, uint64_t first_rep, uint64_t n_reps, double* rows, uint8_t* ok) {
+  if (!p) return ob::fail(OB_E_INVALID, "null pointer");
+  return ob_boot_run_sharded(p->panel, p->seed, first_rep, n_reps, p->ref, rows, ok);
+}
+
 int ob_prepared_boot_device(ob_prepared* p, uint64_t first_rep, uint64_t n_reps, double* d_rows, uint8_t* d_ok,
                             void* hip_stream) {
   if (!p) return ob::fail(OB_E_INVALID, "null pointer");

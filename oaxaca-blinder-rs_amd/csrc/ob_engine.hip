@@ -1366,6 +1366,12 @@ int engine_collect(ob_panel* p) {
     }
   }
   if (p->heckman) p->timing.heckman_ms = p->timing.solve_ms;
+  if (p->gather_timed) {  // ob_shard.cpp: the RCCL all-gather after the last segment
+    float t = 0.f;
+    HIP_OK(hipEventElapsedTime(&t, p->gather_ev[0], p->gather_ev[1]));
+    p->timing.gather_ms = t;
+    p->gather_timed = false;
+  }
   uint32_t flag = 0;
   HIP_OK(hipMemcpy(&flag, p->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost));
   if (flag) return ob::fail(OB_E_OVERFLOW, "a resampled row was drawn more than 255 times in one replicate");
@@ -1418,6 +1424,7 @@ int ob_ctx_create(int device, ob_ctx** out) {
 void ob_ctx_destroy(ob_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+  if (ctx->comm && ctx->comm_free) ctx->comm_free(ctx->comm);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -1586,6 +1593,12 @@ void ob_panel_destroy(ob_panel* p) {
   (void)hipFree(p->d_hactive);
   (void)hipFree(p->d_rows_tmp);
   (void)hipFree(p->d_ok_tmp);
+  (void)hipFree(p->d_shard_rows);
+  (void)hipFree(p->d_shard_ok);
+  (void)hipFree(p->d_gather_rows);
+  (void)hipFree(p->d_gather_ok);
+  for (hipEvent_t e : p->gather_ev)
+    if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : p->seg_events) (void)hipEventDestroy(e);
   if (p->mm_ws_free) p->mm_ws_free(p->mm_ws);
   delete p;
@@ -1648,6 +1661,46 @@ int ob_boot_run(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   OB_TRY(ob::engine_collect(p));
   HIP_OK(hipMemcpy(rows, p->d_rows_tmp, sizeof(double) * n_reps * p->row_len * p->n_y, hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(ok, p->d_ok_tmp, n_reps * p->n_y, hipMemcpyDeviceToHost));
+  return OB_OK;
+}
+
+// Test hook (include/oaxaca_boot.h): the OBRS-1 counts of replicates [first_rep, first_rep + n)
+// exactly as ob_count_kernel leaves them for the Gram kernel, unpacked on the host.
+int ob_debug_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_reps, int group, uint32_t* level1,
+                    uint8_t* row_counts) {
+  if (!p || (group != 0 && group != 1)) return ob::fail(OB_E_INVALID, "bad arguments");
+  if (n_reps == 0) return OB_OK;
+  if (n_reps > 16384) return ob::fail(OB_E_INVALID, "at most 16384 replicates per call");
+  HIP_OK(hipSetDevice(p->ctx->device));
+  hipStream_t s = p->ctx->stream;
+  uint32_t nb = 0, rep_pad = 0;
+  OB_TRY(ob::engine_counts(p, seed, first_rep, n_reps, s, &nb, &rep_pad));
+  HIP_OK(hipStreamSynchronize(s));
+  uint32_t flag = 0;
+  HIP_OK(hipMemcpy(&flag, p->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (flag) return ob::fail(OB_E_OVERFLOW, "a resampled row was drawn more than 255 times in one replicate");
+  const uint32_t tiles = p->ntiles[0] + p->ntiles[1], tg = p->ntiles[group], t0 = group ? p->ntiles[0] : 0u;
+  const uint32_t n = p->n[group];
+  if (level1) {
+    std::vector<uint32_t> m1((size_t)tiles * n_reps);
+    HIP_OK(hipMemcpy(m1.data(), p->d_m1, sizeof(uint32_t) * m1.size(), hipMemcpyDeviceToHost));
+    for (uint32_t r = 0; r < n_reps; ++r)
+      for (uint32_t t = 0; t < tg; ++t) level1[(size_t)r * tg + t] = m1[(size_t)r * tiles + t0 + t];
+  }
+  if (row_counts && n) {
+    const size_t per_tile = (size_t)nb * 4 * kCimgWords;
+    std::vector<uint32_t> img((size_t)tg * per_tile);
+    HIP_OK(hipMemcpy(img.data(), p->d_counts + (size_t)t0 * per_tile, sizeof(uint32_t) * img.size(),
+                     hipMemcpyDeviceToHost));
+    for (uint32_t r = 0; r < n_reps; ++r) {
+      const uint32_t b = r >> 6, lr = r & 63u;
+      for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t t = i / OB_TILE_ROWS, within = i % OB_TILE_ROWS, sub = within >> 6, q = within & 63u;
+        const uint32_t word = img[(size_t)t * per_tile + ((size_t)b * 4 + sub) * kCimgWords + lr * kCimgStride + (q >> 2)];
+        row_counts[(size_t)r * n + i] = (uint8_t)((word >> (8 * (q & 3u))) & 0xFFu);
+      }
+    }
+  }
   return OB_OK;
 }
 

@@ -17,6 +17,10 @@ struct ob_ctx {
   int device = 0;
   int cus = 0;
   hipStream_t stream = nullptr;
+  // rank contexts (ob_ctx_create_rank, ob_shard.cpp): this process's RCCL communicator
+  int rank = 0, world = 1;
+  void* comm = nullptr;             // ncclComm_t
+  void (*comm_free)(void*) = nullptr;
 };
 
 // Normalization lists (normalization.rs:5-51) in the layout the solve kernel reads.
@@ -67,6 +71,14 @@ struct ob_panel {
   size_t cap_m1 = 0, cap_partial = 0, cap_gram = 0, cap_chunks = 0, cap_counts = 0;
   void* mm_ws = nullptr;  // Machado-Mata workspace (ob_mm.hip), freed by mm_ws_free
   void (*mm_ws_free)(void*) = nullptr;
+  // sharded runs (ob_shard.cpp): this rank's rows, the all-gathered rows, the gather's events
+  double* d_shard_rows = nullptr;
+  uint8_t* d_shard_ok = nullptr;
+  double* d_gather_rows = nullptr;
+  uint8_t* d_gather_ok = nullptr;
+  size_t cap_shard = 0, cap_gather = 0, cap_shard_ok = 0, cap_gather_ok = 0;
+  hipEvent_t gather_ev[2] = {nullptr, nullptr};
+  bool gather_timed = false;
   std::vector<hipEvent_t> seg_events;  // 6 per segment of the last boot run
   ob_timing timing = {};
   bool timing_pending = false;

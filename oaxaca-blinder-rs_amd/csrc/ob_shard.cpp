@@ -1,0 +1,329 @@
+// ob_shard.cpp -- replicates sharded over GPUs with one RCCL all-gather of the per-replicate rows
+// (replaces the Rayon `into_par_iter` of builder.rs:816-839 across devices).
+//
+// A replicate's row is a pure function of (seed, replicate id) and the panel (OBRS-1 counters are
+// global replicate ids; the chunking depends on the panel only), so rank r simply runs replicate
+// ids [first + r*per, first + (r+1)*per) on its own GPU and the gathered rows equal a one-GPU run
+// bit for bit. The only collective is ncclAllGather over xGMI: (n_y x per x row_len) f64 plus
+// n_y x per status bytes per rank, once per run.
+//
+// RCCL is bound lazily (dlopen of librccl.so.1): a process that already holds PyTorch's RCCL
+// reuses that copy (same soname), and a host without RCCL still loads the engine for the
+// single-GPU entry points.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#include "ob_common.hpp"
+#include "ob_engine.hpp"
+
+static_assert(sizeof(ob_unique_id) == sizeof(ncclUniqueId), "ob_unique_id mirrors ncclUniqueId");
+
+namespace {
+
+#define SH_HIP(expr)                                                                                      \
+  do {                                                                                                    \
+    hipError_t e_ = (expr);                                                                               \
+    if (e_ != hipSuccess)                                                                                 \
+      return ob::fail(OB_E_HIP, "HIP error %s at %s:%d", hipGetErrorString(e_), __FILE__, __LINE__);     \
+  } while (0)
+
+struct Rccl {
+  void* h = nullptr;
+  ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+  ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+  ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*group_start)() = nullptr;
+  ncclResult_t (*group_end)() = nullptr;
+  const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+std::mutex g_rccl_mu;
+
+// Resolve the RCCL entry points once; nullptr (with ob_last_error set) when RCCL is absent.
+const Rccl* rccl() {
+  static Rccl r;
+  static bool tried = false;
+  std::lock_guard<std::mutex> lk(g_rccl_mu);
+  if (!tried) {
+    tried = true;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (h) {
+      r.get_unique_id = (decltype(r.get_unique_id))dlsym(h, "ncclGetUniqueId");
+      r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(h, "ncclCommInitRank");
+      r.comm_init_all = (decltype(r.comm_init_all))dlsym(h, "ncclCommInitAll");
+      r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+      r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
+      r.group_start = (decltype(r.group_start))dlsym(h, "ncclGroupStart");
+      r.group_end = (decltype(r.group_end))dlsym(h, "ncclGroupEnd");
+      r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
+      if (r.get_unique_id && r.comm_init_rank && r.comm_init_all && r.comm_destroy && r.all_gather &&
+          r.group_start && r.group_end && r.error_string)
+        r.h = h;
+    }
+  }
+  if (!r.h) {
+    ob::fail(OB_E_RCCL, "RCCL (librccl.so.1) is not loadable: the multi-GPU gather needs it");
+    return nullptr;
+  }
+  return &r;
+}
+
+int rccl_fail(const Rccl* r, ncclResult_t e, const char* what) {
+  return ob::fail(OB_E_RCCL, "RCCL %s failed: %s", what, r->error_string(e));
+}
+
+#define SH_NCCL(r, expr, what)                     \
+  do {                                             \
+    ncclResult_t n_ = (expr);                      \
+    if (n_ != ncclSuccess) return rccl_fail(r, n_, what); \
+  } while (0)
+
+void comm_free(void* c) {
+  if (!c) return;
+  std::lock_guard<std::mutex> lk(g_rccl_mu);  // rccl() is resolved: a communicator exists
+  static ncclResult_t (*destroy)(ncclComm_t) = nullptr;
+  if (!destroy) destroy = (decltype(destroy))dlsym(RTLD_DEFAULT, "ncclCommDestroy");
+  if (destroy) (void)destroy((ncclComm_t)c);
+}
+
+struct Shard {
+  uint64_t per, first, count;
+};
+
+Shard shard_of(uint64_t first_rep, uint64_t n_reps, int rank, int world) {
+  Shard s;
+  s.per = (n_reps + (uint64_t)world - 1) / (uint64_t)world;
+  const uint64_t lo = std::min<uint64_t>((uint64_t)rank * s.per, n_reps);
+  s.first = first_rep + lo;
+  s.count = std::min<uint64_t>(n_reps, lo + s.per) - lo;
+  return s;
+}
+
+template <typename T>
+int ensure_dev(T** buf, size_t* cap, size_t elems) {
+  if (*cap >= elems) return OB_OK;
+  (void)hipFree(*buf);
+  *buf = nullptr;
+  *cap = 0;
+  SH_HIP(hipMalloc(buf, sizeof(T) * std::max<size_t>(elems, 1)));
+  *cap = elems;
+  return OB_OK;
+}
+
+// Enqueue this rank's shard into the panel's shard buffers ([t][count][row_len] blocks inside an
+// n_y x per x row_len allocation), then the all-gather of each outcome's per-row block into
+// [t][world x per][row_len]. The gathered blocks are in replicate order (rank r holds ids
+// [r per, (r+1) per)); the padding past n_reps is ignored. Collective calls are enqueued by
+// `gather` so that several devices' calls can share one ncclGroupStart/End.
+int shard_compute(ob_panel* p, uint64_t seed, const Shard& sh, int world, int ref_mode, hipStream_t s) {
+  const size_t rl = (size_t)p->row_len, ny = (size_t)p->n_y;
+  SH_HIP(hipSetDevice(p->ctx->device));
+  const size_t slots = ny * std::max<uint64_t>(sh.per, 1);
+  OB_TRY(ensure_dev(&p->d_shard_rows, &p->cap_shard, slots * rl));
+  OB_TRY(ensure_dev(&p->d_shard_ok, &p->cap_shard_ok, slots));
+  OB_TRY(ensure_dev(&p->d_gather_rows, &p->cap_gather, slots * (size_t)world * rl));
+  OB_TRY(ensure_dev(&p->d_gather_ok, &p->cap_gather_ok, slots * (size_t)world));
+  SH_HIP(hipMemsetAsync(p->d_shard_ok, 0, slots, s));
+  if (sh.count) {
+    OB_TRY(ob::engine_boot(p, seed, sh.first, sh.count, ref_mode, p->d_shard_rows, p->d_shard_ok, s));
+  } else {  // an empty shard (n_reps < world): nothing to time but the gather
+    std::memset(&p->timing, 0, sizeof(p->timing));
+    p->pending_segments = 0;
+  }
+  if (!p->gather_ev[0]) {
+    SH_HIP(hipEventCreate(&p->gather_ev[0]));
+    SH_HIP(hipEventCreate(&p->gather_ev[1]));
+  }
+  SH_HIP(hipEventRecord(p->gather_ev[0], s));
+  return OB_OK;
+}
+
+int shard_gather(const Rccl* r, ob_panel* p, ncclComm_t comm, const Shard& sh, int world, hipStream_t s) {
+  const size_t rl = (size_t)p->row_len;
+  for (int t = 0; t < p->n_y; ++t) {  // engine_boot wrote outcome t's rows at t * count
+    SH_NCCL(r, r->all_gather(p->d_shard_rows + (size_t)t * sh.count * rl,
+                             p->d_gather_rows + (size_t)t * world * sh.per * rl, sh.per * rl, ncclFloat64, comm, s),
+            "ncclAllGather(rows)");
+    SH_NCCL(r, r->all_gather(p->d_shard_ok + (size_t)t * sh.count, p->d_gather_ok + (size_t)t * world * sh.per,
+                             sh.per, ncclUint8, comm, s),
+            "ncclAllGather(ok)");
+  }
+  return OB_OK;
+}
+
+// Gathered blocks -> the caller's [t][n_reps] layout (device or host), then the gather's end event.
+int shard_deliver(ob_panel* p, const Shard& sh, int world, uint64_t n_reps, double* rows, uint8_t* ok,
+                  hipMemcpyKind kind, hipStream_t s) {
+  const size_t rl = (size_t)p->row_len;
+  SH_HIP(hipSetDevice(p->ctx->device));
+  SH_HIP(hipEventRecord(p->gather_ev[1], s));
+  p->gather_timed = true;
+  p->timing_pending = true;  // ob_panel_sync waits on s and reads the gather's events
+  p->last_stream = s;
+  for (int t = 0; t < p->n_y; ++t) {
+    SH_HIP(hipMemcpyAsync(rows + (size_t)t * n_reps * rl, p->d_gather_rows + (size_t)t * world * sh.per * rl,
+                          sizeof(double) * n_reps * rl, kind, s));
+    SH_HIP(hipMemcpyAsync(ok + (size_t)t * n_reps, p->d_gather_ok + (size_t)t * world * sh.per, n_reps, kind, s));
+  }
+  return OB_OK;
+}
+
+bool valid_ref(int m) { return m >= OB_REF_GROUP_A && m <= OB_REF_NEUMARK; }
+
+int check_panel(const ob_panel* p, int ref_mode) {
+  if (!valid_ref(ref_mode)) return ob::fail(OB_E_INVALID, "unknown reference coefficients %d", ref_mode);
+  if (p->n[0] == 0 || p->n[1] == 0) return ob::fail(OB_E_GROUP, "%sOne group has no data", ob::error_prefix(OB_E_GROUP));
+  return OB_OK;
+}
+
+int sharded_device(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps, int ref_mode, double* d_rows,
+                   uint8_t* d_ok, hipStream_t stream) {
+  ob_ctx* c = p->ctx;
+  hipStream_t s = stream ? stream : c->stream;
+  if (!c->comm) {  // a plain context: rank 0 of 1, no collective
+    OB_TRY(ob::engine_boot(p, seed, first_rep, n_reps, ref_mode, d_rows, d_ok, s));
+    return OB_OK;
+  }
+  const Rccl* r = rccl();
+  if (!r) return OB_E_RCCL;
+  const Shard sh = shard_of(first_rep, n_reps, c->rank, c->world);
+  OB_TRY(shard_compute(p, seed, sh, c->world, ref_mode, s));
+  OB_TRY(shard_gather(r, p, (ncclComm_t)c->comm, sh, c->world, s));
+  return shard_deliver(p, sh, c->world, n_reps, d_rows, d_ok, hipMemcpyDeviceToDevice, s);
+}
+
+struct Clique {
+  std::vector<ncclComm_t> comms;
+};
+std::map<std::vector<int>, Clique> g_cliques;  // ob_boot_run_multi: one RCCL clique per device list
+
+}  // namespace
+
+extern "C" {
+
+int ob_get_unique_id(ob_unique_id* id) {
+  if (!id) return ob::fail(OB_E_INVALID, "null pointer");
+  const Rccl* r = rccl();
+  if (!r) return OB_E_RCCL;
+  ncclUniqueId u;
+  SH_NCCL(r, r->get_unique_id(&u), "ncclGetUniqueId");
+  std::memcpy(id->internal, u.internal, sizeof(u.internal));
+  return OB_OK;
+}
+
+int ob_ctx_create_rank(int device, int rank, int world, const ob_unique_id* id, ob_ctx** out) {
+  if (!id || !out) return ob::fail(OB_E_INVALID, "null pointer");
+  *out = nullptr;
+  if (world < 1 || rank < 0 || rank >= world) return ob::fail(OB_E_INVALID, "rank %d of world %d", rank, world);
+  const Rccl* r = rccl();
+  if (!r) return OB_E_RCCL;
+  ob_ctx* c = nullptr;
+  OB_TRY(ob_ctx_create(device, &c));
+  ncclUniqueId u;
+  std::memcpy(u.internal, id->internal, sizeof(u.internal));
+  ncclComm_t comm = nullptr;
+  SH_HIP(hipSetDevice(device));
+  const ncclResult_t e = r->comm_init_rank(&comm, world, u, rank);
+  if (e != ncclSuccess) {
+    ob_ctx_destroy(c);
+    return rccl_fail(r, e, "ncclCommInitRank");
+  }
+  c->rank = rank;
+  c->world = world;
+  c->comm = comm;
+  c->comm_free = comm_free;
+  *out = c;
+  return OB_OK;
+}
+
+int ob_ctx_rank(const ob_ctx* c, int* rank, int* world) {
+  if (!c || !rank || !world) return ob::fail(OB_E_INVALID, "null pointer");
+  *rank = c->rank;
+  *world = c->world;
+  return OB_OK;
+}
+
+int ob_boot_run_sharded_device(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps, int ref_mode,
+                               double* d_rows, uint8_t* d_ok, void* hip_stream) {
+  if (!p || (n_reps && (!d_rows || !d_ok))) return ob::fail(OB_E_INVALID, "null pointer");
+  OB_TRY(check_panel(p, ref_mode));
+  if (n_reps == 0) return OB_OK;
+  return sharded_device(p, seed, first_rep, n_reps, ref_mode, d_rows, d_ok, reinterpret_cast<hipStream_t>(hip_stream));
+}
+
+int ob_boot_run_sharded(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps, int ref_mode, double* rows,
+                        uint8_t* ok) {
+  if (!p || (n_reps && (!rows || !ok))) return ob::fail(OB_E_INVALID, "null pointer");
+  OB_TRY(check_panel(p, ref_mode));
+  if (n_reps == 0) return OB_OK;
+  ob_ctx* c = p->ctx;
+  if (!c->comm) return ob_boot_run(p, seed, first_rep, n_reps, ref_mode, rows, ok);
+  const Rccl* r = rccl();
+  if (!r) return OB_E_RCCL;
+  const Shard sh = shard_of(first_rep, n_reps, c->rank, c->world);
+  OB_TRY(shard_compute(p, seed, sh, c->world, ref_mode, c->stream));
+  OB_TRY(shard_gather(r, p, (ncclComm_t)c->comm, sh, c->world, c->stream));
+  OB_TRY(shard_deliver(p, sh, c->world, n_reps, rows, ok, hipMemcpyDeviceToHost, c->stream));
+  return ob_panel_sync(p);
+}
+
+int ob_boot_run_multi(ob_panel* const* panels, int n_panels, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
+                      int ref_mode, double* rows, uint8_t* ok) {
+  if (!panels || n_panels < 1 || (n_reps && (!rows || !ok))) return ob::fail(OB_E_INVALID, "bad arguments");
+  std::vector<int> devs(n_panels);
+  for (int i = 0; i < n_panels; ++i) {
+    if (!panels[i]) return ob::fail(OB_E_INVALID, "null panel %d", i);
+    OB_TRY(check_panel(panels[i], ref_mode));
+    const ob_panel* p0 = panels[0];
+    const ob_panel* pi = panels[i];
+    if (pi->row_len != p0->row_len || pi->n_y != p0->n_y || pi->n[0] != p0->n[0] || pi->n[1] != p0->n[1] ||
+        pi->p != p0->p)
+      return ob::fail(OB_E_INVALID, "panel %d does not hold the same design as panel 0", i);
+    devs[i] = pi->ctx->device;
+    for (int j = 0; j < i; ++j)
+      if (devs[j] == devs[i]) return ob::fail(OB_E_INVALID, "panels %d and %d share device %d", j, i, devs[i]);
+  }
+  if (n_reps == 0) return OB_OK;
+  const Rccl* r = rccl();
+  if (!r) return OB_E_RCCL;
+  Clique* cq = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_rccl_mu);
+    auto it = g_cliques.find(devs);
+    if (it == g_cliques.end()) {
+      Clique c;
+      c.comms.resize(n_panels);
+      const ncclResult_t e = r->comm_init_all(c.comms.data(), n_panels, devs.data());
+      if (e != ncclSuccess) return rccl_fail(r, e, "ncclCommInitAll");
+      it = g_cliques.emplace(devs, std::move(c)).first;
+    }
+    cq = &it->second;
+  }
+  std::vector<Shard> sh(n_panels);
+  for (int i = 0; i < n_panels; ++i) {
+    sh[i] = shard_of(first_rep, n_reps, i, n_panels);
+    OB_TRY(shard_compute(panels[i], seed, sh[i], n_panels, ref_mode, panels[i]->ctx->stream));
+  }
+  SH_NCCL(r, r->group_start(), "ncclGroupStart");
+  int rc = OB_OK;
+  for (int i = 0; i < n_panels && rc == OB_OK; ++i)
+    rc = shard_gather(r, panels[i], cq->comms[i], sh[i], n_panels, panels[i]->ctx->stream);
+  SH_NCCL(r, r->group_end(), "ncclGroupEnd");
+  OB_TRY(rc);
+  ob_panel* p0 = panels[0];
+  OB_TRY(shard_deliver(p0, sh[0], n_panels, n_reps, rows, ok, hipMemcpyDeviceToHost, p0->ctx->stream));
+  for (int i = 0; i < n_panels; ++i) OB_TRY(ob_panel_sync(panels[i]));
+  return OB_OK;
+}
+
+}  // extern "C"

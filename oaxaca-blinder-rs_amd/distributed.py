@@ -4,8 +4,15 @@ per-replicate rows -- the only collective the bootstrap needs.
 The reference runs every replicate in one process on a Rayon pool (builder.rs:816-839).
 Here rank r computes replicate ids [r*per, (r+1)*per) of the OBRS-1 stream (results are a pure
 function of (seed, replicate id), so the gathered rows equal a single-GPU run bit for bit), the
-rows are all-gathered (RCCL over xGMI on GPUs; gloo on CPU tests), and rank 0 aggregates
-(builder.rs:841-950). Launch with torch.distributed.run; MASTER_ADDR=127.0.0.1.
+rows are all-gathered, and rank 0 aggregates (builder.rs:841-950). Two gathers exist:
+
+* ``engine=True`` (the drop-in's own path): the engine's RCCL communicator
+  (``ob_ctx_create_rank`` + ``ob_prepared_boot_sharded``), exactly what a Rust caller binds;
+  torch.distributed only carries the 128-byte unique id from rank 0.
+* ``engine=False``: torch.distributed's all_gather_into_tensor -- on-device over RCCL for an
+  nccl group, through host tensors for gloo (the CPU tests).
+
+Launch with torch.distributed.run; MASTER_ADDR=127.0.0.1.
 """
 from __future__ import annotations
 
@@ -23,9 +30,10 @@ def gather_rows(prepared, n_reps: int, group=None, device=None):
     """Compute this rank's replicates and all-gather every rank's rows.
 
     ``prepared`` is anything with ``row_len``, ``boot(first, n) -> (rows, ok)`` and, for the
-    device path, ``boot_device(first, n, rows_ptr, ok_ptr, stream)`` + ``sync()``
-    (``api.PreparedRun`` provides all of them). Returns (rows, ok) for all ``n_reps`` replicates
-    in replicate order on every rank.
+    device path, ``boot_device(first, n, rows_ptr, ok_ptr, stream)`` + ``sync()`` + ``device``
+    (``api.PreparedRun`` provides all of them). Under an nccl group the rows stay on the GPU
+    (``device`` defaults to the panel's GPU and must equal it). Returns (rows, ok) for all
+    ``n_reps`` replicates in replicate order on every rank.
     """
     import torch
     import torch.distributed as dist
@@ -34,8 +42,14 @@ def gather_rows(prepared, n_reps: int, group=None, device=None):
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     first, count, per = shard(n_reps, rank, world)
     rl = prepared.row_len
-    on_gpu = device is not None and dist.is_initialized() and dist.get_backend(group) == "nccl"
+    on_gpu = dist.is_initialized() and dist.get_backend(group) == "nccl"
     if on_gpu:
+        panel_dev = getattr(prepared, "device", None)
+        if device is None:
+            device = panel_dev if panel_dev is not None else torch.cuda.current_device()
+        device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        if panel_dev is not None and device.index != panel_dev:
+            raise ValueError(f"gather device {device} differs from the panel's GPU {panel_dev}")
         rows = torch.empty((per, rl), dtype=torch.float64, device=device)
         ok = torch.zeros(per, dtype=torch.uint8, device=device)
         if count:
@@ -56,24 +70,53 @@ def gather_rows(prepared, n_reps: int, group=None, device=None):
         dist.all_gather_into_tensor(all_ok, ok, group=group)
     else:
         all_rows, all_ok = rows, ok
-    if on_gpu:
+    if on_gpu and count:
         prepared.sync()
     return all_rows[:n_reps].cpu().numpy(), all_ok[:n_reps].cpu().numpy()
 
 
-def fit_sharded(builder, group=None, device=None):
+def engine_context(device: int, group=None):
+    """This rank's engine context on an RCCL communicator spanning the group's ranks: rank 0's
+    ncclUniqueId travels by broadcast_object_list; the engine owns the communicator."""
+    import torch.distributed as dist
+
+    from . import _native as N
+
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    uid = [N.unique_id() if rank == 0 else None]
+    if world > 1:
+        dist.broadcast_object_list(uid, src=0, group=group)
+    return N.rank_context(device, rank, world, uid[0])
+
+
+def fit_sharded(builder, group=None, device=None, engine=False):
     """``OaxacaBuilder.run()`` over all ranks: every rank prepares the same panel (rank 0's seed
     is broadcast when the builder is unseeded), computes its shard, all ranks gather, rank 0
-    returns the OaxacaResults (other ranks return None)."""
+    returns the OaxacaResults (other ranks return None). ``engine=True`` gathers through the
+    engine's own RCCL communicator (ob_prepared_boot_sharded) instead of torch.distributed."""
     import torch.distributed as dist
+
+    from . import _native as N
 
     if dist.is_initialized() and builder._seed is None:
         seed = [int(np.random.SeedSequence().generate_state(1, np.uint64)[0])]
         dist.broadcast_object_list(seed, src=0, group=group)
         builder.seed(seed[0])
-    prep = builder.prepare()
+    if device is None:
+        device = N.resolve_device(builder._device)
+    builder.device(device)
+    if engine:
+        builder._ctx = engine_context(device, group)
     try:
-        rows, ok = gather_rows(prep, builder._bootstrap_reps, group=group, device=device)
+        prep = builder.prepare()
+    finally:
+        builder._ctx = None
+    try:
+        if engine:
+            rows, ok = prep.boot_sharded(0, builder._bootstrap_reps)
+        else:
+            rows, ok = gather_rows(prep, builder._bootstrap_reps, group=group, device=device)
         rank = dist.get_rank(group) if dist.is_initialized() else 0
         return prep.finish(rows, ok) if rank == 0 else None
     finally:

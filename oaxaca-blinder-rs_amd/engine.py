@@ -41,7 +41,7 @@ class Panel:
     from one Gram pass, and ``point_estimate``/``boot`` return an outcome axis first.
     """
 
-    def __init__(self, xa, ya, xb, yb, wa=None, wb=None, n_num=None, norm=None, device=None):
+    def __init__(self, xa, ya, xb, yb, wa=None, wb=None, n_num=None, norm=None, device=None, ctx=None):
         xa = np.asarray(xa, dtype=np.float64)
         xb = np.asarray(xb, dtype=np.float64)
         if xa.ndim != 2 or xb.ndim != 2 or xa.shape[1] != xb.shape[1]:
@@ -78,7 +78,8 @@ class Panel:
             d.n_norm = len(arrs[2])
             (d.norm_start, d.norm_idx, d.norm_m, d.pooled_start, d.pooled_idx, d.has_base) = [_ip(a) for a in arrs]
         self._h = C.c_void_p()
-        N.check(N.lib().ob_panel_create(N.context(device), C.byref(d), C.byref(self._h)))
+        self._ctx = ctx if ctx is not None else N.context(device)
+        N.check(N.lib().ob_panel_create(self._ctx, C.byref(d), C.byref(self._h)))
         self.k = N.lib().ob_panel_k(self._h)
         self.n_base = N.lib().ob_panel_n_base(self._h)
         self.row_len = N.lib().ob_panel_row_len(self._h)
@@ -118,6 +119,33 @@ class Panel:
         N.check(N.lib().ob_boot_run_device(self._h, seed & ((1 << 64) - 1), first_rep, n_reps, int(ref),
                                            C.c_void_p(rows_ptr), C.c_void_p(ok_ptr), C.c_void_p(stream or 0)))
 
+    def boot_sharded(self, seed: int, first_rep: int, n_reps: int, ref=ReferenceCoefficients.GroupA):
+        """This rank's shard of [first_rep, first_rep + n_reps) plus the RCCL all-gather
+        (ob_boot_run_sharded): every rank returns all rows. Collective over the panel's rank ctx."""
+        rows = np.empty((self.n_y, n_reps, self.row_len))
+        ok = np.zeros((self.n_y, n_reps), dtype=np.uint8)
+        if n_reps:
+            N.check(N.lib().ob_boot_run_sharded(self._h, seed & ((1 << 64) - 1), first_rep, n_reps, int(ref), _dp(rows),
+                                                ok.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return (rows[0], ok[0]) if self.n_y == 1 else (rows, ok)
+
+    def boot_sharded_device(self, seed: int, first_rep: int, n_reps: int, rows_ptr: int, ok_ptr: int,
+                            ref=ReferenceCoefficients.GroupA, stream: int | None = None):
+        N.check(N.lib().ob_boot_run_sharded_device(self._h, seed & ((1 << 64) - 1), first_rep, n_reps, int(ref),
+                                                   C.c_void_p(rows_ptr), C.c_void_p(ok_ptr), C.c_void_p(stream or 0)))
+
+    def debug_counts(self, seed: int, first_rep: int, n_reps: int, group: int):
+        """OBRS-1 counts as the Gram kernel consumes them (ob_debug_counts): (level-1 tile counts
+        [n_reps, tiles], per-row counts [n_reps, n_g] uint8)."""
+        ng = self.n_a if group == 0 else self.n_b
+        tiles = -(-ng // 256)
+        l1 = np.zeros((n_reps, tiles), dtype=np.uint32)
+        rc = np.zeros((n_reps, ng), dtype=np.uint8)
+        N.check(N.lib().ob_debug_counts(self._h, seed & ((1 << 64) - 1), first_rep, n_reps, group,
+                                        l1.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                        rc.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return l1, rc
+
     def sync(self):
         N.check(N.lib().ob_panel_sync(self._h))
 
@@ -136,6 +164,19 @@ class Panel:
             self.close()
         except Exception:
             pass
+
+
+def boot_multi(panels, seed: int, first_rep: int, n_reps: int, ref=ReferenceCoefficients.GroupA):
+    """One process, several GPUs (ob_boot_run_multi): panels[i] (same design, distinct devices)
+    runs shard i; the shards are all-gathered over an RCCL clique of those devices."""
+    p0 = panels[0]
+    rows = np.empty((p0.n_y, n_reps, p0.row_len))
+    ok = np.zeros((p0.n_y, n_reps), dtype=np.uint8)
+    hs = (C.c_void_p * len(panels))(*[p._h for p in panels])
+    if n_reps:
+        N.check(N.lib().ob_boot_run_multi(hs, len(panels), seed & ((1 << 64) - 1), first_rep, n_reps, int(ref),
+                                          _dp(rows), ok.ctypes.data_as(C.POINTER(C.c_uint8))))
+    return (rows[0], ok[0]) if p0.n_y == 1 else (rows, ok)
 
 
 def bootstrap_stats(values, point_estimate: float = 0.0):
