@@ -160,6 +160,7 @@ typedef struct {
   int32_t mm_iterations;     /* ob_mm_run: most IPM iterations of a batch */
   double mm_ms;              /* ob_mm_run: whole call, host clock */
   double gather_ms;          /* sharded runs: the RCCL all-gather of the per-replicate rows (HIP events) */
+  int32_t gram_path;         /* last boot run: 1 = f64 MFMA Gram, 2 = exact integer-sliced i8 MFMA Gram */
 } ob_timing;
 int ob_panel_last_timing(const ob_panel* panel, ob_timing* out);
 /* Synchronize the stream used by the last *_device call and collect its timings. */
@@ -206,6 +207,10 @@ int ob_boot_run_multi(ob_panel* const* panels, int n_panels, uint64_t seed, uint
  * as the Gram kernel consumes them. Either output may be NULL. */
 int ob_debug_counts(ob_panel* panel, uint64_t seed, uint64_t first_rep, uint32_t n_reps, int group,
                     uint32_t* level1, uint8_t* row_counts);
+/* Test hook: the reduced extended Grams G_r = sum_i c_ri v_i v_i^T (upper triangle, row-major pairs,
+   e_pad per group) of replicates [first_rep, first_rep + n_reps <= 16384), gram: n_reps x 2 x e_pad,
+   computed by path 1 (f64 MFMA) or 2 (exact integer-sliced i8 MFMA); 0 = the default choice. */
+int ob_debug_gram(ob_panel* panel, int path, uint64_t seed, uint64_t first_rep, uint32_t n_reps, double* gram);
 
 /* ---- inference (host) --------------------------------------------------------------------- */
 /* inference.rs:4-34: out = {std_err, p_value, ci_lower, ci_upper}; n = 0 gives NaNs. */

@@ -38,7 +38,7 @@ EXPORTED = (
     "ob_mm_run", "ob_quantile_decomposition_run", "ob_qd_results_dims", "ob_qd_results_get",
     "ob_qd_results_n_failed", "ob_qd_results_free",
     "ob_get_unique_id", "ob_ctx_create_rank", "ob_ctx_rank", "ob_boot_run_sharded", "ob_boot_run_sharded_device",
-    "ob_boot_run_multi", "ob_debug_counts", "ob_prepared_boot_sharded",
+    "ob_boot_run_multi", "ob_debug_counts", "ob_prepared_boot_sharded", "ob_debug_gram",
 )
 
 
@@ -72,7 +72,7 @@ class ob_timing(C.Structure):
                 ("blocks", C.c_int32), ("counts_ms", C.c_double),
                 ("heckman_ms", C.c_double), ("probit_iterations", C.c_int32),
                 ("mm_assemble_ms", C.c_double), ("mm_fit_rows", C.c_double), ("mm_iterations", C.c_int32),
-                ("mm_ms", C.c_double), ("gather_ms", C.c_double)]
+                ("mm_ms", C.c_double), ("gather_ms", C.c_double), ("gram_path", C.c_int32)]
 
 
 class ob_unique_id(C.Structure):
@@ -181,6 +181,7 @@ _SIGS = {
     "ob_boot_run_sharded": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, _D, _U8]),
     "ob_boot_run_sharded_device": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, _P, _P, _P]),
     "ob_boot_run_multi": (C.c_int, [C.POINTER(_P), C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, _D, _U8]),
+    "ob_debug_gram": (C.c_int, [_P, C.c_int, C.c_uint64, C.c_uint64, C.c_uint32, _D]),
     "ob_prepared_boot_sharded": (C.c_int, [_P, C.c_uint64, C.c_uint64, _D, _U8]),
     "ob_debug_counts": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_int, C.POINTER(C.c_uint32), _U8]),
 }

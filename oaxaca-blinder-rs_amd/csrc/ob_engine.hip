@@ -382,12 +382,16 @@ __device__ __forceinline__ void level2_draws(const GramArgs& a, const Work& w, u
 // Four threads per replicate (consecutive lanes); threads my in [0, 256). With zero, each thread
 // then clears the 16 words it checked, recycling the image without another barrier.
 __device__ __forceinline__ void check_counts(const GramArgs& a, uint32_t* cnt, const uint32_t* mc, int my,
-                                             bool zero = false) {
+                                             bool zero = false, bool i8 = false) {
   const int r = my >> 2, part = my & 3;
   uint32_t* row = cnt + r * kCntStride + part * 16;
-  uint32_t sum = 0;
+  uint32_t sum = 0, hib = 0;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) sum = __builtin_amdgcn_sad_u8(row[i], 0u, sum);
+  for (int i = 0; i < 16; ++i) {
+    sum = __builtin_amdgcn_sad_u8(row[i], 0u, sum);
+    hib |= row[i] & 0x80808080u;
+  }
+  if (i8 && hib) atomicOr(a.flags, 1u);  // the i8 Gram reads counts as signed bytes: at most 127
   if (zero)
 #pragma unroll
     for (int i = 0; i < 16; ++i) row[i] = 0u;
@@ -443,6 +447,10 @@ __device__ __forceinline__ void store_partials(const GramArgs& a, const Work& w,
 // ---------------------------------------------------------------------------------------------
 constexpr int kCntTilesPerBlock = 8;
 
+// I8: the image is written in the A-fragment order of ob_gram_i8.hip instead: per (tile, batch)
+// [sub-tile][k-half][replicate half][lane][16 B], lane l = replicate (l & 31) of the half, rows
+// 16 (l >> 5) + j of the k-half -- 16 KB, one 16-byte store per thread and unit.
+template <bool I8>
 __global__ __launch_bounds__(kBlock) void ob_count_kernel(const GramArgs a) {
   __shared__ uint32_t img[64 * kCntStride];
   __shared__ uint32_t mc[64], cum[65];
@@ -466,12 +474,21 @@ __global__ __launch_bounds__(kBlock) void ob_count_kernel(const GramArgs a) {
     __syncthreads();
     level2_draws(a, w, tile, img, mc, cum, 0, 1, wave, 4, lane);
     __syncthreads();
-    check_counts(a, img, mc, tid);
+    check_counts(a, img, mc, tid, false, I8);
     const uint32_t ns = (min(OB_TILE_ROWS, w.n - tile * OB_TILE_ROWS) + 63) >> 6;
-    uint32_t* out = const_cast<uint32_t*>(a.counts) + ((size_t)tt * a.nb_rep + w.rb) * 4 * kCimgWords;
-    for (uint32_t i = tid; i < ns * kCimgWords; i += kBlock) {
-      const uint32_t s = i / kCimgWords, rem = i - s * kCimgWords, r = rem / kCimgStride, wd = rem - r * kCimgStride;
-      out[i] = wd < 16 ? img[r * kCntStride + s * 16 + wd] : 0u;
+    if constexpr (I8) {
+      uint4* out = reinterpret_cast<uint4*>(const_cast<uint32_t*>(a.counts)) + ((size_t)tt * a.nb_rep + w.rb) * 1024;
+      for (uint32_t u = tid; u < ns * 256; u += kBlock) {
+        const uint32_t ln = u & 63u, rh = (u >> 6) & 1u, k2 = (u >> 7) & 1u, sb = u >> 8;
+        const uint32_t* src = img + (rh * 32 + (ln & 31u)) * kCntStride + sb * 16 + k2 * 8 + 4 * (ln >> 5);
+        out[u] = make_uint4(src[0], src[1], src[2], src[3]);
+      }
+    } else {
+      uint32_t* out = const_cast<uint32_t*>(a.counts) + ((size_t)tt * a.nb_rep + w.rb) * 4 * kCimgWords;
+      for (uint32_t i = tid; i < ns * kCimgWords; i += kBlock) {
+        const uint32_t s = i / kCimgWords, rem = i - s * kCimgWords, r = rem / kCimgStride, wd = rem - r * kCimgStride;
+        out[i] = wd < 16 ? img[r * kCntStride + s * 16 + wd] : 0u;
+      }
     }
     __syncthreads();
   }
@@ -1222,7 +1239,7 @@ int engine_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_rep
   ga.key1 = key1;
   ga.counts = p->d_counts;
   ga.tiles_total = tiles;
-  hipLaunchKernelGGL(ob_count_kernel, dim3((tiles + kCntTilesPerBlock - 1) / kCntTilesPerBlock, pl.nb_rep),
+  hipLaunchKernelGGL(ob_count_kernel<false>, dim3((tiles + kCntTilesPerBlock - 1) / kCntTilesPerBlock, pl.nb_rep),
                      dim3(kBlock), 0, s, ga);
   HIP_OK(hipGetLastError());
   *nb_rep = pl.nb_rep;
@@ -1254,6 +1271,20 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   OB_TRY(ensure_buf(&p->d_gram, p->cap_gram, (size_t)2 * pl.rep_pad * p->e_pad));
   OB_TRY(ensure_buf(&p->d_chunks, p->cap_chunks, std::max(pl.chunks.size(), pl_tail.chunks.size())));
   if (p->heckman) OB_TRY(ensure_heck(p, pl));
+  // Gram path: the exact integer-sliced i8 GEMM (ob_gram_i8.hip) unless forced to f64 MFMA
+  // (OB_GRAM_PATH=f64), a Heckman panel (its kernels read the f64 path's count images), or the
+  // digit images do not fit.
+  int force = p->gram_force;
+  if (!force) {
+    const char* ev = getenv("OB_GRAM_PATH");
+    force = ev && !strcmp(ev, "f64") ? 1 : (ev && !strcmp(ev, "i8") ? 2 : 0);
+  }
+  bool use_i8 = !p->heckman && force != 1;
+  if (use_i8) {
+    OB_TRY(ob::oz_prepare(p, pl.chunks));
+    use_i8 = p->oz_state == 1;
+    if (!use_i8 && force == 2) return ob::fail(OB_E_UNSUPPORTED, "the i8 Gram's digit images do not fit in HBM");
+  }
   HIP_OK(hipMemcpyAsync(p->d_chunks, pl.chunks.data(), sizeof(uint32_t) * pl.chunks.size(), hipMemcpyHostToDevice, s));
   HIP_OK(hipStreamSynchronize(s));  // the host vector dies with this call
   HIP_OK(hipMemsetAsync(p->d_flags, 0, sizeof(uint32_t), s));
@@ -1264,7 +1295,9 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
                              (int)solve_lds_bytes(p)));
   std::memset(&p->timing, 0, sizeof(p->timing));
   p->timing.chunks = nch;
-  p->timing.blocks = (int32_t)(pl.nb_rep * pl.n_cg * (uint32_t)nch);
+  p->timing.blocks = use_i8 ? (int32_t)((uint32_t)nch * ((pl.nb_rep + 3) / 4) * (uint32_t)p->oz_n_ct)
+                            : (int32_t)(pl.nb_rep * pl.n_cg * (uint32_t)nch);
+  p->timing.gram_path = use_i8 ? 2 : 1;
   p->pending_segments = 0;
   const uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
   const size_t nseg = (size_t)((n_reps + seg - 1) / seg);
@@ -1302,12 +1335,17 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     ga.counts = p->d_counts;
     ga.tiles_total = tiles;
     ga.diag = diag_mode();
-    hipLaunchKernelGGL(ob_count_kernel, dim3((tiles + kCntTilesPerBlock - 1) / kCntTilesPerBlock, plx.nb_rep),
-                       dim3(kBlock), 0, s, ga);
+    const dim3 cgrid((tiles + kCntTilesPerBlock - 1) / kCntTilesPerBlock, plx.nb_rep);
+    if (use_i8) hipLaunchKernelGGL(ob_count_kernel<true>, cgrid, dim3(kBlock), 0, s, ga);
+    else hipLaunchKernelGGL(ob_count_kernel<false>, cgrid, dim3(kBlock), 0, s, ga);
     HIP_OK(hipGetLastError());
     if (timed) HIP_OK(hipEventRecord(ev[2], s));
-    const uint32_t blocks = plx.nb_rep * plx.n_cg * (uint32_t)nchx;
-    HIP_OK(launch_gram(p, plx.cb, false, ga, blocks, s));
+    if (use_i8) {
+      OB_TRY(ob::oz_gram(p, p->d_chunks, nchx, p->d_counts, plx.nb_rep, plx.rep_pad, ns, p->d_partial, s));
+    } else {
+      const uint32_t blocks = plx.nb_rep * plx.n_cg * (uint32_t)nchx;
+      HIP_OK(launch_gram(p, plx.cb, false, ga, blocks, s));
+    }
     if (timed) HIP_OK(hipEventRecord(ev[3], s));
     const size_t nred = (size_t)ns * p->e_pad;
     hipLaunchKernelGGL(ob_reduce_kernel, dim3((unsigned)((nred + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
@@ -1599,6 +1637,9 @@ void ob_panel_destroy(ob_panel* p) {
   (void)hipFree(p->d_gather_ok);
   for (hipEvent_t e : p->gather_ev)
     if (e) (void)hipEventDestroy(e);
+  (void)hipFree(p->d_oz_b[0]);
+  (void)hipFree(p->d_oz_b[1]);
+  (void)hipFree(p->d_oz_pexp);
   for (hipEvent_t e : p->seg_events) (void)hipEventDestroy(e);
   if (p->mm_ws_free) p->mm_ws_free(p->mm_ws);
   delete p;
@@ -1702,6 +1743,31 @@ int ob_debug_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_r
     }
   }
   return OB_OK;
+}
+
+// Test hook: the reduced extended Grams [n_reps][2 groups][e_pad] of replicates
+// [first_rep, first_rep + n_reps) through the requested Gram path (0 auto, 1 f64 MFMA, 2 i8).
+int ob_debug_gram(ob_panel* p, int path, uint64_t seed, uint64_t first_rep, uint32_t n_reps, double* gram) {
+  if (!p || !gram || path < 0 || path > 2) return ob::fail(OB_E_INVALID, "bad arguments");
+  if (n_reps == 0) return OB_OK;
+  if (n_reps > 16384) return ob::fail(OB_E_INVALID, "at most 16384 replicates per call (one segment)");
+  if (p->heckman) return ob::fail(OB_E_UNSUPPORTED, "Heckman panels use the f64 Gram only");
+  HIP_OK(hipSetDevice(p->ctx->device));
+  double* d_rows = nullptr;
+  uint8_t* d_ok = nullptr;
+  HIP_OK(hipMalloc(&d_rows, sizeof(double) * n_reps * p->row_len * p->n_y));
+  HIP_OK(hipMalloc(&d_ok, (size_t)n_reps * p->n_y));
+  const int saved = p->gram_force;
+  p->gram_force = path;
+  int rc = ob_boot_run_device(p, seed, first_rep, n_reps, OB_REF_GROUP_A, d_rows, d_ok, nullptr);
+  p->gram_force = saved;
+  if (rc == OB_OK) rc = ob::engine_collect(p);
+  if (rc == OB_OK && hipMemcpy(gram, p->d_gram, sizeof(double) * 2 * (size_t)n_reps * p->e_pad,
+                               hipMemcpyDeviceToHost) != hipSuccess)
+    rc = ob::fail(OB_E_HIP, "copy of the Gram failed");
+  (void)hipFree(d_rows);
+  (void)hipFree(d_ok);
+  return rc;
 }
 
 int ob_panel_sync(ob_panel* p) {

@@ -79,6 +79,12 @@ struct ob_panel {
   size_t cap_shard = 0, cap_gather = 0, cap_shard_ok = 0, cap_gather_ok = 0;
   hipEvent_t gather_ev[2] = {nullptr, nullptr};
   bool gather_timed = false;
+  // integer-sliced Gram (ob_gram_i8.hip): digit images per group, pair exponents per chunk
+  int oz_state = 0;  // 0 not built, 1 ready, -1 unavailable (the f64 MFMA Gram is used)
+  int gram_force = 0;  // 0: i8 when available; 1: f64 MFMA Gram; 2: i8 (ob_debug_gram, OB_GRAM_PATH)
+  int oz_n_ct = 0;
+  void* d_oz_b[2] = {nullptr, nullptr};
+  int32_t* d_oz_pexp = nullptr;
   std::vector<hipEvent_t> seg_events;  // 6 per segment of the last boot run
   ob_timing timing = {};
   bool timing_pending = false;
@@ -93,4 +99,8 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
 int engine_collect(ob_panel* p);
 int engine_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_reps, hipStream_t s,
                   uint32_t* nb_rep, uint32_t* rep_pad);
+// ob_gram_i8.hip
+int oz_prepare(ob_panel* p, const std::vector<uint32_t>& chunks);
+int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t* counts, uint32_t nb_rep,
+            uint32_t rep_pad, uint32_t n_reps, double* partial, hipStream_t s);
 }  // namespace ob

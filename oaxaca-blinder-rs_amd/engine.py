@@ -146,6 +146,14 @@ class Panel:
                                         rc.ctypes.data_as(C.POINTER(C.c_uint8))))
         return l1, rc
 
+    def debug_gram(self, seed: int, first_rep: int, n_reps: int, path: int = 0):
+        """Reduced extended Grams [n_reps, 2, e_pad] (ob_debug_gram): path 1 = f64 MFMA,
+        2 = exact integer-sliced i8 MFMA, 0 = the engine's default."""
+        e_pad = -(-((self.k + self.n_y) * (self.k + self.n_y + 1) // 2) // 16) * 16
+        g = np.empty((n_reps, 2, e_pad))
+        N.check(N.lib().ob_debug_gram(self._h, int(path), seed & ((1 << 64) - 1), first_rep, n_reps, _dp(g)))
+        return g
+
     def sync(self):
         N.check(N.lib().ob_panel_sync(self._h))
 
