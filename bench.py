@@ -30,6 +30,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 F64_MFMA_PEAK_TFLOPS = 78.6  # MI355X dense FP64 matrix peak (v_mfma_f64_16x16x4_f64, 2.4 GHz)
+I8_MFMA_PEAK_TOPS = 5000.0  # dense I8 MFMA: 2x the ~2.5 PF dense BF16 rate per clock (MI355X_MICROARCH.md, Matrix cores)
+OZ_SLICES = 8  # ob_gram_i8.hip: 7-bit digits per pair product
+OZ_PAIRS_PER_TILE = 32
 HBM_PEAK_GBPS = 8000.0
 
 
@@ -340,9 +343,10 @@ def cpu_baseline_heckman(frame, names, zs, target_s, threads):
                       f"{threads} threads, {dt:.1f} s"}
 
 
-def load_traffic(rows, preds, reps):
-    """HBM bytes per ob_gram_kernel launch from the committed rocprofv3 PMC summary."""
-    path = os.path.join(ROOT, "profiles", "pmc_gram.json")
+def load_traffic(rows, preds, reps, gram_path=1):
+    """HBM bytes per Gram launch (ob_gram_kernel, or oz_gram_kernel for the i8 path) from the
+    committed rocprofv3 PMC summary."""
+    path = os.path.join(ROOT, "profiles", "pmc_gram.json" if gram_path == 1 else "pmc_gram_i8.json")
     try:
         with open(path) as f:
             j = json.load(f)
@@ -461,11 +465,13 @@ def main():
     sums = {"gram_ms": 0.0, "level1_ms": 0.0, "counts_ms": 0.0, "reduce_ms": 0.0, "solve_ms": 0.0, "gather_ms": 0.0}
     launches = 0
     stats = None
+    gram_path = 1
     for i in range(args.steps):
         stats, tm = step(args.warmup + i)
         for k_ in sums:
             sums[k_] += tm[k_]
         launches += tm["gram_launches"]
+        gram_path = tm["gram_path"]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -482,7 +488,25 @@ def main():
         bytes_rep = args.rows * (args.preds + (2 if weighted else 1)) * 8.0
         reps_per_launch = min(per_rank, 16384) if launches else 0
         achieved = flops_rep * reps_per_launch / (gram_launch_ms * 1e-3) / 1e12 if gram_launch_ms else 0.0
-        traffic = load_traffic(args.rows, args.preds, per_rank) if not taus else None
+        traffic = load_traffic(args.rows, args.preds, per_rank, gram_path) if not taus else None
+        if gram_path == 2:
+            # exact integer-sliced Gram (ob_gram_i8.hip): the algorithmic work is one i8 multiply-add per
+            # (replicate, row, live pair, 7-bit digit); the MFMA work pads pairs to 32-wide column tiles
+            pairs = (k + ny) * (k + ny + 1) // 2
+            ops_rep = 2.0 * args.rows * pairs * OZ_SLICES
+            ops_issued = 2.0 * args.rows * (-(-pairs // OZ_PAIRS_PER_TILE) * OZ_PAIRS_PER_TILE) * OZ_SLICES
+            i8_tops = ops_rep * reps_per_launch / (gram_launch_ms * 1e-3) / 1e12 if gram_launch_ms else 0.0
+            roof = {"bound": "mfma", "achieved": i8_tops, "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS (i8)",
+                    "frac": i8_tops / I8_MFMA_PEAK_TOPS, "traffic": traffic, "kernel": "oz_gram_kernel",
+                    "avg_launch_ms": gram_launch_ms, "i8_ops_per_replicate": ops_rep,
+                    "i8_ops_issued_per_replicate": ops_issued,
+                    "f64_equivalent_tflops": achieved, "f64_flops_per_replicate": flops_rep,
+                    "f64_equivalent_frac_of_f64_mfma_peak": achieved / F64_MFMA_PEAK_TFLOPS}
+        else:
+            roof = {"bound": "mfma", "achieved": achieved, "peak": F64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                    "frac": achieved / F64_MFMA_PEAK_TFLOPS, "traffic": traffic,
+                    "kernel": "ob_gram_kernel", "avg_launch_ms": gram_launch_ms,
+                    "flops_per_replicate": flops_rep}
         mode = "strong" if args.strong else "weak"
         out = {
             "metric": "bootstrap replicates/sec on 1M-row×20-pred panel at 1/2/4/8 MI355X" if not taus else
@@ -504,10 +528,8 @@ def main():
                        "rows": args.rows, "predictors": args.preds, "weighted": weighted,
                        "replicates_per_step": total, "replicates_per_gpu_per_step": per_rank,
                        "parallelism": f"replicates sharded x{world}, engine RCCL all-gather (ob_boot_run_sharded_device)"},
-            "roofline": {"bound": "mfma", "achieved": achieved, "peak": F64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / F64_MFMA_PEAK_TFLOPS, "traffic": traffic,
-                         "kernel": "ob_gram_kernel", "avg_launch_ms": gram_launch_ms,
-                         "flops_per_replicate": flops_rep},
+            "roofline": roof,
+            "gram_path": "i8 MFMA, exact 8 x 7-bit digit slices (f64-equivalent)" if gram_path == 2 else "f64 MFMA",
             "gather_equivalent": {"algorithmic_bytes_per_replicate": bytes_rep,
                                   "GBps": bytes_rep * value / world / 1e9,
                                   "frac_of_hbm_peak": bytes_rep * value / world / 1e9 / HBM_PEAK_GBPS},

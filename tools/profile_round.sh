@@ -2,9 +2,10 @@
 # Round profile of the headline bench (run on the GPU box from the repo root):
 #   bench JSON, rocprofv3 kernel-trace stats, FETCH_SIZE and WRITE_SIZE passes (separate, per
 #   MI355X_MICROARCH.md), and a GRBM_GUI_ACTIVE + MFMA-busy pass for the effective clock.
-# usage: [SKIP_BENCH=1] bash tools/profile_round.sh TAG   -> gpurun_out/TAG_*
+# usage: [SKIP_BENCH=1] [KERNEL=oz_gram_kernel] bash tools/profile_round.sh TAG   -> gpurun_out/TAG_*
 set -euo pipefail
 TAG=${1:-rXX}
+KERNEL=${KERNEL:-oz_gram_kernel}
 OUT=$PWD/gpurun_out
 mkdir -p "$OUT"
 REPO=$PWD
@@ -22,7 +23,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BU
   -d "$OUT/${TAG}_clock" -o run -- \
   python3 "$REPO/bench.py" --steps 1 --warmup 0 --cpu-seconds 0 > "$OUT/${TAG}_clock.log" 2>&1
 cd "$REPO"
-python tools/pmc_summary.py "$OUT/${TAG}_fetch" "$OUT/${TAG}_write" 1000000 20 10000 "$OUT/${TAG}_pmc_gram.json"
-python tools/pmc_clock.py "$OUT/${TAG}_clock" > "$OUT/${TAG}_clock_mfma.txt"
+python tools/pmc_summary.py "$OUT/${TAG}_fetch" "$OUT/${TAG}_write" 1000000 20 10000 "$OUT/${TAG}_pmc_gram.json" "$KERNEL"
+python tools/pmc_clock.py "$OUT/${TAG}_clock" "$KERNEL" > "$OUT/${TAG}_clock_mfma.txt"
 cat "$OUT/${TAG}_pmc_gram.json" "$OUT/${TAG}_clock_mfma.txt"
 find "$OUT/${TAG}_stats" -name '*kernel_stats.csv' -exec cat {} \;
