@@ -4,28 +4,31 @@
 //   G_r[e] = sum_i c_{r,i} P_i[e],   P_i[e] = v_i[a(e)] v_i[b(e)],  v = sqrt(w) [1, x, y]
 // (the reference's own sqrt(w) scaling, ols.rs:68-78; X^T W X, X^T W y, sum w and the weighted
 // sums of estimation.rs:56-71 are all entries of G). Counts are small integers, so the
-// resample weighting is exact in int8; the pair products are written once per panel as S = 8
-// fixed-point digits of 7 bits each (Ozaki-style splitting) relative to a per-(chunk, pair)
-// power of two 2^E > max |P|:
-//     P = sign * sum_s d_s 2^(E - 7 (s + 1)),   d_s in [0, 127]      (56 bits; |error| <= 2^(E-57))
-// and  sum_i c_i P_i = sum_s 2^(E - 7 (s + 1)) sum_i c_i (sign d_s)_i,  each inner sum an exact
-// int32 (|c| <= 127, sum_i c_i <= n_g, so |sum| <= 127 n_g < 2^31). The slices meet in int64 and
-// one f64 rounding per chunk partial. The representation error is at most 2^-57 of the chunk's
-// max |P| per row, below f64 summation error, so the Gram equals the f64 MFMA Gram to ~1e-15
-// relative (tests/test_gpu_gram_i8.py holds it to 1e-12).
+// resample weighting is exact in int8; the pair products are written once per panel as S = 7
+// balanced 8-bit digits (Ozaki-style splitting) of a 54-bit fixed-point value relative to the
+// per-(chunk, pair) power of two 2^E with 2^(E-1) <= max |P| < 2^E:
+//     m = rint(P 2^(54-E)),  |m| <= 2^54,   m = sum_s d_s 2^(8 (6 - s)),  d_s in [-128, 127]
+// (|d_0| <= 64), so |P - m 2^(E-54)| <= 2^(E-55) <= 2^-54 max |P| -- finer than f64's own
+// rounding of the chunk's largest product. Then
+//     sum_i c_i P_i = 2^(E-54) sum_s 2^(8 (6 - s)) sum_i c_i d_{s,i},
+// each inner sum an exact int32 (|c| <= 127, |d| <= 128, sum_i c_i <= n_g <= 10,485,760, so
+// |sum| < 2^31). The slices meet in int64, two f64 roundings per chunk partial, so the Gram
+// equals the f64 MFMA Gram to ~1e-15 relative (tests/test_gpu_gram_i8.py holds it to 1e-12).
 //
-// v_mfma_i32_32x32x32_i8 runs 64x the f64 MFMA rate (MI355X_MICROARCH.md, Matrix cores): 8
-// slices cost 8x the f64 multiply count and still leave 8x headroom. Layouts (HBM, built once):
+// v_mfma_i32_32x32x32_i8 issues in 32 cycles like v_mfma_f32_32x32x16_bf16 (MI355X_MICROARCH.md,
+// Matrix cores): 64x the f64 MFMA rate, so 7 slices cost 7x the f64 multiply count and still
+// leave 9x headroom. Layouts (HBM, built once per panel):
 //   B (digits): per group [sub-tile 64 rows][col tile: 32 pairs][slice][k-half 32 rows][lane][16 B]
 //               -- lane l holds pair (l & 31), rows 16 (l >> 5) + j of the k-half: the B fragment
-//               of 32x32x32_i8 (probed: tools/mfma_i8_probe.hip), one 16 KB DMA per sub-tile.
+//               of 32x32x32_i8 (probed: tools/mfma_i8_probe.hip), one 14 KB DMA per sub-tile.
 //   A (counts): ob_count_kernel<true> writes [tile][64-rep batch][sub-tile][k-half][rep half][lane][16 B]
 //               -- lane l holds replicate (l & 31) of the half, the same rows: the A fragment.
-// Kernel: 8 waves (two per SIMD), one block per CU, block tile 256 replicates x 32 pairs x S
-// slices; wave w owns replicate batch 4 rt + (w & 3) (2 x 32 replicates) and slice half w >> 2
-// (S/2 x 32 columns): 8 accumulators of 32 x 32 i32. Per 64-row sub-tile a wave issues S x 2
-// MFMAs (A from HBM straight into registers, prefetched one sub-tile ahead; B from the block's
-// LDS copy, DMA'd one sub-tile ahead). The two slice halves meet through LDS at the end.
+// Kernel: 8 waves (two per SIMD), one block per CU, block tile 256 replicates x 32 pairs x 7
+// slices; wave w owns replicate batch w & 3 (2 x 32 replicates) and slice group w >> 2 (slices
+// 0-3 or 4-6): 8 or 6 accumulators of 32 x 32 i32. Both operands arrive in LDS by DMA, four
+// sub-tiles ahead. The loop runs in half-steps (sub-tile, k-half): the fragments of the next
+// half-step are read from LDS while the MFMAs of this one issue, and one barrier per sub-tile
+// (between its two halves) publishes the next sub-tile and frees the oldest ring stage.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -42,9 +45,11 @@ typedef int ob_v16i __attribute__((ext_vector_type(16)));
 
 namespace {
 
-constexpr int kS = 8;                  // 7-bit digits per pair product (56 bits)
+constexpr int kS = 7;                  // balanced 8-bit digits per pair product (54-bit fixed point)
+constexpr int kFracBits = 54;          // m = rint(P 2^(kFracBits - E))
 constexpr int kPairsPerTile = 32;      // pairs per column tile (one 32-wide MFMA column block)
-constexpr int kSubUnits = kS * 2 * 64; // 16-byte units of one (sub-tile, column tile) B image
+constexpr int kSubUnits = kS * 2 * 64; // 16-byte units of one (sub-tile, column tile) B image (14 KB)
+constexpr int kSlo = 4;                // slices of slice group 0 (waves 0-3); group 1 has kS - kSlo
 
 #define OZ_HIP(expr)                                                                                  \
   do {                                                                                                \
@@ -62,12 +67,30 @@ __device__ __forceinline__ double oz_v(const double* cols, int64_t ld, int nxy, 
   return c == 0 ? 1.0 : cols[(size_t)(c - 1) * ld + row];
 }
 
-// Per (chunk, column): the exponent e with max |v_c| < 2^e over the chunk's rows (0 if all zero).
-__global__ __launch_bounds__(256) void oz_colexp_kernel(const double* cols0, const double* cols1, int64_t ld0,
-                                                        int64_t ld1, uint32_t n0, uint32_t n1, int nxy, int weighted,
-                                                        const uint32_t* chunks, int k1, int32_t* colexp) {
+__device__ __forceinline__ void oz_pair_cols(int pair, int k1, int* a, int* b) {
+  int aa = 0, rem = pair;
+  while (rem >= k1 - aa) {
+    rem -= k1 - aa;
+    ++aa;
+  }
+  *a = aa;
+  *b = aa + rem;
+}
+
+// Per (chunk, pair): the exponent E with 2^(E-1) <= max |P| < 2^E over the chunk's rows (0 if all
+// zero or a padding pair). Same product expression as oz_digits_kernel.
+__global__ __launch_bounds__(256) void oz_pairexp_kernel(const double* cols0, const double* cols1, int64_t ld0,
+                                                         int64_t ld1, uint32_t n0, uint32_t n1, int nxy, int weighted,
+                                                         const uint32_t* chunks, int k1, int e, int n_pairs_pad,
+                                                         int32_t* pexp) {
   __shared__ double red[256];
-  const int chunk = blockIdx.x, c = blockIdx.y, tid = threadIdx.x;
+  const int chunk = blockIdx.x, pair = blockIdx.y, tid = threadIdx.x;
+  if (pair >= e) {
+    if (tid == 0) pexp[chunk * n_pairs_pad + pair] = 0;
+    return;
+  }
+  int ca, cb;
+  oz_pair_cols(pair, k1, &ca, &cb);
   const uint32_t g = chunks[3 * chunk];
   const double* cols = g ? cols1 : cols0;
   const int64_t ld = g ? ld1 : ld0;
@@ -75,7 +98,8 @@ __global__ __launch_bounds__(256) void oz_colexp_kernel(const double* cols0, con
   const size_t r0 = (size_t)chunks[3 * chunk + 1] * OB_TILE_ROWS;
   const size_t r1 = std::min<size_t>((size_t)chunks[3 * chunk + 2] * OB_TILE_ROWS, n);
   double m = 0.0;
-  for (size_t r = r0 + tid; r < r1; r += 256) m = fmax(m, fabs(oz_v(cols, ld, nxy, weighted, r, c)));
+  for (size_t r = r0 + tid; r < r1; r += 256)
+    m = fmax(m, fabs(oz_v(cols, ld, nxy, weighted, r, ca) * oz_v(cols, ld, nxy, weighted, r, cb)));
   red[tid] = m;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
@@ -83,68 +107,43 @@ __global__ __launch_bounds__(256) void oz_colexp_kernel(const double* cols0, con
     __syncthreads();
   }
   if (tid == 0) {
-    int e = 0;
-    if (red[0] > 0.0) (void)frexp(red[0], &e);  // red[0] = f 2^e, f in [0.5, 1): max < 2^e
-    colexp[chunk * k1 + c] = e;
+    int ex = 0;
+    if (red[0] > 0.0) (void)frexp(red[0], &ex);  // red[0] = f 2^ex, f in [0.5, 1)
+    pexp[chunk * n_pairs_pad + pair] = ex;
   }
 }
 
-// Pair exponents E[chunk][pair] = e_a + e_b (max |v_a v_b| <= max|v_a| max|v_b| < 2^(e_a + e_b)).
-__global__ void oz_pairexp_kernel(const int32_t* colexp, int k1, int e, int n_pairs_pad, int n_chunks, int32_t* pexp) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n_chunks * n_pairs_pad) return;
-  const int chunk = i / n_pairs_pad, q = i % n_pairs_pad;
-  int v = 0;
-  if (q < e) {
-    int a = 0, rem = q;
-    while (rem >= k1 - a) {
-      rem -= k1 - a;
-      ++a;
-    }
-    v = colexp[chunk * k1 + a] + colexp[chunk * k1 + a + rem];
-  }
-  pexp[i] = v;
-}
-
-// B digits of one group: grid (sub-tile, column tile), 256 threads = (slice half, k-half, lane).
+// B digits of one group: grid (sub-tile, column tile), 256 threads = (slice group, k-half, lane).
 __global__ __launch_bounds__(256) void oz_digits_kernel(const double* cols, int64_t ld, uint32_t n, int nxy,
                                                         int weighted, int k1, int e, int n_ct, int n_pairs_pad,
                                                         const int32_t* tile_chunk, const int32_t* pexp,
                                                         ob_v4i* B) {
   const uint32_t sub = blockIdx.x;
-  const int ct = blockIdx.y, t = threadIdx.x, lane = t & 63, k2 = (t >> 6) & 1, half = t >> 7;
+  const int ct = blockIdx.y, t = threadIdx.x, lane = t & 63, k2 = (t >> 6) & 1, grp = t >> 7;
   const int pair = ct * kPairsPerTile + (lane & 31);
   int a = 0, b = 0;
   const bool live = pair < e;
-  if (live) {
-    int rem = pair;
-    while (rem >= k1 - a) {
-      rem -= k1 - a;
-      ++a;
-    }
-    b = a + rem;
-  }
+  if (live) oz_pair_cols(pair, k1, &a, &b);
   const int E = live ? pexp[tile_chunk[sub >> 2] * n_pairs_pad + pair] : 0;
-  long long mag[16];
-  bool neg[16];
+  int8_t dig[16][kS];
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
     const size_t row = (size_t)sub * 64 + k2 * 32 + 16 * (lane >> 5) + j;
     double P = 0.0;
     if (live && row < n) P = oz_v(cols, ld, nxy, weighted, row, a) * oz_v(cols, ld, nxy, weighted, row, b);
-    const double m = rint(ldexp(P, 7 * kS - E));  // |m| < 2^56: exact, already integral when >= 2^53
-    neg[j] = m < 0.0;
-    mag[j] = (long long)fabs(m);
+    long long m = (long long)rint(ldexp(P, kFracBits - E));  // |m| <= 2^54: exact
+#pragma unroll
+    for (int sl = kS - 1; sl >= 0; --sl) {  // balanced digits, least significant first
+      const int8_t d = (int8_t)(m & 0xff);
+      dig[j][sl] = d;
+      m = (m - d) >> 8;
+    }
   }
-  for (int sl = half * (kS / 2); sl < (half + 1) * (kS / 2); ++sl) {
-    const int sh = 7 * (kS - 1 - sl);
+  const int sl0 = grp ? kSlo : 0, sl1 = grp ? kS : kSlo;
+  for (int sl = sl0; sl < sl1; ++sl) {
     uint32_t w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int d = (int)((mag[j] >> sh) & 127);
-      const uint32_t byte = (uint32_t)(uint8_t)(int8_t)(neg[j] ? -d : d);
-      w[j >> 2] |= byte << (8 * (j & 3));
-    }
+    for (int j = 0; j < 16; ++j) w[j >> 2] |= (uint32_t)(uint8_t)dig[j][sl] << (8 * (j & 3));
     B[(((size_t)sub * n_ct + ct) * kS + sl) * 2 * 64 + k2 * 64 + lane] = (ob_v4i){(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
   }
 }
@@ -160,37 +159,52 @@ struct OzArgs {
   int n_ct, e_pad, n_pairs_pad;
 };
 
-__device__ __forceinline__ void oz_lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-constexpr int kWaves = 8;                        // 2 per SIMD: (replicate batch, slice half)
-constexpr int kHalf = kS / 2;                      // slices per wave
-constexpr int kDist = 3;                           // sub-tiles in flight ahead of the MFMAs
-constexpr int kNbuf = kDist + 1;                   // B ring in LDS
-static_assert(kNbuf == 4, "the main loop below is unrolled over a 4-stage ring");
-constexpr int kDmaPerWave = kSubUnits / (64 * kWaves);        // 1 KB B-DMA instructions per wave and sub-tile
-constexpr int kAUnits = 4 * 256;                               // 16-byte units of a sub-tile's A (4 batches x 4 KB)
-constexpr int kADmaPerWave = 2;                                // each wave DMAs half of its batch's 4 KB
-constexpr size_t kLdsB = kNbuf * (size_t)kSubUnits * 16;      // B ring (64 KB)
+constexpr int kWaves = 8;                         // 2 per SIMD: (replicate batch, slice group)
+constexpr int kNbuf = 4;                          // LDS ring stages (sub-tiles)
+constexpr int kBDma = (kSubUnits + 64 * kWaves - 1) / (64 * kWaves);  // B DMA instructions per wave (<=)
+constexpr int kBDmaTotal = kSubUnits / 64;        // 14 per sub-tile, spread over the waves
+constexpr int kAUnits = 4 * 256;                  // 16-byte units of a sub-tile's A (4 batches x 4 KB)
+constexpr int kADmaPerWave = 2;                   // each wave DMAs one k-half of its batch's 4 KB
+constexpr size_t kLdsB = kNbuf * (size_t)kSubUnits * 16;      // B ring (56 KB)
 constexpr size_t kLdsA = kNbuf * (size_t)kAUnits * 16;        // A ring (64 KB)
-constexpr size_t kLdsX = 4 * 64 * (size_t)kPairsPerTile * 8;  // low-half exchange (64 KB, over the B ring)
-constexpr size_t kLdsBytes = (kLdsB > kLdsX ? kLdsB : kLdsX) + kLdsA;
+constexpr size_t kLdsX = 4 * 64 * (size_t)kPairsPerTile * 8;  // slice-group exchange (64 KB, over the rings)
+constexpr size_t kLdsBytes = (kLdsB + kLdsA > kLdsX ? kLdsB + kLdsA : kLdsX);
+static_assert(kBDma == 2 && kBDmaTotal == 14, "B DMA split below assumes 14 instructions over 8 waves");
 
-template <int N>
-struct IC {
-  static constexpr int value = N;
-};
+// One 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4: lane l lands at lds + 16 l). Issued from
+// inline asm so the compiler does not track it: its wait model counts LDS-DMA against the LDS
+// counter and would then drain every fragment read (lgkmcnt(0)) before the next MFMAs. The
+// kernel waits for these loads itself (counted vmcnt before each publishing barrier).
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"  // m0 is reserved, and this asm does overwrite it
+__device__ __forceinline__ void oz_dma16(const void* src, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(lds) : "memory", "m0");
+}
+#pragma clang diagnostic pop
 
-// Both operands arrive by LDS-DMA (global_load_lds), kDist sub-tiles ahead: the compiler does not
-// track those loads in registers, so it inserts no vmcnt(0) before the MFMAs; the only waits are
-// the explicit vmcnt(n) + barrier that publish sub-tile s + 1.
-__global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const size_t a_off = kLdsB > kLdsX ? kLdsB : kLdsX;
-  const ob_v4i* bs = reinterpret_cast<const ob_v4i*>(smem);          // [kNbuf][kSubUnits]
-  const ob_v4i* as = reinterpret_cast<const ob_v4i*>(smem + a_off);  // [kNbuf][4 batches][256]
-  __attribute__((address_space(3))) unsigned char* lds3 = (__attribute__((address_space(3))) unsigned char*)smem;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wb = wave & 3, half = wave >> 2;  // replicate batch in the tile, slice half
+__device__ __forceinline__ void oz_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int NQ>
+__device__ __forceinline__ void oz_mfmas(ob_v16i (&acc)[2][kSlo], const ob_v4i (&af)[2], const ob_v4i (&bf)[kSlo]) {
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    acc[0][q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[0], bf[q], acc[0][q], 0, 0, 0);
+    acc[1][q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[1], bf[q], acc[1][q], 0, 0, 0);
+  }
+}
+
+// Block: (chunk, replicate tile of 4 batches, column tile). NQ = slices of this wave's group, PER =
+// its DMA instructions per sub-tile, LIVE = its replicate batch exists. DIAG (OB_GRAM_DIAG, timing
+// ablations only, wrong results): 2 no MFMAs, 4 no sub-tile DMA after the prologue. All three are wave-uniform
+// template constants, so the loop has no divergent control flow and the compiler's LDS-counter
+// bookkeeping stays exact (a wait only for the fragments an MFMA consumes).
+template <int NQ, int PER, bool LIVE, int DIAG>
+__device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* smem, int wave) {
+  const ob_v4i* bs = reinterpret_cast<const ob_v4i*>(smem);           // [kNbuf][kSubUnits]
+  const ob_v4i* as = reinterpret_cast<const ob_v4i*>(smem + kLdsB);   // [kNbuf][4 batches][256]
+  const int lane = threadIdx.x & 63;
+  const int wb = wave & 3, grp = wave >> 2;  // replicate batch in the tile, slice group
+  const int slo = grp ? kSlo : 0;
   // XCD-aware remap (as ob_gram_kernel's map_work): consecutive work items -- the column tiles of
   // one replicate tile, then the replicate tiles of one chunk -- share an XCD's L2.
   const uint32_t nwg = gridDim.x, bid = blockIdx.x;
@@ -205,89 +219,83 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
   const uint32_t s1 = min(a.chunks[3 * chunk + 2] * 4u, (n + 63u) >> 6);
   const ob_v4i* Bg = g ? a.B1 : a.B0;
   const uint32_t batch = rt * 4u + (uint32_t)wb;
-  const bool live = batch < a.nb_rep;
+  constexpr int NB = PER - (LIVE ? kADmaPerWave : 0);  // B pieces: waves 0-5 two, 6-7 one
 
   auto dma = [&](int buf, uint32_t s) {
-    const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct) * kSubUnits;  // B: 16 KB
+    const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct) * kSubUnits;  // B: 14 KB
 #pragma unroll
-    for (int t = 0; t < kDmaPerWave; ++t) {
-      const int u = (t * kWaves + wave) * 64;
-      __builtin_amdgcn_global_load_lds(src + u + lane,
-                                       (__attribute__((address_space(3))) void*)(lds3 + (size_t)(buf * kSubUnits + u) * 16),
-                                       16, 0, 0);
+    for (int t = 0; t < NB; ++t) {
+      const int piece = t * kWaves + wave;
+      oz_dma16(src + piece * 64 + lane, (uint32_t)(buf * kSubUnits + piece * 64) * 16u);
     }
-    if (live) {  // A: this wave's half of its batch's 4 KB
+    if constexpr (LIVE) {  // A: one k-half of this wave's batch (the two slice groups split the 4 KB)
       const ob_v4i* asrc = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256;
 #pragma unroll
       for (int t = 0; t < kADmaPerWave; ++t) {
-        const int u = (half * kADmaPerWave + t) * 64;
-        __builtin_amdgcn_global_load_lds(
-            asrc + u + lane,
-            (__attribute__((address_space(3))) void*)(lds3 + a_off + (size_t)(buf * kAUnits + wb * 256 + u) * 16), 16, 0,
-            0);
+        const int u = (grp * kADmaPerWave + t) * 64;
+        oz_dma16(asrc + u + lane, (uint32_t)(kLdsB + (size_t)(buf * kAUnits + wb * 256 + u) * 16));
       }
     }
   };
-  auto wait_ahead = [&]() {  // everything but the kDist - 1 newest sub-tiles has landed
-    if (live) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kDist - 1) * (kDmaPerWave + kADmaPerWave)) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((kDist - 1) * kDmaPerWave) : "memory");
+  // fragments of half-step (sub-tile in ring stage buf, k-half k2)
+  auto read = [&](int buf, int k2, ob_v4i (&af)[2], ob_v4i (&bf)[kSlo]) {
+    const ob_v4i* ab = as + buf * kAUnits + wb * 256 + k2 * 128 + lane;
+    af[0] = ab[0];
+    af[1] = ab[64];
+    const ob_v4i* bb = bs + buf * kSubUnits + (slo * 2 + k2) * 64 + lane;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) bf[q] = bb[q * 128];
   };
 
-  ob_v16i acc[2][kHalf];
+  ob_v16i acc[2][kSlo];
 #pragma unroll
   for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-    for (int q = 0; q < kHalf; ++q) acc[rb][q] = (ob_v16i){};
-  // prologue: sub-tiles s0 .. s0 + kDist - 1 in flight; publish s0
+    for (int q = 0; q < kSlo; ++q) acc[rb][q] = (ob_v16i){};
+  // prologue: sub-tiles s0 .. s0 + 3 in flight; publish s0
 #pragma unroll
-  for (int j = 0; j < kDist; ++j)
+  for (int j = 0; j < kNbuf; ++j)
     if (s0 + j < s1) dma(j, s0 + j);
-  if (s0 + kDist <= s1) wait_ahead();
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  auto step = [&](uint32_t s, auto J) {
-    constexpr int j = decltype(J)::value;
-    const uint32_t sp = s + kDist;
-    const bool issue = sp < s1;
-    if (issue) dma((j + kDist) % kNbuf, sp);  // into the stage freed by s - 1 (every wave is past its barrier)
-    if (live) {
-      const ob_v4i* bb = bs + j * kSubUnits + half * kHalf * 2 * 64 + lane;
-      const ob_v4i* ab = as + j * kAUnits + wb * 256 + lane;
-      ob_v4i af[2][2], bf[2][kHalf];  // every fragment of the sub-tile is read before the MFMAs
-#pragma unroll
-      for (int k2 = 0; k2 < 2; ++k2) {
-        af[k2][0] = ab[(k2 * 2 + 0) * 64];
-        af[k2][1] = ab[(k2 * 2 + 1) * 64];
-#pragma unroll
-        for (int q = 0; q < kHalf; ++q) bf[k2][q] = bb[(q * 2 + k2) * 64];
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int k2 = 0; k2 < 2; ++k2)
-#pragma unroll
-        for (int q = 0; q < kHalf; ++q) {
-          acc[0][q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[k2][0], bf[k2][q], acc[0][q], 0, 0, 0);
-          acc[1][q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[k2][1], bf[k2][q], acc[1][q], 0, 0, 0);
-        }
-    }
-    // sub-tile s + 1 must have landed; the kDist - 1 later ones may stay in flight
-    if (issue) wait_ahead();
+  {
+    const uint32_t left = s1 - s0;  // >= 1
+    if (left >= 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PER) : "memory");
+    else if (left == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+    else if (left == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    oz_lds_barrier();
-  };
-  for (uint32_t s = s0; s < s1; s += kNbuf) {
-    step(s, IC<0>{});
-    if (s + 1 < s1) step(s + 1, IC<1>{});
-    if (s + 2 < s1) step(s + 2, IC<2>{});
-    if (s + 3 < s1) step(s + 3, IC<3>{});
   }
-  // slices -> f64: this wave's 4 digits meet exactly in int64 (< 2^52), one ldexp each; the low
-  // half goes through LDS to its high-half partner, which adds (one rounding) and stores.
+  __syncthreads();
+  ob_v4i fa0[2], fb0[kSlo], fa1[2], fb1[kSlo];
+  if constexpr (LIVE) read(0, 0, fa0, fb0);
+
+  // Half-step (s, 0): read (s, 1); MFMAs on (s, 0). Barrier B_s: sub-tile s + 1 landed (own DMAs,
+  // then everyone's), every read of sub-tile s done. Refill stage s with s + 4. Half-step (s, 1):
+  // read (s + 1, 0) (after the last sub-tile: a stale stage, never used); MFMAs on (s, 1).
+  for (uint32_t s = s0; s < s1; ++s) {
+    const int buf = (int)((s - s0) & (kNbuf - 1));
+    if constexpr (LIVE) {
+      read(buf, 1, fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(DIAG & 2)) oz_mfmas<NQ>(acc, fa0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const uint32_t ahead = (DIAG & 4) ? 0u : s1 - 1 - s;  // sub-tiles after s
+    if (ahead >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");  // s + 2, s + 3 in flight
+    else if (ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    oz_barrier();
+    if (!(DIAG & 4) && s + kNbuf < s1) dma(buf, s + kNbuf);
+    if constexpr (LIVE) {
+      read((buf + 1) & (kNbuf - 1), 0, fa0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(DIAG & 2)) oz_mfmas<NQ>(acc, fa1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  // slices -> f64: this wave's digits meet exactly in int64, one ldexp each; group 1 goes through
+  // LDS to its group-0 partner, which adds (one rounding) and stores.
   const int pair = ct * kPairsPerTile + (lane & 31);
   const int E = a.pexp[chunk * a.n_pairs_pad + min(pair, a.n_pairs_pad - 1)];
-  const int shift = E - 7 * kS + (half ? 0 : 7 * kHalf);
-  double* xch = reinterpret_cast<double*>(smem);  // [batch in tile][64 reps][32 pairs]
+  const int shift = E - kFracBits + 8 * (kS - slo - NQ);  // weight of this group's last slice
   double v[2][16];
 #pragma unroll
   for (int rb = 0; rb < 2; ++rb)
@@ -295,10 +303,12 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
     for (int r = 0; r < 16; ++r) {
       long long part = 0;
 #pragma unroll
-      for (int q = 0; q < kHalf; ++q) part = part * 128 + acc[rb][q][r];
+      for (int q = 0; q < NQ; ++q) part = part * 256 + acc[rb][q][r];
       v[rb][r] = ldexp((double)part, shift);
     }
-  if (half) {
+  __syncthreads();  // every wave is done with the rings: the exchange overlays them
+  double* xch = reinterpret_cast<double*>(smem);  // [batch in tile][64 reps][32 pairs]
+  if (grp) {
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
@@ -308,7 +318,7 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
       }
   }
   __syncthreads();
-  if (half || !live || pair >= a.e_pad) return;
+  if (grp || !LIVE || pair >= a.e_pad) return;
 #pragma unroll
   for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
@@ -318,6 +328,29 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
       const double val = v[rb][r] + xch[(wb * 64 + rl) * kPairsPerTile + (lane & 31)];
       if (rep < a.n_reps) a.partial[((size_t)chunk * a.rep_pad + rep) * a.e_pad + pair] = val;
     }
+}
+
+template <int DIAG>
+__global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // the replicate tile of this block (same map as the body) decides which batches exist
+  const uint32_t nwg = gridDim.x, bid = blockIdx.x;
+  const uint32_t xcd = bid & 7u, slot = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7u;
+  const uint32_t wi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const uint32_t rt = (wi / (uint32_t)a.n_ct) % a.n_rt;
+  const bool live = rt * 4u + (uint32_t)(wave & 3) < a.nb_rep;
+  // waves 0-3: slices 0-3, two B pieces; 4-5: slices 4-6, two B pieces; 6-7: slices 4-6, one piece
+  if (wave < 4) {
+    if (live) oz_gram_body<kSlo, 4, true, DIAG>(a, smem, wave);
+    else oz_gram_body<kSlo, 2, false, DIAG>(a, smem, wave);
+  } else if (wave < 6) {
+    if (live) oz_gram_body<kS - kSlo, 4, true, DIAG>(a, smem, wave);
+    else oz_gram_body<kS - kSlo, 2, false, DIAG>(a, smem, wave);
+  } else {
+    if (live) oz_gram_body<kS - kSlo, 3, true, DIAG>(a, smem, wave);
+    else oz_gram_body<kS - kSlo, 1, false, DIAG>(a, smem, wave);
+  }
 }
 
 }  // namespace
@@ -344,7 +377,7 @@ int oz_prepare(ob_panel* p, const std::vector<uint32_t>& chunks) {
   for (int g = 0; g < 2; ++g)
     OZ_HIP(hipMalloc(&p->d_oz_b[g], std::max<size_t>((size_t)(p->ld[g] >> 6) * n_ct * kSubUnits * 16, 16)));
   OZ_HIP(hipMalloc(&p->d_oz_pexp, sizeof(int32_t) * (size_t)n_chunks * npp));
-  int32_t *d_colexp = nullptr, *d_tc = nullptr;
+  int32_t* d_tc = nullptr;
   uint32_t* d_chunks = nullptr;
   int rc = OB_OK;
   do {
@@ -356,17 +389,12 @@ int oz_prepare(ob_panel* p, const std::vector<uint32_t>& chunks) {
       break;                                                                                             \
     }                                                                                                    \
   }
-    OZ_TRY(hipMalloc(&d_colexp, sizeof(int32_t) * (size_t)n_chunks * p->k1));
     OZ_TRY(hipMalloc(&d_chunks, sizeof(uint32_t) * chunks.size()));
     OZ_TRY(hipMemcpy(d_chunks, chunks.data(), sizeof(uint32_t) * chunks.size(), hipMemcpyHostToDevice));
     const int nxy = p->p + p->n_y;
-    hipLaunchKernelGGL(oz_colexp_kernel, dim3(n_chunks, p->k1), dim3(256), 0, 0, (const double*)p->d_cols[0],
+    hipLaunchKernelGGL(oz_pairexp_kernel, dim3(n_chunks, npp), dim3(256), 0, 0, (const double*)p->d_cols[0],
                        (const double*)p->d_cols[1], p->ld[0], p->ld[1], p->n[0], p->n[1], nxy, p->weighted,
-                       (const uint32_t*)d_chunks, p->k1, d_colexp);
-    OZ_TRY(hipGetLastError());
-    const int tot = n_chunks * npp;
-    hipLaunchKernelGGL(oz_pairexp_kernel, dim3((tot + 255) / 256), dim3(256), 0, 0, (const int32_t*)d_colexp, p->k1,
-                       p->e, npp, n_chunks, p->d_oz_pexp);
+                       (const uint32_t*)d_chunks, p->k1, p->e, npp, p->d_oz_pexp);
     OZ_TRY(hipGetLastError());
     for (int g = 0; g < 2 && rc == OB_OK; ++g) {
       const uint32_t nsub = (uint32_t)(p->ld[g] >> 6);
@@ -388,7 +416,6 @@ int oz_prepare(ob_panel* p, const std::vector<uint32_t>& chunks) {
     if (rc == OB_OK) OZ_TRY(hipDeviceSynchronize());
 #undef OZ_TRY
   } while (0);
-  (void)hipFree(d_colexp);
   (void)hipFree(d_tc);
   (void)hipFree(d_chunks);
   if (rc != OB_OK) return rc;
@@ -418,10 +445,23 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
   a.n_ct = p->oz_n_ct;
   a.e_pad = p->e_pad;
   a.n_pairs_pad = p->oz_n_ct * kPairsPerTile;
-  OZ_HIP(hipFuncSetAttribute((const void*)oz_gram_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes));
+  static const int diag = [] {
+    const char* e = getenv("OB_GRAM_DIAG");
+    return e ? atoi(e) & 6 : 0;
+  }();
   const uint32_t blocks = (uint32_t)n_chunks * a.n_rt * (uint32_t)a.n_ct;
-  hipLaunchKernelGGL(oz_gram_kernel, dim3(blocks), dim3(kWaves * 64), kLdsBytes, s, a);
-  OZ_HIP(hipGetLastError());
+  auto launch = [&](auto kern) -> hipError_t {
+    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(kWaves * 64), kLdsBytes, s, a);
+    return hipGetLastError();
+  };
+  switch (diag) {
+    case 2: OZ_HIP(launch(oz_gram_kernel<2>)); break;
+    case 4: OZ_HIP(launch(oz_gram_kernel<4>)); break;
+    case 6: OZ_HIP(launch(oz_gram_kernel<6>)); break;
+    default: OZ_HIP(launch(oz_gram_kernel<0>)); break;
+  }
   return OB_OK;
 }
 
