@@ -184,6 +184,11 @@ __device__ __forceinline__ void oz_dma16(const void* src, uint32_t lds) {
 
 __device__ __forceinline__ void oz_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+template <int N>
+struct IC {
+  static constexpr int value = N;
+};
+
 template <int NQ>
 __device__ __forceinline__ void oz_mfmas(ob_v16i (&acc)[2][kSlo], const ob_v4i (&af)[2], const ob_v4i (&bf)[kSlo]) {
 #pragma unroll
@@ -193,13 +198,16 @@ __device__ __forceinline__ void oz_mfmas(ob_v16i (&acc)[2][kSlo], const ob_v4i (
   }
 }
 
-// Block: (chunk, replicate tile of 4 batches, column tile). NQ = slices of this wave's group, PER =
-// its DMA instructions per sub-tile, LIVE = its replicate batch exists. DIAG (OB_GRAM_DIAG, timing
-// ablations only, wrong results): 2 no MFMAs, 4 no sub-tile DMA after the prologue. All three are wave-uniform
-// template constants, so the loop has no divergent control flow and the compiler's LDS-counter
-// bookkeeping stays exact (a wait only for the fragments an MFMA consumes).
-template <int NQ, int PER, bool LIVE, int DIAG>
+// Block: (chunk, replicate tile of 4 batches, column tile). NQ = slices of this wave's group, NB =
+// its B DMA pieces per sub-tile, LIVE = its replicate batch exists, AREG = its A fragments come
+// straight from HBM/L2 into registers (else through the LDS A ring). All are wave-uniform template
+// constants, so the loop has no divergent control flow and the compiler's LDS-counter bookkeeping
+// stays exact (a wait only for the fragments an MFMA consumes). DIAG (OB_GRAM_DIAG, timing
+// ablations only, wrong results): 2 no MFMAs, 4 no sub-tile loads after the prologue.
+template <int NQ, int NB, bool LIVE, bool AREG, int DIAG>
 __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* smem, int wave) {
+  constexpr int PA = LIVE ? (AREG ? 4 : kADmaPerWave) : 0;  // A instructions per sub-tile
+  constexpr int PER = NB + PA;                              // this wave's vector-memory ops per sub-tile
   const ob_v4i* bs = reinterpret_cast<const ob_v4i*>(smem);           // [kNbuf][kSubUnits]
   const ob_v4i* as = reinterpret_cast<const ob_v4i*>(smem + kLdsB);   // [kNbuf][4 batches][256]
   const int lane = threadIdx.x & 63;
@@ -219,8 +227,9 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   const uint32_t s1 = min(a.chunks[3 * chunk + 2] * 4u, (n + 63u) >> 6);
   const ob_v4i* Bg = g ? a.B1 : a.B0;
   const uint32_t batch = rt * 4u + (uint32_t)wb;
-  constexpr int NB = PER - (LIVE ? kADmaPerWave : 0);  // B pieces: waves 0-5 two, 6-7 one
-
+  auto asrc = [&](uint32_t s) {  // this wave's batch of sub-tile s: [k-half][rep half][lane]
+    return a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256;
+  };
   auto dma = [&](int buf, uint32_t s) {
     const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct) * kSubUnits;  // B: 14 KB
 #pragma unroll
@@ -228,20 +237,31 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
       const int piece = t * kWaves + wave;
       oz_dma16(src + piece * 64 + lane, (uint32_t)(buf * kSubUnits + piece * 64) * 16u);
     }
-    if constexpr (LIVE) {  // A: one k-half of this wave's batch (the two slice groups split the 4 KB)
-      const ob_v4i* asrc = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256;
+    if constexpr (LIVE && !AREG) {  // A: one k-half of this wave's batch (the two slice groups split the 4 KB)
+      const ob_v4i* src_a = asrc(s);
 #pragma unroll
       for (int t = 0; t < kADmaPerWave; ++t) {
         const int u = (grp * kADmaPerWave + t) * 64;
-        oz_dma16(asrc + u + lane, (uint32_t)(kLdsB + (size_t)(buf * kAUnits + wb * 256 + u) * 16));
+        oz_dma16(src_a + u + lane, (uint32_t)(kLdsB + (size_t)(buf * kAUnits + wb * 256 + u) * 16));
       }
     }
   };
-  // fragments of half-step (sub-tile in ring stage buf, k-half k2)
+  // A fragments held in registers (AREG): three slots, sub-tile s in slot (s - s0) % 3
+  ob_v4i ar[3][2][2];
+  auto aload = [&](ob_v4i (&dst)[2][2], uint32_t s) {
+    const ob_v4i* src_a = asrc(s) + lane;
+#pragma unroll
+    for (int k2 = 0; k2 < 2; ++k2)
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) dst[k2][rb] = __builtin_nontemporal_load(src_a + (k2 * 2 + rb) * 64);
+  };
+  // B fragments (and the LDS A fragments) of half-step (sub-tile in ring stage buf, k-half k2)
   auto read = [&](int buf, int k2, ob_v4i (&af)[2], ob_v4i (&bf)[kSlo]) {
-    const ob_v4i* ab = as + buf * kAUnits + wb * 256 + k2 * 128 + lane;
-    af[0] = ab[0];
-    af[1] = ab[64];
+    if constexpr (!AREG) {
+      const ob_v4i* ab = as + buf * kAUnits + wb * 256 + k2 * 128 + lane;
+      af[0] = ab[0];
+      af[1] = ab[64];
+    }
     const ob_v4i* bb = bs + buf * kSubUnits + (slo * 2 + k2) * 64 + lane;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) bf[q] = bb[q * 128];
@@ -252,45 +272,68 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
     for (int q = 0; q < kSlo; ++q) acc[rb][q] = (ob_v16i){};
-  // prologue: sub-tiles s0 .. s0 + 3 in flight; publish s0
+  // prologue: B of sub-tiles s0 .. s0 + 3 and A of s0 .. s0 + 2 in flight; publish s0
+  // (A loads unconditional, clamped to the last sub-tile, so that the three register slots are
+  // loaded in the same order on entry to the loop as on its back edge)
+  if constexpr (LIVE && AREG) {
+    aload(ar[0], s0);
+    aload(ar[1], min(s0 + 1, s1 - 1));
+    aload(ar[2], min(s0 + 2, s1 - 1));
+  }
 #pragma unroll
   for (int j = 0; j < kNbuf; ++j)
     if (s0 + j < s1) dma(j, s0 + j);
-  {
-    const uint32_t left = s1 - s0;  // >= 1
-    if (left >= 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * PER) : "memory");
-    else if (left == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
-    else if (left == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
+  // every prologue load is waited for: simple, and once per block
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   ob_v4i fa0[2], fb0[kSlo], fa1[2], fb1[kSlo];
   if constexpr (LIVE) read(0, 0, fa0, fb0);
 
-  // Half-step (s, 0): read (s, 1); MFMAs on (s, 0). Barrier B_s: sub-tile s + 1 landed (own DMAs,
-  // then everyone's), every read of sub-tile s done. Refill stage s with s + 4. Half-step (s, 1):
-  // read (s + 1, 0) (after the last sub-tile: a stale stage, never used); MFMAs on (s, 1).
-  for (uint32_t s = s0; s < s1; ++s) {
+  // Half-step (s, 0): read (s, 1); MFMAs on (s, 0). Barrier B_s: sub-tile s + 1 landed (own loads,
+  // then everyone's), every read of sub-tile s done. Refill stage s with B of s + 4. Half-step
+  // (s, 1): read (s + 1, 0) (after the last sub-tile: a stale stage, never used); MFMAs on (s, 1);
+  // then A of s + 3 into the register slot s frees. Issue order per sub-tile t: B(t + 4) after
+  // B_t, A(t + 3) at the end of step t, so at B_s the loads newer than those of s + 1 are
+  // B(s + 3), A(s + 2) (after step s - 1) and B(s + 2) is older than A(s + 1): the wait leaves
+  // PER in flight while two or more sub-tiles follow.
+  auto step = [&](uint32_t s, auto J) {
+    constexpr int j = decltype(J)::value;
     const int buf = (int)((s - s0) & (kNbuf - 1));
     if constexpr (LIVE) {
       read(buf, 1, fa1, fb1);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!(DIAG & 2)) oz_mfmas<NQ>(acc, fa0, fb0);
+      if constexpr (!(DIAG & 2)) {
+        if constexpr (AREG) oz_mfmas<NQ>(acc, ar[j][0], fb0);
+        else oz_mfmas<NQ>(acc, fa0, fb0);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
     const uint32_t ahead = (DIAG & 4) ? 0u : s1 - 1 - s;  // sub-tiles after s
-    if (ahead >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");  // s + 2, s + 3 in flight
-    else if (ahead == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+    if (ahead >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     oz_barrier();
     if (!(DIAG & 4) && s + kNbuf < s1) dma(buf, s + kNbuf);
     if constexpr (LIVE) {
       read((buf + 1) & (kNbuf - 1), 0, fa0, fb0);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!(DIAG & 2)) oz_mfmas<NQ>(acc, fa1, fb1);
+      if constexpr (!(DIAG & 2)) {
+        if constexpr (AREG) oz_mfmas<NQ>(acc, ar[j][1], fb1);
+        else oz_mfmas<NQ>(acc, fa1, fb1);
+      }
       __builtin_amdgcn_sched_barrier(0);
+      // unconditional (past the end: a re-read of the last sub-tile, never used), so the compiler's
+      // count of outstanding A loads is exact at every MFMA
+      if constexpr (AREG && !(DIAG & 4)) aload(ar[j], min(s + 3, s1 - 1));
     }
+  };
+  uint32_t s = s0;
+  for (; s + 3 <= s1; s += 3) {
+    step(s, IC<0>{});
+    step(s + 1, IC<1>{});
+    step(s + 2, IC<2>{});
   }
+  if (s < s1) step(s, IC<0>{});
+  if (s + 1 < s1) step(s + 1, IC<1>{});
   // slices -> f64: this wave's digits meet exactly in int64, one ldexp each; group 1 goes through
   // LDS to its group-0 partner, which adds (one rounding) and stores.
   const int pair = ct * kPairsPerTile + (lane & 31);
@@ -330,7 +373,7 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
     }
 }
 
-template <int DIAG>
+template <bool AREG, int DIAG>
 __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -342,14 +385,14 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
   const bool live = rt * 4u + (uint32_t)(wave & 3) < a.nb_rep;
   // waves 0-3: slices 0-3, two B pieces; 4-5: slices 4-6, two B pieces; 6-7: slices 4-6, one piece
   if (wave < 4) {
-    if (live) oz_gram_body<kSlo, 4, true, DIAG>(a, smem, wave);
-    else oz_gram_body<kSlo, 2, false, DIAG>(a, smem, wave);
+    if (live) oz_gram_body<kSlo, 2, true, AREG, DIAG>(a, smem, wave);
+    else oz_gram_body<kSlo, 2, false, AREG, DIAG>(a, smem, wave);
   } else if (wave < 6) {
-    if (live) oz_gram_body<kS - kSlo, 4, true, DIAG>(a, smem, wave);
-    else oz_gram_body<kS - kSlo, 2, false, DIAG>(a, smem, wave);
+    if (live) oz_gram_body<kS - kSlo, 2, true, AREG, DIAG>(a, smem, wave);
+    else oz_gram_body<kS - kSlo, 2, false, AREG, DIAG>(a, smem, wave);
   } else {
-    if (live) oz_gram_body<kS - kSlo, 3, true, DIAG>(a, smem, wave);
-    else oz_gram_body<kS - kSlo, 1, false, DIAG>(a, smem, wave);
+    if (live) oz_gram_body<kS - kSlo, 1, true, AREG, DIAG>(a, smem, wave);
+    else oz_gram_body<kS - kSlo, 1, false, AREG, DIAG>(a, smem, wave);
   }
 }
 
@@ -449,6 +492,10 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
     const char* e = getenv("OB_GRAM_DIAG");
     return e ? atoi(e) & 6 : 0;
   }();
+  static const bool areg = [] {  // OB_OZ_AREG=0: A fragments through the LDS ring (measurement)
+    const char* e = getenv("OB_OZ_AREG");
+    return !(e && e[0] == '0');
+  }();
   const uint32_t blocks = (uint32_t)n_chunks * a.n_rt * (uint32_t)a.n_ct;
   auto launch = [&](auto kern) -> hipError_t {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
@@ -456,11 +503,15 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(kWaves * 64), kLdsBytes, s, a);
     return hipGetLastError();
   };
-  switch (diag) {
-    case 2: OZ_HIP(launch(oz_gram_kernel<2>)); break;
-    case 4: OZ_HIP(launch(oz_gram_kernel<4>)); break;
-    case 6: OZ_HIP(launch(oz_gram_kernel<6>)); break;
-    default: OZ_HIP(launch(oz_gram_kernel<0>)); break;
+  switch (diag + (areg ? 8 : 0)) {
+    case 2: OZ_HIP(launch(oz_gram_kernel<false, 2>)); break;
+    case 4: OZ_HIP(launch(oz_gram_kernel<false, 4>)); break;
+    case 6: OZ_HIP(launch(oz_gram_kernel<false, 6>)); break;
+    case 0: OZ_HIP(launch(oz_gram_kernel<false, 0>)); break;
+    case 10: OZ_HIP(launch(oz_gram_kernel<true, 2>)); break;
+    case 12: OZ_HIP(launch(oz_gram_kernel<true, 4>)); break;
+    case 14: OZ_HIP(launch(oz_gram_kernel<true, 6>)); break;
+    default: OZ_HIP(launch(oz_gram_kernel<true, 0>)); break;
   }
   return OB_OK;
 }
