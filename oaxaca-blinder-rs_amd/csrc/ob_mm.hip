@@ -109,13 +109,20 @@ __device__ __forceinline__ uint32_t row_count(const MmArgs& a, uint32_t slot, ui
 // values from LDS. The rows' design values are gathered 64 list rows at a time into
 // double-buffered LDS (loaded one sub-tile ahead); the (fit, row) state streams into registers
 // kRing steps ahead of use, across sub-tile seams.
-constexpr int kXs = 18;     // LDS stride of a staged row: [1, x_1..x_p, 0.., y at 16, 0 at 17]
-constexpr int kXy = 16, kXzero = 17;
+// LDS stride of a staged row: [1, x_1..x_p, 0.., y at S - 2, 0 at S - 1]; 18 doubles up to K = 16
+// (odd in 8-byte units: conflict-free row reads), 34 up to K = 32.
+template <int K>
+struct Xs {
+  static_assert(K >= 1 && K <= 32, "Machado-Mata panels take at most 32 columns");
+  static constexpr int S = K <= 16 ? 18 : 34;
+  static constexpr int Y = S - 2, Z = S - 1;
+  static constexpr int Stage = (64 * S + 255) / 256;  // staging values per thread (kSub = 64 rows)
+  static constexpr int NXB = (K + 15) / 16;           // 16-column blocks of X' v products
+};
 constexpr int kSub = 64;    // list rows per staged sub-tile (16 wave steps of 4 rows)
 constexpr int kRing = 4;    // wave steps of state in flight (affine / final)
 constexpr int kRingA = 4;   // the same for the assemble pass (its fragments sit in LDS to make room)
 constexpr int kStoreAt = 4; // step after which the next sub-tile's staged values are written
-constexpr int kStage = (kSub * kXs + 255) / 256;  // staging values per thread
 typedef double mm_d4 __attribute__((ext_vector_type(4)));
 static_assert(kRc % 256 == 0 && kRc / 256 == 8, "mm_rows_kernel: 8 rows per thread");
 static_assert(16 % kRing == 0, "ring slots are static per unrolled step");
@@ -189,25 +196,27 @@ __device__ __forceinline__ Blk blk_ctx(const MmArgs& a, uint32_t* lst, bool all_
 // select: no branch around a load) ...
 template <int K>
 __device__ __forceinline__ void xs_load(const MmArgs& a, const Blk& b, const uint32_t* lst, uint32_t t,
-                                        double (&v)[kStage]) {
+                                        double (&v)[Xs<K>::Stage]) {
+  constexpr int S = Xs<K>::S;
 #pragma unroll
-  for (int j = 0; j < kStage; ++j) {
+  for (int j = 0; j < Xs<K>::Stage; ++j) {
     const int i = threadIdx.x + 256 * j;
-    const int rr = i / kXs, col = i % kXs;
+    const int rr = i / S, col = i % S;
     const uint32_t e = t * kSub + rr;
-    const bool in = i < kSub * kXs && e < b.n_ent;
+    const bool in = i < kSub * S && e < b.n_ent;
     const uint32_t row = b.r0 + (lst[min(e, b.n_ent - 1)] >> 8);
-    const int src = (col >= 1 && col < K) ? col - 1 : (col == kXy ? a.p : 0);
+    const int src = (col >= 1 && col < K) ? col - 1 : (col == Xs<K>::Y ? a.p : 0);
     const double x = b.X[(size_t)src * b.ld + row];
-    v[j] = !in ? 0.0 : (col == 0 ? 1.0 : ((col < K || col == kXy) ? x : 0.0));
+    v[j] = !in ? 0.0 : (col == 0 ? 1.0 : ((col < K || col == Xs<K>::Y) ? x : 0.0));
   }
 }
 // ... -> LDS.
-__device__ __forceinline__ void xs_store(double* xs, const double (&v)[kStage]) {
+template <int K>
+__device__ __forceinline__ void xs_store(double* xs, const double (&v)[Xs<K>::Stage]) {
 #pragma unroll
-  for (int j = 0; j < kStage; ++j) {
+  for (int j = 0; j < Xs<K>::Stage; ++j) {
     const int i = threadIdx.x + 256 * j;
-    if (i < kSub * kXs) xs[i] = v[j];
+    if (i < kSub * Xs<K>::S) xs[i] = v[j];
   }
 }
 
@@ -246,7 +255,7 @@ __device__ __forceinline__ void group_dots(const double* X, int G, const Blk& b,
   for (int v = 0; v < NV; ++v) d[v] = (mm_d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
   for (int kb = 0; kb < (K + 3) / 4; ++kb) {
-    const double av = X[(16 * G + b.fl) * kXs + 4 * kb + b.rl];
+    const double av = X[(16 * G + b.fl) * Xs<K>::S + 4 * kb + b.rl];
 #pragma unroll
     for (int v = 0; v < NV; ++v) d[v] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, f[v][kb], d[v], 0, 0, 0);
   }
@@ -261,7 +270,7 @@ __device__ __forceinline__ void group_dots_lds(const double* X, int G, const Blk
   const int fit = b.wave * 16 + b.fl;
 #pragma unroll
   for (int kb = 0; kb < (K + 3) / 4; ++kb) {
-    const double av = X[(16 * G + b.fl) * kXs + 4 * kb + b.rl];
+    const double av = X[(16 * G + b.fl) * Xs<K>::S + 4 * kb + b.rl];
     const int k = 4 * kb + b.rl;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
@@ -327,10 +336,11 @@ __device__ __forceinline__ Corrector corrector_row(const Affine& f, double xd, d
 // column block cb < NCB has B = x_i x_j of pair columns cb*16.. (ob_pair_index order), block NCB
 // has A = q r and B = x.
 template <int K, bool STEP>
-__global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a, int mode) {
+__global__ __launch_bounds__(256, K <= 16 ? 2 : 1) void mm_assemble_mfma_kernel(const MmArgs a, int mode) {
   constexpr int NP = K * (K + 1) / 2, NV = NP + K + 2;
   constexpr int NCB = (NP + 15) / 16;
-  __shared__ __attribute__((aligned(16))) double xs[2][kSub * kXs];
+  constexpr int NXB = Xs<K>::NXB;  // X'Q r column blocks
+  __shared__ __attribute__((aligned(16))) double xs[2][kSub * Xs<K>::S];
   __shared__ uint32_t lst[kRc];
   const Blk b = blk_ctx(a, lst, mode == 0);
   if (!b.any) return;  // partials of dead fits are never reduced
@@ -353,13 +363,13 @@ __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a
     delta = a.fs[b.F * kFs + FS_DELTA];
     sigmu = a.fs[b.F * kFs + FS_SIGMU];
   }
-  // B-operand columns (i, j) of this lane (n = fl) per pair block, packed i | j << 8; kXzero
-  // past the last pair
+  // B-operand columns (i, j) of this lane (n = fl) per pair block, packed i | j << 8; the zero
+  // slot past the last pair
   uint32_t pp[NCB];
 #pragma unroll
   for (int cb = 0; cb < NCB; ++cb) {
     const int e = cb * 16 + b.fl;
-    pp[cb] = kXzero | (kXzero << 8);
+    pp[cb] = Xs<K>::Z | (Xs<K>::Z << 8);
     if (e < NP) {
       int i = 0, e0 = 0;
       while (e >= e0 + (K - i)) {
@@ -369,16 +379,16 @@ __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a
       pp[cb] = (uint32_t)i | (uint32_t)(i + (e - e0)) << 8;
     }
   }
-  mm_d4 acc[NCB + 1];
+  mm_d4 acc[NCB + NXB];
 #pragma unroll
-  for (int cb = 0; cb <= NCB; ++cb) acc[cb] = (mm_d4){0.0, 0.0, 0.0, 0.0};
+  for (int cb = 0; cb < NCB + NXB; ++cb) acc[cb] = (mm_d4){0.0, 0.0, 0.0, 0.0};
   double gap = 0.0, obj = 0.0;
   __syncthreads();  // lst
   const uint32_t nsub = (b.n_ent + kSub - 1) / kSub;
   if (__syncthreads_or(b.live) && nsub) {
-    double stg[kStage];
+    double stg[Xs<K>::Stage];
     xs_load<K>(a, b, lst, 0, stg);
-    xs_store(xs[0], stg);
+    xs_store<K>(xs[0], stg);
     double rx[kRingA], rz[kRingA], rw[kRingA];
     auto load = [&](int k, uint32_t e) {
       if (STEP) {
@@ -402,8 +412,8 @@ __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a
           load(k, e + 4 * kRingA);
           const bool valid = e < b.n_ent && b.live;
           const double c = valid ? (double)(lst[e] & 255u) : 0.0;
-          const double* xr = X + (4 * j + b.rl) * kXs;
-          const double y = xr[kXy];
+          const double* xr = X + (4 * j + b.rl) * Xs<K>::S;
+          const double y = xr[Xs<K>::Y];
           double q = 0.0, qr = 0.0;
           if (valid) {
             if (mode == 0) {
@@ -441,13 +451,15 @@ __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a
 #pragma unroll
           for (int cb = 0; cb < NCB; ++cb)
             acc[cb] = __builtin_amdgcn_mfma_f64_16x16x4f64(q, xr[pp[cb] & 255u] * xr[pp[cb] >> 8], acc[cb], 0, 0, 0);
-          acc[NCB] = __builtin_amdgcn_mfma_f64_16x16x4f64(qr, xr[b.fl], acc[NCB], 0, 0, 0);
+#pragma unroll
+          for (int xb = 0; xb < NXB; ++xb)
+            acc[NCB + xb] = __builtin_amdgcn_mfma_f64_16x16x4f64(qr, xr[16 * xb + b.fl], acc[NCB + xb], 0, 0, 0);
       };
       // the next sub-tile's values go to the other buffer after a few steps (registers freed)
       if (b.wave_live)
 #pragma unroll
         for (int j = 0; j < kStoreAt; ++j) step(j);
-      xs_store(xs[(t + 1) & 1], stg);
+      xs_store<K>(xs[(t + 1) & 1], stg);
       if (b.wave_live)
 #pragma unroll
         for (int j = kStoreAt; j < 16; ++j) step(j);
@@ -458,13 +470,14 @@ __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a
   double* P = a.partial + ((size_t)b.slot * (a.nch[0] + a.nch[1]) + b.gch) * a.S_pad * NV;
   const size_t fw = (size_t)b.fb * 64 + b.wave * 16;
 #pragma unroll
-  for (int cb = 0; cb <= NCB; ++cb)
+  for (int cb = 0; cb < NCB + NXB; ++cb)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const size_t fit = fw + b.rl + 4 * r;
       const int col = cb * 16 + b.fl;
       if (cb < NCB && col < NP) P[fit * NV + col] = acc[cb][r];
-      if (cb == NCB && b.fl < K) P[fit * NV + NP + b.fl] = acc[cb][r];
+      const int xc = (cb - NCB) * 16 + b.fl;
+      if (cb >= NCB && xc < K) P[fit * NV + NP + xc] = acc[cb][r];
     }
   gap = rows_sum(gap);
   obj = rows_sum(obj);
@@ -478,14 +491,14 @@ __global__ __launch_bounds__(256, 2) void mm_assemble_mfma_kernel(const MmArgs a
 // design values from the double-buffered sub-tiles, x_i . v for the fragments fb on MFMA once per
 // 4 steps. body(j-th step's state, valid, count, xr, dots).
 template <int K, int NDOT, typename Body>
-__device__ __forceinline__ void state_walk(const MmArgs& a, const Blk& b, const uint32_t* lst, double (*xs)[kSub * kXs],
+__device__ __forceinline__ void state_walk(const MmArgs& a, const Blk& b, const uint32_t* lst, double (*xs)[kSub * Xs<K>::S],
                                            const double (&fb)[NDOT][(K + 3) / 4], Body&& body) {
   mm_d4 dots[NDOT];
   const uint32_t nsub = (b.n_ent + kSub - 1) / kSub;
   if (!__syncthreads_or(b.live) || !nsub) return;
-  double stg[kStage];
+  double stg[Xs<K>::Stage];
   xs_load<K>(a, b, lst, 0, stg);
-  xs_store(xs[0], stg);
+  xs_store<K>(xs[0], stg);
   double rx[kRing], rz[kRing], rw[kRing];
   auto load = [&](int k, uint32_t e) {
     const size_t si = state_at(a, b, lst, e);
@@ -509,12 +522,12 @@ __device__ __forceinline__ void state_walk(const MmArgs& a, const Blk& b, const 
       double dv[NDOT];
 #pragma unroll
       for (int v = 0; v < NDOT; ++v) dv[v] = dots[v][j & 3];
-      body(xv, zv, wv, valid, valid ? (double)(lst[e] & 255u) : 1.0, X + (4 * j + b.rl) * kXs, dv);
+      body(xv, zv, wv, valid, valid ? (double)(lst[e] & 255u) : 1.0, X + (4 * j + b.rl) * Xs<K>::S, dv);
     };
     if (b.wave_live)
 #pragma unroll
       for (int j = 0; j < kStoreAt; ++j) step(j);
-    xs_store(xs[(t + 1) & 1], stg);
+    xs_store<K>(xs[(t + 1) & 1], stg);
     if (b.wave_live)
 #pragma unroll
       for (int j = kStoreAt; j < 16; ++j) step(j);
@@ -524,9 +537,10 @@ __device__ __forceinline__ void state_walk(const MmArgs& a, const Blk& b, const 
 
 // [0] primal step bound, [1] dual step bound, [2..4] mu_aff terms, then X'q rho0, X'q rho1.
 template <int K>
-__global__ __launch_bounds__(256, 3) void mm_affine_kernel(const MmArgs a) {
+__global__ __launch_bounds__(256, K <= 16 ? 3 : 2) void mm_affine_kernel(const MmArgs a) {
   constexpr int NV = 5 + 2 * K;
-  __shared__ __attribute__((aligned(16))) double xs[2][kSub * kXs];
+  constexpr int NXB = Xs<K>::NXB;
+  __shared__ __attribute__((aligned(16))) double xs[2][kSub * Xs<K>::S];
   __shared__ uint32_t lst[kRc];
   const Blk b = blk_ctx(a, lst, false);
   if (!b.any) return;  // partials of dead fits are never reduced
@@ -534,13 +548,15 @@ __global__ __launch_bounds__(256, 3) void mm_affine_kernel(const MmArgs a) {
   bfrag<K>(a.beta, b, b.live, fb[0]);
   bfrag<K>(a.dba, b, b.live, fb[1]);
   double acc[5] = {1e300, 1e300, 0.0, 0.0, 0.0};
-  mm_d4 m0 = {0.0, 0.0, 0.0, 0.0}, m1 = {0.0, 0.0, 0.0, 0.0};
+  mm_d4 m0[NXB], m1[NXB];
+#pragma unroll
+  for (int xb = 0; xb < NXB; ++xb) m0[xb] = m1[xb] = (mm_d4){0.0, 0.0, 0.0, 0.0};
   __syncthreads();  // lst
   state_walk<K, 2>(a, b, lst, xs, fb, [&](double xv, double zv, double wv, bool valid, double c, const double* xr,
                                           const double (&dv)[2]) {
     double q0 = 0.0, q1 = 0.0;
     if (valid) {
-      const Affine f = affine_row(xv, zv, wv, c, xr[kXy], dv[0], dv[1]);
+      const Affine f = affine_row(xv, zv, wv, c, xr[Xs<K>::Y], dv[0], dv[1]);
       if (f.dxa != 0.0) acc[0] = fmin(acc[0], (f.dxa < 0.0 ? -f.xv : f.sv) * mm_rcp(f.dxa));
       if (f.dza < 0.0) acc[1] = fmin(acc[1], -f.zv * mm_rcp(f.dza));
       if (f.dwa < 0.0) acc[1] = fmin(acc[1], -f.wv * mm_rcp(f.dwa));
@@ -550,19 +566,24 @@ __global__ __launch_bounds__(256, 3) void mm_affine_kernel(const MmArgs a) {
       q0 = f.q * (f.r - f.dxa * (f.dwa * f.is + f.dza * f.ix));
       q1 = f.q * (f.ix - f.is);
     }
-    const double bx = xr[b.fl];  // B: row rl, column fl (zero past K)
-    m0 = __builtin_amdgcn_mfma_f64_16x16x4f64(q0, bx, m0, 0, 0, 0);
-    m1 = __builtin_amdgcn_mfma_f64_16x16x4f64(q1, bx, m1, 0, 0, 0);
+#pragma unroll
+    for (int xb = 0; xb < NXB; ++xb) {
+      const double bx = xr[16 * xb + b.fl];  // B: row rl, column 16 xb + fl (zero past K)
+      m0[xb] = __builtin_amdgcn_mfma_f64_16x16x4f64(q0, bx, m0[xb], 0, 0, 0);
+      m1[xb] = __builtin_amdgcn_mfma_f64_16x16x4f64(q1, bx, m1[xb], 0, 0, 0);
+    }
   });
   double* P = a.partial + ((size_t)b.slot * (a.nch[0] + a.nch[1]) + b.gch) * a.S_pad * NV;
   const size_t fw = (size_t)b.fb * 64 + b.wave * 16;
-  if (b.fl < K)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const size_t fit = fw + b.rl + 4 * r;
-      P[fit * NV + 5 + b.fl] = m0[r];
-      P[fit * NV + 5 + K + b.fl] = m1[r];
-    }
+  for (int xb = 0; xb < NXB; ++xb)
+    if (16 * xb + b.fl < K)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const size_t fit = fw + b.rl + 4 * r;
+        P[fit * NV + 5 + 16 * xb + b.fl] = m0[xb][r];
+        P[fit * NV + 5 + K + 16 * xb + b.fl] = m1[xb][r];
+      }
   acc[0] = rows_min(acc[0]);
   acc[1] = rows_min(acc[1]);
 #pragma unroll
@@ -575,7 +596,7 @@ __global__ __launch_bounds__(256, 3) void mm_affine_kernel(const MmArgs a) {
 // Step-length bounds of the corrector direction (the next assemble replays the direction).
 template <int K>
 __global__ __launch_bounds__(256, 2) void mm_final_kernel(const MmArgs a) {
-  __shared__ __attribute__((aligned(16))) double xs[2][kSub * kXs];
+  __shared__ __attribute__((aligned(16))) double xs[2][kSub * Xs<K>::S];
   __shared__ uint32_t lst[kRc];
   const Blk b = blk_ctx(a, lst, false);
   if (!b.any) return;  // partials of dead fits are never reduced
@@ -589,7 +610,7 @@ __global__ __launch_bounds__(256, 2) void mm_final_kernel(const MmArgs a) {
   state_walk<K, 3>(a, b, lst, xs, fb, [&](double xv, double zv, double wv, bool valid, double c, const double* xr,
                                           const double (&dv)[3]) {
     if (!valid) return;
-    const Affine f = affine_row(xv, zv, wv, c, xr[kXy], dv[0], dv[1]);
+    const Affine f = affine_row(xv, zv, wv, c, xr[Xs<K>::Y], dv[0], dv[1]);
     const Corrector d = corrector_row(f, dv[2], sigmu);
     const double dx = d.dx, dz = d.dz, dw = d.dw;
     if (dx != 0.0) acc[0] = fmin(acc[0], (dx < 0.0 ? -f.xv : f.sv) * mm_rcp(dx));
@@ -716,7 +737,7 @@ __global__ __launch_bounds__(1024) void mm_shift_kernel(const MmArgs a, int K) {
   __shared__ double key[kShiftSamples];
   __shared__ double wt[kShiftSamples];
   __shared__ uint32_t pre[1024 + 1];
-  __shared__ double beta[16];
+  __shared__ double beta[ob::kMmMaxK];
   const uint32_t slot = blockIdx.x >> 1, g = blockIdx.x & 1;
   const uint32_t nch = a.nch[0] + a.nch[1], c0 = g ? a.nch[0] : 0u, ncg = a.nch[g];
   const size_t F0 = fit_index(a, slot, g, 0);
@@ -1035,6 +1056,8 @@ void pass(int K, int which, const MmArgs& a, dim3 grid, int mode, hipStream_t s)
   case k: launch_pass<k>(which, a, grid, mode, s); break;
     OB_MM_K(1) OB_MM_K(2) OB_MM_K(3) OB_MM_K(4) OB_MM_K(5) OB_MM_K(6) OB_MM_K(7) OB_MM_K(8)
     OB_MM_K(9) OB_MM_K(10) OB_MM_K(11) OB_MM_K(12) OB_MM_K(13) OB_MM_K(14) OB_MM_K(15) OB_MM_K(16)
+    OB_MM_K(17) OB_MM_K(18) OB_MM_K(19) OB_MM_K(20) OB_MM_K(21) OB_MM_K(22) OB_MM_K(23) OB_MM_K(24)
+    OB_MM_K(25) OB_MM_K(26) OB_MM_K(27) OB_MM_K(28) OB_MM_K(29) OB_MM_K(30) OB_MM_K(31) OB_MM_K(32)
 #undef OB_MM_K
     default: break;
   }

@@ -6,7 +6,7 @@
 #include "ob_engine.hpp"
 
 namespace ob {
-constexpr int kMmMaxK = 16;      // intercept + predictors (register-resident normal matrix)
+constexpr int kMmMaxK = 32;      // intercept + predictors (LDS row stride 34, two X'v column blocks)
 constexpr int kMmMaxSims = 4096;  // simulations per pass (LDS sort in the finish kernel)
 constexpr int kMmMaxIter = 200;   // IPM iterations per fit (Clarabel's default max_iter)
 

@@ -38,7 +38,8 @@ def oracle_rows(O, d, sims, qs, reps):
     return np.array(rows)
 
 
-@pytest.mark.parametrize("n,p,sims", [(600, 1, 30), (1500, 3, 40), (3000, 5, 24), (5000, 15, 12)])
+@pytest.mark.parametrize("n,p,sims", [(600, 1, 30), (1500, 3, 40), (3000, 5, 24), (5000, 15, 12),
+                                      (6000, 16, 8), (6000, 23, 8), (8000, 31, 6)])
 def test_mm_rows_match_oracle(ob, O, n, p, sims):
     d = mm_data(n, p, seed=n + p)
     panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"])
@@ -107,6 +108,18 @@ def test_mm_errors(ob, N):
     with pytest.raises(N.OaxacaError) as e:  # :202-206
         ob.QuantileDecompositionBuilder(h, "wage", "gender", "F").predictors(["education"]).run()
     assert "insufficient data" in str(e.value)
+
+
+def test_mm_width_limit(ob, N):
+    """32 columns (intercept + 31 predictors) run; 33 are refused with OB_E_UNSUPPORTED."""
+    d = mm_data(800, 32, seed=3)
+    panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"])
+    try:
+        with pytest.raises(N.OaxacaError) as e:
+            panel.mm(SEED, 8, QS, 0, 1)
+        assert e.value.code == N.OB_E_UNSUPPORTED
+    finally:
+        panel.close()
 
 
 def test_mm_deterministic_and_shard_invariant(ob):
