@@ -114,7 +114,7 @@ bool parse_f64(const std::string& t, double& v) {
 // Line starts/ends (a trailing '\r' is stripped). Quoted newlines are not split when the
 // file contains quotes (then the scan runs sequentially with quote tracking).
 void find_lines(const char* data, size_t size, std::vector<std::pair<size_t, size_t>>& lines) {
-  const bool has_quote = std::memchr(data, '"', size) != nullptr;
+  const bool has_quote = size && std::memchr(data, '"', size) != nullptr;  // an empty file maps no data
   size_t b = 0;
   bool inq = false;
   for (size_t k = 0; k < size; ++k) {
