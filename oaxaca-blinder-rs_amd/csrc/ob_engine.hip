@@ -69,7 +69,8 @@ struct GramArgs {
   uint32_t* flags;
   const uint32_t* counts;  // level-2 count images [tile (A then B)][batch][sub-tile][kCimgWords]
   uint32_t tiles_total;
-  int diag;  // OB_GRAM_DIAG bits: 2 no MFMAs, 4 no sub-tile DMA (tools/gram_ablate.py), 8 raw Heckman statuses
+  int diag;  // OB_GRAM_DIAG bits: 2 no MFMAs, 4 no sub-tile DMA (tools/gram_ablate.py), 8 raw Heckman
+             // statuses; count kernel timing ablations (wrong counts): 32 no LDS atomics, 64 no Philox
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -351,9 +352,15 @@ __device__ __forceinline__ void level2_draws(const GramArgs& a, const Work& w, u
     }
     if (f < f_hi) {
       const uint32_t pp = f - base;
-      const ob_u32x4 u = ob_philox(pp, rep0 + r, c2, OB_TAG_L2, a.key0, a.key1);
+      ob_u32x4 u;
+      if (a.diag & 64)  // timing ablation (OB_GRAM_DIAG 64): no Philox, wrong draws
+        u = ob_u32x4{pp * 0x9E3779B9u ^ r, pp * 0x85EBCA6Bu ^ c2, pp * 0xC2B2AE35u, pp ^ 0x27D4EB2Fu};
+      else
+        u = ob_philox(pp, rep0 + r, c2, OB_TAG_L2, a.key0, a.key1);
       uint32_t* row = cnt + r * kCntStride;
-      if (full) {
+      if (full && (a.diag & 32)) {  // timing ablation (OB_GRAM_DIAG 32): no LDS atomics
+        if ((u.x ^ u.y ^ u.z ^ u.w) == 0x5EED5EEDu) row[0] = 1u;
+      } else if (full) {
         const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
         for (int d = 0; d < 16; ++d) add_draw(row, (wd[d >> 2] >> (8 * (d & 3))) & 0xFFu);
@@ -391,13 +398,13 @@ __device__ __forceinline__ void check_counts(const GramArgs& a, uint32_t* cnt, c
     sum = __builtin_amdgcn_sad_u8(row[i], 0u, sum);
     hib |= row[i] & 0x80808080u;
   }
-  if (i8 && hib) atomicOr(a.flags, 1u);  // the i8 Gram reads counts as signed bytes: at most 127
+  if (i8 && hib && !(a.diag & 96)) atomicOr(a.flags, 2u);  // the i8 Gram reads counts as signed bytes: at most 127
   if (zero)
 #pragma unroll
     for (int i = 0; i < 16; ++i) row[i] = 0u;
   sum += __shfl_xor(sum, 1);
   sum += __shfl_xor(sum, 2);
-  if (part == 0 && sum != mc[r]) atomicOr(a.flags, 1u);
+  if (part == 0 && sum != mc[r] && !(a.diag & 96)) atomicOr(a.flags, 1u);
 }
 
 // Level-1 count of global tile tt (group 0's tiles, then group 1's) for batch replicate r.
@@ -1412,7 +1419,10 @@ int engine_collect(ob_panel* p) {
   }
   uint32_t flag = 0;
   HIP_OK(hipMemcpy(&flag, p->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost));
-  if (flag) return ob::fail(OB_E_OVERFLOW, "a resampled row was drawn more than 255 times in one replicate");
+  if (flag & 1u) return ob::fail(OB_E_OVERFLOW, "a resampled row was drawn more than 255 times in one replicate");
+  if (flag & 2u)  // p ~ 1e-215 per row and replicate; the f64 Gram path takes counts up to 255
+    return ob::fail(OB_E_OVERFLOW, "a resampled row was drawn more than 127 times in one replicate "
+                                   "(the i8 Gram's range; OB_GRAM_PATH=f64 runs the f64 MFMA Gram)");
   return OB_OK;
 }
 
@@ -1719,7 +1729,7 @@ int ob_debug_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_r
   HIP_OK(hipStreamSynchronize(s));
   uint32_t flag = 0;
   HIP_OK(hipMemcpy(&flag, p->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost));
-  if (flag) return ob::fail(OB_E_OVERFLOW, "a resampled row was drawn more than 255 times in one replicate");
+  if (flag & 1u) return ob::fail(OB_E_OVERFLOW, "a resampled row was drawn more than 255 times in one replicate");
   const uint32_t tiles = p->ntiles[0] + p->ntiles[1], tg = p->ntiles[group], t0 = group ? p->ntiles[0] : 0u;
   const uint32_t n = p->n[group];
   if (level1) {
