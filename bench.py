@@ -31,7 +31,7 @@ sys.path.insert(0, ROOT)
 
 F64_MFMA_PEAK_TFLOPS = 78.6  # MI355X dense FP64 matrix peak (v_mfma_f64_16x16x4_f64, 2.4 GHz)
 I8_MFMA_PEAK_TOPS = 5000.0  # dense I8 MFMA: 2x the ~2.5 PF dense BF16 rate per clock (MI355X_MICROARCH.md, Matrix cores)
-OZ_SLICES = 8  # ob_gram_i8.hip: 7-bit digits per pair product
+OZ_SLICES = 7  # ob_gram_i8.hip: balanced 8-bit digits per pair product (54-bit fixed point)
 OZ_PAIRS_PER_TILE = 32
 HBM_PEAK_GBPS = 8000.0
 
@@ -529,7 +529,7 @@ def main():
                        "replicates_per_step": total, "replicates_per_gpu_per_step": per_rank,
                        "parallelism": f"replicates sharded x{world}, engine RCCL all-gather (ob_boot_run_sharded_device)"},
             "roofline": roof,
-            "gram_path": "i8 MFMA, exact 8 x 7-bit digit slices (f64-equivalent)" if gram_path == 2 else "f64 MFMA",
+            "gram_path": "i8 MFMA (v_mfma_i32_16x16x64_i8), exact 7 x 8-bit digit slices (f64-equivalent)" if gram_path == 2 else "f64 MFMA",
             "gather_equivalent": {"algorithmic_bytes_per_replicate": bytes_rep,
                                   "GBps": bytes_rep * value / world / 1e9,
                                   "frac_of_hbm_peak": bytes_rep * value / world / 1e9 / HBM_PEAK_GBPS},

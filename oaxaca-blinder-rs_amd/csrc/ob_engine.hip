@@ -454,9 +454,9 @@ __device__ __forceinline__ void store_partials(const GramArgs& a, const Work& w,
 // ---------------------------------------------------------------------------------------------
 constexpr int kCntTilesPerBlock = 8;
 
-// I8: the image is written in the A-fragment order of ob_gram_i8.hip instead: per (tile, batch)
-// [sub-tile][k-half][replicate half][lane][16 B], lane l = replicate (l & 31) of the half, rows
-// 16 (l >> 5) + j of the k-half -- 16 KB, one 16-byte store per thread and unit.
+// I8: the image is written in the A-fragment order of ob_gram_i8.hip instead (v_mfma_i32_16x16x64_i8):
+// per (tile, batch) [sub-tile][16-replicate block m][lane][16 B], lane l = replicate 16 m + (l & 15),
+// rows 16 (l >> 4) + j of the sub-tile -- 16 KB, one 16-byte store per thread and unit.
 template <bool I8>
 __global__ __launch_bounds__(kBlock) void ob_count_kernel(const GramArgs a) {
   __shared__ uint32_t img[64 * kCntStride];
@@ -486,8 +486,8 @@ __global__ __launch_bounds__(kBlock) void ob_count_kernel(const GramArgs a) {
     if constexpr (I8) {
       uint4* out = reinterpret_cast<uint4*>(const_cast<uint32_t*>(a.counts)) + ((size_t)tt * a.nb_rep + w.rb) * 1024;
       for (uint32_t u = tid; u < ns * 256; u += kBlock) {
-        const uint32_t ln = u & 63u, rh = (u >> 6) & 1u, k2 = (u >> 7) & 1u, sb = u >> 8;
-        const uint32_t* src = img + (rh * 32 + (ln & 31u)) * kCntStride + sb * 16 + k2 * 8 + 4 * (ln >> 5);
+        const uint32_t ln = u & 63u, mb = (u >> 6) & 3u, sb = u >> 8;
+        const uint32_t* src = img + (mb * 16 + (ln & 15u)) * kCntStride + sb * 16 + 4 * (ln >> 4);
         out[u] = make_uint4(src[0], src[1], src[2], src[3]);
       }
     } else {

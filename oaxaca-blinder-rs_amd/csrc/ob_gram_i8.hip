@@ -15,20 +15,21 @@
 // |sum| < 2^31). The slices meet in int64, two f64 roundings per chunk partial, so the Gram
 // equals the f64 MFMA Gram to ~1e-15 relative (tests/test_gpu_gram_i8.py holds it to 1e-12).
 //
-// v_mfma_i32_32x32x32_i8 issues in 32 cycles like v_mfma_f32_32x32x16_bf16 (MI355X_MICROARCH.md,
+// v_mfma_i32_16x16x64_i8 issues in 16 cycles like v_mfma_f32_16x16x32_bf16 (MI355X_MICROARCH.md,
 // Matrix cores): 64x the f64 MFMA rate, so 7 slices cost 7x the f64 multiply count and still
 // leave 9x headroom. Layouts (HBM, built once per panel):
-//   B (digits): per group [sub-tile 64 rows][col tile: 32 pairs][slice][k-half 32 rows][lane][16 B]
-//               -- lane l holds pair (l & 31), rows 16 (l >> 5) + j of the k-half: the B fragment
-//               of 32x32x32_i8 (probed: tools/mfma_i8_probe.hip), one 14 KB DMA per sub-tile.
-//   A (counts): ob_count_kernel<true> writes [tile][64-rep batch][sub-tile][k-half][rep half][lane][16 B]
-//               -- lane l holds replicate (l & 31) of the half, the same rows: the A fragment.
+//   B (digits): per group [sub-tile 64 rows][col tile: 32 pairs][slice][pair block h][lane][16 B]
+//               -- lane l holds pair 16 h + (l & 15), rows 16 (l >> 4) + j: the B fragment of
+//               16x16x64_i8 (probed: tools/mfma_i8_probe.hip), one 14 KB DMA per sub-tile.
+//   A (counts): ob_count_kernel<true> writes [tile][64-rep batch][sub-tile][rep block m][lane][16 B]
+//               -- lane l holds replicate 16 m + (l & 15), the same rows: the A fragment.
 // Kernel: 8 waves (two per SIMD), one block per CU, block tile 256 replicates x 32 pairs x 7
-// slices; wave w owns replicate batch w & 3 (2 x 32 replicates) and slice group w >> 2 (slices
-// 0-3 or 4-6): 8 or 6 accumulators of 32 x 32 i32. Both operands arrive in LDS by DMA, four
-// sub-tiles ahead. The loop runs in half-steps (sub-tile, k-half): the fragments of the next
-// half-step are read from LDS while the MFMAs of this one issue, and one barrier per sub-tile
-// (between its two halves) publishes the next sub-tile and frees the oldest ring stage.
+// slices; wave w owns replicate batch w & 3 (4 x 16 replicates) and slice group w >> 2 (slices
+// 0-3 or 4-6): 16 or 12 accumulators of 16 x 16 i32 per pair block. B arrives in LDS by DMA four
+// sub-tiles ahead; A goes straight from HBM/L2 into registers three sub-tiles ahead. The loop runs
+// in half-steps (sub-tile, pair block): the B fragments of the next half-step are read from LDS
+// while the MFMAs of this one issue, and one barrier per sub-tile (between its two halves)
+// publishes the next sub-tile and frees the oldest ring stage.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -113,14 +114,14 @@ __global__ __launch_bounds__(256) void oz_pairexp_kernel(const double* cols0, co
   }
 }
 
-// B digits of one group: grid (sub-tile, column tile), 256 threads = (slice group, k-half, lane).
+// B digits of one group: grid (sub-tile, column tile), 256 threads = (slice group, pair block, lane).
 __global__ __launch_bounds__(256) void oz_digits_kernel(const double* cols, int64_t ld, uint32_t n, int nxy,
                                                         int weighted, int k1, int e, int n_ct, int n_pairs_pad,
                                                         const int32_t* tile_chunk, const int32_t* pexp,
                                                         ob_v4i* B) {
   const uint32_t sub = blockIdx.x;
-  const int ct = blockIdx.y, t = threadIdx.x, lane = t & 63, k2 = (t >> 6) & 1, grp = t >> 7;
-  const int pair = ct * kPairsPerTile + (lane & 31);
+  const int ct = blockIdx.y, t = threadIdx.x, lane = t & 63, nb = (t >> 6) & 1, grp = t >> 7;
+  const int pair = ct * kPairsPerTile + 16 * nb + (lane & 15);
   int a = 0, b = 0;
   const bool live = pair < e;
   if (live) oz_pair_cols(pair, k1, &a, &b);
@@ -128,7 +129,7 @@ __global__ __launch_bounds__(256) void oz_digits_kernel(const double* cols, int6
   int8_t dig[16][kS];
 #pragma unroll
   for (int j = 0; j < 16; ++j) {
-    const size_t row = (size_t)sub * 64 + k2 * 32 + 16 * (lane >> 5) + j;
+    const size_t row = (size_t)sub * 64 + 16 * (lane >> 4) + j;
     double P = 0.0;
     if (live && row < n) P = oz_v(cols, ld, nxy, weighted, row, a) * oz_v(cols, ld, nxy, weighted, row, b);
     long long m = (long long)rint(ldexp(P, kFracBits - E));  // |m| <= 2^54: exact
@@ -144,7 +145,7 @@ __global__ __launch_bounds__(256) void oz_digits_kernel(const double* cols, int6
     uint32_t w[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
     for (int j = 0; j < 16; ++j) w[j >> 2] |= (uint32_t)(uint8_t)dig[j][sl] << (8 * (j & 3));
-    B[(((size_t)sub * n_ct + ct) * kS + sl) * 2 * 64 + k2 * 64 + lane] = (ob_v4i){(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+    B[(((size_t)sub * n_ct + ct) * kS + sl) * 2 * 64 + nb * 64 + lane] = (ob_v4i){(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
   }
 }
 
@@ -163,12 +164,9 @@ constexpr int kWaves = 8;                         // 2 per SIMD: (replicate batc
 constexpr int kNbuf = 4;                          // LDS ring stages (sub-tiles)
 constexpr int kBDma = (kSubUnits + 64 * kWaves - 1) / (64 * kWaves);  // B DMA instructions per wave (<=)
 constexpr int kBDmaTotal = kSubUnits / 64;        // 14 per sub-tile, spread over the waves
-constexpr int kAUnits = 4 * 256;                  // 16-byte units of a sub-tile's A (4 batches x 4 KB)
-constexpr int kADmaPerWave = 2;                   // each wave DMAs one k-half of its batch's 4 KB
 constexpr size_t kLdsB = kNbuf * (size_t)kSubUnits * 16;      // B ring (56 KB)
-constexpr size_t kLdsA = kNbuf * (size_t)kAUnits * 16;        // A ring (64 KB)
-constexpr size_t kLdsX = 4 * 64 * (size_t)kPairsPerTile * 8;  // slice-group exchange (64 KB, over the rings)
-constexpr size_t kLdsBytes = (kLdsB + kLdsA > kLdsX ? kLdsB + kLdsA : kLdsX);
+constexpr size_t kLdsX = 4 * 64 * (size_t)kPairsPerTile * 8;  // slice-group exchange (64 KB, over the ring)
+constexpr size_t kLdsBytes = kLdsB > kLdsX ? kLdsB : kLdsX;
 static_assert(kBDma == 2 && kBDmaTotal == 14, "B DMA split below assumes 14 instructions over 8 waves");
 
 // One 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4: lane l lands at lds + 16 l). Issued from
@@ -189,27 +187,32 @@ struct IC {
   static constexpr int value = N;
 };
 
+// Half-step h of a sub-tile: pair block h (16 pairs) of every slice q < NQ against the four
+// 16-replicate blocks: 4 NQ v_mfma_i32_16x16x64_i8, K = the whole 64-row sub-tile.
 template <int NQ>
-__device__ __forceinline__ void oz_mfmas(ob_v16i (&acc)[2][kSlo], const ob_v4i (&af)[2], const ob_v4i (&bf)[kSlo]) {
+__device__ __forceinline__ void oz_mfmas(ob_v4i (&acc)[4][kSlo][2], int h, const ob_v4i (&af)[4],
+                                         const ob_v4i (&bf)[kSlo]) {
 #pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    acc[0][q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[0], bf[q], acc[0][q], 0, 0, 0);
-    acc[1][q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(af[1], bf[q], acc[1][q], 0, 0, 0);
-  }
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+      acc[m][q][h] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[m], bf[q], acc[m][q][h], 0, 0, 0);
 }
 
 // Block: (chunk, replicate tile of 4 batches, column tile). NQ = slices of this wave's group, NB =
-// its B DMA pieces per sub-tile, LIVE = its replicate batch exists, AREG = its A fragments come
-// straight from HBM/L2 into registers (else through the LDS A ring). All are wave-uniform template
+// its B DMA pieces per sub-tile, LIVE = its replicate batch exists. All are wave-uniform template
 // constants, so the loop has no divergent control flow and the compiler's LDS-counter bookkeeping
 // stays exact (a wait only for the fragments an MFMA consumes). DIAG (OB_GRAM_DIAG, timing
 // ablations only, wrong results): 2 no MFMAs, 4 no sub-tile loads after the prologue.
-template <int NQ, int NB, bool LIVE, bool AREG, int DIAG>
+// MFMA shape: v_mfma_i32_16x16x64_i8 (the 16x16 forms hold a higher clock than the 32x32 forms on
+// random operands at equal cycles per op, MI355X_MICROARCH.md 'DVFS give-back' item 7). Lane l of
+// an A fragment holds replicate 16 m + (l & 15), rows 16 (l >> 4) + j of the sub-tile; lane l of a B
+// fragment pair 16 h + (l & 15) of the column tile, the same rows; D: pair 16 h + (l & 15),
+// replicates 16 m + 4 (l >> 4) + i.
+template <int NQ, int NB, bool LIVE, int DIAG>
 __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* smem, int wave) {
-  constexpr int PA = LIVE ? (AREG ? 4 : kADmaPerWave) : 0;  // A instructions per sub-tile
-  constexpr int PER = NB + PA;                              // this wave's vector-memory ops per sub-tile
-  const ob_v4i* bs = reinterpret_cast<const ob_v4i*>(smem);           // [kNbuf][kSubUnits]
-  const ob_v4i* as = reinterpret_cast<const ob_v4i*>(smem + kLdsB);   // [kNbuf][4 batches][256]
+  constexpr int PER = NB + (LIVE ? 4 : 0);  // this wave's vector-memory ops per sub-tile
+  const ob_v4i* bs = reinterpret_cast<const ob_v4i*>(smem);  // [kNbuf][kSubUnits]
   const int lane = threadIdx.x & 63;
   const int wb = wave & 3, grp = wave >> 2;  // replicate batch in the tile, slice group
   const int slo = grp ? kSlo : 0;
@@ -227,9 +230,6 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   const uint32_t s1 = min(a.chunks[3 * chunk + 2] * 4u, (n + 63u) >> 6);
   const ob_v4i* Bg = g ? a.B1 : a.B0;
   const uint32_t batch = rt * 4u + (uint32_t)wb;
-  auto asrc = [&](uint32_t s) {  // this wave's batch of sub-tile s: [k-half][rep half][lane]
-    return a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256;
-  };
   auto dma = [&](int buf, uint32_t s) {
     const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct) * kSubUnits;  // B: 14 KB
 #pragma unroll
@@ -237,45 +237,31 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
       const int piece = t * kWaves + wave;
       oz_dma16(src + piece * 64 + lane, (uint32_t)(buf * kSubUnits + piece * 64) * 16u);
     }
-    if constexpr (LIVE && !AREG) {  // A: one k-half of this wave's batch (the two slice groups split the 4 KB)
-      const ob_v4i* src_a = asrc(s);
-#pragma unroll
-      for (int t = 0; t < kADmaPerWave; ++t) {
-        const int u = (grp * kADmaPerWave + t) * 64;
-        oz_dma16(src_a + u + lane, (uint32_t)(kLdsB + (size_t)(buf * kAUnits + wb * 256 + u) * 16));
-      }
-    }
   };
-  // A fragments held in registers (AREG): three slots, sub-tile s in slot (s - s0) % 3
-  ob_v4i ar[3][2][2];
-  auto aload = [&](ob_v4i (&dst)[2][2], uint32_t s) {
-    const ob_v4i* src_a = asrc(s) + lane;
+  // A fragments in registers: three slots, sub-tile s in slot (s - s0) % 3; this wave's batch of
+  // sub-tile s is 4 x 1 KB, [replicate block][lane]
+  ob_v4i ar[3][4];
+  auto aload = [&](ob_v4i (&dst)[4], uint32_t s) {
+    const ob_v4i* src_a = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256 + lane;
 #pragma unroll
-    for (int k2 = 0; k2 < 2; ++k2)
-#pragma unroll
-      for (int rb = 0; rb < 2; ++rb) dst[k2][rb] = __builtin_nontemporal_load(src_a + (k2 * 2 + rb) * 64);
+    for (int m = 0; m < 4; ++m) dst[m] = __builtin_nontemporal_load(src_a + m * 64);
   };
-  // B fragments (and the LDS A fragments) of half-step (sub-tile in ring stage buf, k-half k2)
-  auto read = [&](int buf, int k2, ob_v4i (&af)[2], ob_v4i (&bf)[kSlo]) {
-    if constexpr (!AREG) {
-      const ob_v4i* ab = as + buf * kAUnits + wb * 256 + k2 * 128 + lane;
-      af[0] = ab[0];
-      af[1] = ab[64];
-    }
-    const ob_v4i* bb = bs + buf * kSubUnits + (slo * 2 + k2) * 64 + lane;
+  // B fragments of half-step h (sub-tile in ring stage buf)
+  auto read = [&](int buf, int h, ob_v4i (&bf)[kSlo]) {
+    const ob_v4i* bb = bs + buf * kSubUnits + (slo * 2 + h) * 64 + lane;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) bf[q] = bb[q * 128];
   };
 
-  ob_v16i acc[2][kSlo];
+  ob_v4i acc[4][kSlo][2];
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb)
+  for (int m = 0; m < 4; ++m)
 #pragma unroll
-    for (int q = 0; q < kSlo; ++q) acc[rb][q] = (ob_v16i){};
+    for (int q = 0; q < kSlo; ++q) acc[m][q][0] = acc[m][q][1] = (ob_v4i){};
   // prologue: B of sub-tiles s0 .. s0 + 3 and A of s0 .. s0 + 2 in flight; publish s0
   // (A loads unconditional, clamped to the last sub-tile, so that the three register slots are
   // loaded in the same order on entry to the loop as on its back edge)
-  if constexpr (LIVE && AREG) {
+  if constexpr (LIVE) {
     aload(ar[0], s0);
     aload(ar[1], min(s0 + 1, s1 - 1));
     aload(ar[2], min(s0 + 2, s1 - 1));
@@ -283,11 +269,10 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
 #pragma unroll
   for (int j = 0; j < kNbuf; ++j)
     if (s0 + j < s1) dma(j, s0 + j);
-  // every prologue load is waited for: simple, and once per block
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every prologue load: once per block
   __syncthreads();
-  ob_v4i fa0[2], fb0[kSlo], fa1[2], fb1[kSlo];
-  if constexpr (LIVE) read(0, 0, fa0, fb0);
+  ob_v4i fb0[kSlo], fb1[kSlo];
+  if constexpr (LIVE) read(0, 0, fb0);
 
   // Half-step (s, 0): read (s, 1); MFMAs on (s, 0). Barrier B_s: sub-tile s + 1 landed (own loads,
   // then everyone's), every read of sub-tile s done. Refill stage s with B of s + 4. Half-step
@@ -300,12 +285,9 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
     constexpr int j = decltype(J)::value;
     const int buf = (int)((s - s0) & (kNbuf - 1));
     if constexpr (LIVE) {
-      read(buf, 1, fa1, fb1);
+      read(buf, 1, fb1);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!(DIAG & 2)) {
-        if constexpr (AREG) oz_mfmas<NQ>(acc, ar[j][0], fb0);
-        else oz_mfmas<NQ>(acc, fa0, fb0);
-      }
+      if constexpr (!(DIAG & 2)) oz_mfmas<NQ>(acc, 0, ar[j], fb0);
       __builtin_amdgcn_sched_barrier(0);
     }
     const uint32_t ahead = (DIAG & 4) ? 0u : s1 - 1 - s;  // sub-tiles after s
@@ -314,16 +296,13 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
     oz_barrier();
     if (!(DIAG & 4) && s + kNbuf < s1) dma(buf, s + kNbuf);
     if constexpr (LIVE) {
-      read((buf + 1) & (kNbuf - 1), 0, fa0, fb0);
+      read((buf + 1) & (kNbuf - 1), 0, fb0);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!(DIAG & 2)) {
-        if constexpr (AREG) oz_mfmas<NQ>(acc, ar[j][1], fb1);
-        else oz_mfmas<NQ>(acc, fa1, fb1);
-      }
+      if constexpr (!(DIAG & 2)) oz_mfmas<NQ>(acc, 1, ar[j], fb1);
       __builtin_amdgcn_sched_barrier(0);
       // unconditional (past the end: a re-read of the last sub-tile, never used), so the compiler's
       // count of outstanding A loads is exact at every MFMA
-      if constexpr (AREG && !(DIAG & 4)) aload(ar[j], min(s + 3, s1 - 1));
+      if constexpr (!(DIAG & 4)) aload(ar[j], min(s + 3, s1 - 1));
     }
   };
   uint32_t s = s0;
@@ -336,44 +315,56 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   if (s + 1 < s1) step(s + 1, IC<1>{});
   // slices -> f64: this wave's digits meet exactly in int64, one ldexp each; group 1 goes through
   // LDS to its group-0 partner, which adds (one rounding) and stores.
-  const int pair = ct * kPairsPerTile + (lane & 31);
-  const int E = a.pexp[chunk * a.n_pairs_pad + min(pair, a.n_pairs_pad - 1)];
-  const int shift = E - kFracBits + 8 * (kS - slo - NQ);  // weight of this group's last slice
-  double v[2][16];
+  int E[2];
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb)
+  for (int h = 0; h < 2; ++h) {
+    const int pair = ct * kPairsPerTile + 16 * h + (lane & 15);
+    E[h] = a.pexp[chunk * a.n_pairs_pad + min(pair, a.n_pairs_pad - 1)];
+  }
+  double v[4][2][4];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      long long part = 0;
+  for (int m = 0; m < 4; ++m)
 #pragma unroll
-      for (int q = 0; q < NQ; ++q) part = part * 256 + acc[rb][q][r];
-      v[rb][r] = ldexp((double)part, shift);
+    for (int h = 0; h < 2; ++h) {
+      const int shift = E[h] - kFracBits + 8 * (kS - slo - NQ);  // weight of this group's last slice
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        long long part = 0;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) part = part * 256 + acc[m][q][h][i];
+        v[m][h][i] = ldexp((double)part, shift);
+      }
     }
-  __syncthreads();  // every wave is done with the rings: the exchange overlays them
+  __syncthreads();  // every wave is done with the ring: the exchange overlays it
   double* xch = reinterpret_cast<double*>(smem);  // [batch in tile][64 reps][32 pairs]
   if (grp) {
 #pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
+    for (int m = 0; m < 4; ++m)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int rl = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        xch[(wb * 64 + rl) * kPairsPerTile + (lane & 31)] = v[rb][r];
-      }
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          xch[(wb * 64 + 16 * m + 4 * (lane >> 4) + i) * kPairsPerTile + 16 * h + (lane & 15)] = v[m][h][i];
   }
   __syncthreads();
-  if (grp || !LIVE || pair >= a.e_pad) return;
+  if (grp || !LIVE) return;
 #pragma unroll
-  for (int rb = 0; rb < 2; ++rb)
+  for (int h = 0; h < 2; ++h) {
+    const int pair = ct * kPairsPerTile + 16 * h + (lane & 15);
+    if (pair >= a.e_pad) continue;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int rl = rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-      const uint32_t rep = batch * 64u + (uint32_t)rl;
-      const double val = v[rb][r] + xch[(wb * 64 + rl) * kPairsPerTile + (lane & 31)];
-      if (rep < a.n_reps) a.partial[((size_t)chunk * a.rep_pad + rep) * a.e_pad + pair] = val;
-    }
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rl = 16 * m + 4 * (lane >> 4) + i;
+        const uint32_t rep = batch * 64u + (uint32_t)rl;
+        const double val = v[m][h][i] + xch[(wb * 64 + rl) * kPairsPerTile + 16 * h + (lane & 15)];
+        if (rep < a.n_reps) a.partial[((size_t)chunk * a.rep_pad + rep) * a.e_pad + pair] = val;
+      }
+  }
 }
 
-template <bool AREG, int DIAG>
+template <int DIAG>
 __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -385,14 +376,14 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
   const bool live = rt * 4u + (uint32_t)(wave & 3) < a.nb_rep;
   // waves 0-3: slices 0-3, two B pieces; 4-5: slices 4-6, two B pieces; 6-7: slices 4-6, one piece
   if (wave < 4) {
-    if (live) oz_gram_body<kSlo, 2, true, AREG, DIAG>(a, smem, wave);
-    else oz_gram_body<kSlo, 2, false, AREG, DIAG>(a, smem, wave);
+    if (live) oz_gram_body<kSlo, 2, true, DIAG>(a, smem, wave);
+    else oz_gram_body<kSlo, 2, false, DIAG>(a, smem, wave);
   } else if (wave < 6) {
-    if (live) oz_gram_body<kS - kSlo, 2, true, AREG, DIAG>(a, smem, wave);
-    else oz_gram_body<kS - kSlo, 2, false, AREG, DIAG>(a, smem, wave);
+    if (live) oz_gram_body<kS - kSlo, 2, true, DIAG>(a, smem, wave);
+    else oz_gram_body<kS - kSlo, 2, false, DIAG>(a, smem, wave);
   } else {
-    if (live) oz_gram_body<kS - kSlo, 1, true, AREG, DIAG>(a, smem, wave);
-    else oz_gram_body<kS - kSlo, 1, false, AREG, DIAG>(a, smem, wave);
+    if (live) oz_gram_body<kS - kSlo, 1, true, DIAG>(a, smem, wave);
+    else oz_gram_body<kS - kSlo, 1, false, DIAG>(a, smem, wave);
   }
 }
 
@@ -492,10 +483,6 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
     const char* e = getenv("OB_GRAM_DIAG");
     return e ? atoi(e) & 6 : 0;
   }();
-  static const bool areg = [] {  // OB_OZ_AREG=0: A fragments through the LDS ring (measurement)
-    const char* e = getenv("OB_OZ_AREG");
-    return !(e && e[0] == '0');
-  }();
   const uint32_t blocks = (uint32_t)n_chunks * a.n_rt * (uint32_t)a.n_ct;
   auto launch = [&](auto kern) -> hipError_t {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
@@ -503,15 +490,11 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(kWaves * 64), kLdsBytes, s, a);
     return hipGetLastError();
   };
-  switch (diag + (areg ? 8 : 0)) {
-    case 2: OZ_HIP(launch(oz_gram_kernel<false, 2>)); break;
-    case 4: OZ_HIP(launch(oz_gram_kernel<false, 4>)); break;
-    case 6: OZ_HIP(launch(oz_gram_kernel<false, 6>)); break;
-    case 0: OZ_HIP(launch(oz_gram_kernel<false, 0>)); break;
-    case 10: OZ_HIP(launch(oz_gram_kernel<true, 2>)); break;
-    case 12: OZ_HIP(launch(oz_gram_kernel<true, 4>)); break;
-    case 14: OZ_HIP(launch(oz_gram_kernel<true, 6>)); break;
-    default: OZ_HIP(launch(oz_gram_kernel<true, 0>)); break;
+  switch (diag) {
+    case 2: OZ_HIP(launch(oz_gram_kernel<2>)); break;
+    case 4: OZ_HIP(launch(oz_gram_kernel<4>)); break;
+    case 6: OZ_HIP(launch(oz_gram_kernel<6>)); break;
+    default: OZ_HIP(launch(oz_gram_kernel<0>)); break;
   }
   return OB_OK;
 }
