@@ -161,6 +161,9 @@ typedef struct {
   double mm_ms;              /* ob_mm_run: whole call, host clock */
   double gather_ms;          /* sharded runs: the RCCL all-gather of the per-replicate rows (HIP events) */
   int32_t gram_path;         /* last boot run: 1 = f64 MFMA Gram, 2 = exact integer-sliced i8 MFMA Gram */
+  double probit_ms;          /* Heckman panels: ob_probit_kernel time (HIP events), summed over iterations */
+  int32_t probit_launches;   /* Heckman panels: ob_probit_kernel launches in those ms */
+  double heck_sums_ms;       /* Heckman panels: ob_heck_sums_kernel (IMR sums) time */
 } ob_timing;
 int ob_panel_last_timing(const ob_panel* panel, ob_timing* out);
 /* Synchronize the stream used by the last *_device call and collect its timings. */

@@ -11,7 +11,8 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liboaxaca_boot.so")
+# OB_LIB_PATH: an alternative build for A/B timing runs (tools/build_alt.sh); never set in tests.
+LIB_PATH = os.environ.get("OB_LIB_PATH") or os.path.join(_HERE, "liboaxaca_boot.so")
 
 OB_OK = 0
 OB_E_POLARS, OB_E_COLUMN, OB_E_GROUP, OB_E_LINALG, OB_E_DIAG, OB_E_INSUFFICIENT = 1, 2, 3, 4, 5, 6
@@ -72,7 +73,8 @@ class ob_timing(C.Structure):
                 ("blocks", C.c_int32), ("counts_ms", C.c_double),
                 ("heckman_ms", C.c_double), ("probit_iterations", C.c_int32),
                 ("mm_assemble_ms", C.c_double), ("mm_fit_rows", C.c_double), ("mm_iterations", C.c_int32),
-                ("mm_ms", C.c_double), ("gather_ms", C.c_double), ("gram_path", C.c_int32)]
+                ("mm_ms", C.c_double), ("gather_ms", C.c_double), ("gram_path", C.c_int32),
+                ("probit_ms", C.c_double), ("probit_launches", C.c_int32), ("heck_sums_ms", C.c_double)]
 
 
 class ob_unique_id(C.Structure):

@@ -1279,14 +1279,13 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   OB_TRY(ensure_buf(&p->d_chunks, p->cap_chunks, std::max(pl.chunks.size(), pl_tail.chunks.size())));
   if (p->heckman) OB_TRY(ensure_heck(p, pl));
   // Gram path: the exact integer-sliced i8 GEMM (ob_gram_i8.hip) unless forced to f64 MFMA
-  // (OB_GRAM_PATH=f64), a Heckman panel (its kernels read the f64 path's count images), or the
-  // digit images do not fit.
+  // (OB_GRAM_PATH=f64) or the digit images do not fit. Heckman's kernels read either image layout.
   int force = p->gram_force;
   if (!force) {
     const char* ev = getenv("OB_GRAM_PATH");
     force = ev && !strcmp(ev, "f64") ? 1 : (ev && !strcmp(ev, "i8") ? 2 : 0);
   }
-  bool use_i8 = !p->heckman && force != 1;
+  bool use_i8 = force != 1;
   if (use_i8) {
     OB_TRY(ob::oz_prepare(p, pl.chunks));
     use_i8 = p->oz_state == 1;
@@ -1363,13 +1362,18 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     if (p->heckman) {  // probit iterations + IMR sums + two-step solve (synchronizes the stream)
       ob_heck_seg hs = heck_seg(p, plx, p->d_chunks, p->d_gram, ref_mode);
       hs.counts = p->d_counts;
+      hs.counts_i8 = use_i8 ? 1 : 0;
       hs.n_reps = ns;
       hs.rows = d_rows + s0 * p->row_len;
       hs.ok = d_ok + s0;
       hs.raw_status = (diag_mode() & 8) ? 1 : 0;  // OB_GRAM_DIAG bit 8: ok[] = ob_heck_status codes
       int it = 0;
-      OB_TRY(ob::heckman_segment(hs, s, &it));
+      ob::ob_heck_times ht;
+      OB_TRY(ob::heckman_segment(hs, s, &it, &ht));
       p->timing.probit_iterations = std::max(p->timing.probit_iterations, it);
+      p->timing.probit_ms += ht.probit_ms;
+      p->timing.probit_launches += ht.probit_launches;
+      p->timing.heck_sums_ms += ht.sums_ms;
     }
     for (int t = 0; t < p->n_y && !p->heckman; ++t) {  // outcome-major row blocks
       SolveArgs sa = solve_args(p, ref_mode);

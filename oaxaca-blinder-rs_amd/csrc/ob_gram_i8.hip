@@ -51,6 +51,12 @@ constexpr int kFracBits = 54;          // m = rint(P 2^(kFracBits - E))
 constexpr int kPairsPerTile = 32;      // pairs per column tile (one 32-wide MFMA column block)
 constexpr int kSubUnits = kS * 2 * 64; // 16-byte units of one (sub-tile, column tile) B image (14 KB)
 constexpr int kSlo = 4;                // slices of slice group 0 (waves 0-3); group 1 has kS - kSlo
+#ifndef OB_OZ_A_NT
+// A fragments by ordinary loads, so that the 8 column-tile blocks of a (chunk, replicate tile),
+// which run together on one XCD, share them through its L2. Nontemporal loads (OB_OZ_A_NT=1,
+// tools/build_alt.sh) measured 14.6 ms per Gram launch against 13.4 ms at configs[1].
+#define OB_OZ_A_NT 0
+#endif
 
 #define OZ_HIP(expr)                                                                                  \
   do {                                                                                                \
@@ -244,7 +250,7 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   auto aload = [&](ob_v4i (&dst)[4], uint32_t s) {
     const ob_v4i* src_a = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256 + lane;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) dst[m] = __builtin_nontemporal_load(src_a + m * 64);
+    for (int m = 0; m < 4; ++m) dst[m] = OB_OZ_A_NT ? __builtin_nontemporal_load(src_a + m * 64) : src_a[m * 64];
   };
   // B fragments of half-step h (sub-tile in ring stage buf)
   auto read = [&](int buf, int h, ob_v4i (&bf)[kSlo]) {

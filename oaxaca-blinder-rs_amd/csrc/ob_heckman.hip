@@ -77,11 +77,23 @@ __device__ __forceinline__ Lanes lanes(const ob_heck_seg& a) {
   return l;
 }
 
-// This lane's count words for the wave's sub-tile of a tile (NULL: every row once).
+// This lane's count words for the wave's sub-tile of a tile (NULL: every row once). f64 Gram
+// images: 16 consecutive words at lane * 17. I8 images (ob_count_kernel<true>, the A fragments of
+// ob_gram_i8.hip: per sub-tile [16-replicate block][lane][16 B], lane = replicate 16 m + (l & 15),
+// rows 16 (l >> 4) + j): the lane's rows 16 q .. 16 q + 15 are the 16-byte unit 16 q past the
+// returned one (count_word).
 __device__ __forceinline__ const uint32_t* count_row(const ob_heck_seg& a, const Lanes& l, uint32_t tile) {
   if (!a.counts) return nullptr;
   const size_t tt = (l.g ? a.tiles0 : 0u) + tile;
+  if (a.counts_i8)
+    return a.counts + ((tt * a.nb_rep + l.rb) * 1024 + l.wave * 256 + (l.lane >> 4) * 64 + (l.lane & 15)) * 4;
   return a.counts + ((tt * a.nb_rep + l.rb) * 4 + l.wave) * kCimgWords + l.lane * kCimgStride;
+}
+
+// Count bytes of the lane's rows ri .. ri + 3 of its sub-tile (ri % 4 == 0).
+__device__ __forceinline__ uint32_t count_word(const ob_heck_seg& a, const uint32_t* cw, uint32_t ri) {
+  if (!cw) return 0x01010101u;
+  return a.counts_i8 ? cw[(ri >> 4) * 64 + ((ri >> 2) & 3u)] : cw[ri >> 2];
 }
 
 // Fixed-order block sum of acc over the 4 waves into LDS row `lane` (wave 3 + 2 + 1, then + 0).
@@ -138,7 +150,7 @@ __global__ __launch_bounds__(kHB) void ob_probit_kernel(const ob_heck_seg a) {
     const uint32_t* cw = count_row(a, l, tile);
     uint32_t word = 0;
     for (uint32_t ri = 0; ri < nr; ++ri) {
-      if ((ri & 3) == 0) word = cw ? cw[ri >> 2] : 0x01010101u;
+      if ((ri & 3) == 0) word = count_word(a, cw, ri);
       const uint32_t cu = (word >> ((ri & 3) * 8)) & 255u;
       if (!act || cu == 0) continue;
       const double c = (double)cu;
@@ -356,7 +368,7 @@ __global__ __launch_bounds__(kHB) void ob_heck_sums_kernel(const ob_heck_seg a) 
     const uint32_t* cw = count_row(a, l, tile);
     uint32_t word = 0;
     for (uint32_t ri = 0; ri < nr; ++ri) {
-      if ((ri & 3) == 0) word = cw ? cw[ri >> 2] : 0x01010101u;
+      if ((ri & 3) == 0) word = count_word(a, cw, ri);
       const uint32_t cu = (word >> ((ri & 3) * 8)) & 255u;
       if (!act || cu == 0) continue;
       const double c = (double)cu;
@@ -534,24 +546,26 @@ __global__ __launch_bounds__(64) void ob_heck_solve_kernel(const ob_heck_seg a) 
 }
 
 template <int KS>
-hipError_t launch_probit_iter(const ob_heck_seg& a, hipStream_t s) {
+hipError_t launch_probit_iter(const ob_heck_seg& a, hipStream_t s, hipEvent_t* ev) {
+  if (ev) (void)hipEventRecord(ev[0], s);
   hipLaunchKernelGGL(ob_probit_kernel<KS>, dim3(a.n_chunks, a.rep_pad / 64), dim3(kHB), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (ev) (void)hipEventRecord(ev[1], s);
   hipLaunchKernelGGL(ob_probit_step_kernel<KS>, dim3(a.rep_pad / 64, 2), dim3(64), 0, s, a);
   return hipGetLastError();
 }
 
-hipError_t probit_iter(const ob_heck_seg& a, hipStream_t s) {
+hipError_t probit_iter(const ob_heck_seg& a, hipStream_t s, hipEvent_t* ev) {
   switch (a.ks) {
-    case 1: return launch_probit_iter<1>(a, s);
-    case 2: return launch_probit_iter<2>(a, s);
-    case 3: return launch_probit_iter<3>(a, s);
-    case 4: return launch_probit_iter<4>(a, s);
-    case 5: return launch_probit_iter<5>(a, s);
-    case 6: return launch_probit_iter<6>(a, s);
-    case 7: return launch_probit_iter<7>(a, s);
-    default: return launch_probit_iter<8>(a, s);
+    case 1: return launch_probit_iter<1>(a, s, ev);
+    case 2: return launch_probit_iter<2>(a, s, ev);
+    case 3: return launch_probit_iter<3>(a, s, ev);
+    case 4: return launch_probit_iter<4>(a, s, ev);
+    case 5: return launch_probit_iter<5>(a, s, ev);
+    case 6: return launch_probit_iter<6>(a, s, ev);
+    case 7: return launch_probit_iter<7>(a, s, ev);
+    default: return launch_probit_iter<8>(a, s, ev);
   }
 }
 
@@ -559,19 +573,34 @@ hipError_t probit_iter(const ob_heck_seg& a, hipStream_t s) {
 
 namespace ob {
 
-int heckman_segment(const ob_heck_seg& a, hipStream_t s, int* iters) {
+int heckman_segment(const ob_heck_seg& a, hipStream_t s, int* iters, ob_heck_times* tm) {
   if (a.ks < 1 || a.ks > kHeckMaxKs || a.p > kHeckMaxP || a.rep_pad % 64 != 0)
     return ob::fail(OB_E_INVALID, "heckman segment: bad shape");
+  struct Events {  // [0, 1] around each probit pass, [2, 3] around the sums pass
+    hipEvent_t e[4] = {};
+    ~Events() {
+      for (hipEvent_t x : e)
+        if (x) (void)hipEventDestroy(x);
+    }
+  } ev;
+  if (tm)
+    for (hipEvent_t& x : ev.e) HK_OK(hipEventCreate(&x));
   HK_OK(hipMemsetAsync(a.gamma, 0, sizeof(double) * 2 * a.rep_pad * a.ks, s));
   HK_OK(hipMemsetAsync(a.hflags, 0, sizeof(uint32_t) * 2 * a.rep_pad, s));
   int it = 0;
   while (it < a.max_iter) {  // probit.rs:48-147, each replicate stopping on its own
     HK_OK(hipMemsetAsync(a.active, 0, sizeof(uint32_t), s));
-    HK_OK(probit_iter(a, s));
+    HK_OK(probit_iter(a, s, tm ? ev.e : nullptr));
     ++it;
     uint32_t active = 0;
     HK_OK(hipMemcpyAsync(&active, a.active, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     HK_OK(hipStreamSynchronize(s));
+    if (tm) {
+      float ms = 0.f;
+      HK_OK(hipEventElapsedTime(&ms, ev.e[0], ev.e[1]));
+      tm->probit_ms += ms;
+      tm->probit_launches += 1;
+    }
     if (active == 0) break;
   }
   if (iters) *iters = it;
@@ -583,6 +612,7 @@ int heckman_segment(const ob_heck_seg& a, hipStream_t s, int* iters) {
   const void* fn = nb == 32 ? (const void*)ob_heck_sums_kernel<32>
                             : (nb == 40 ? (const void*)ob_heck_sums_kernel<40> : (const void*)ob_heck_sums_kernel<64>);
   HK_OK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sums));
+  if (tm) HK_OK(hipEventRecord(ev.e[2], s));
   if (nb == 32)
     hipLaunchKernelGGL(ob_heck_sums_kernel<32>, grid, dim3(kHB), lds_sums, s, a);
   else if (nb == 40)
@@ -590,10 +620,17 @@ int heckman_segment(const ob_heck_seg& a, hipStream_t s, int* iters) {
   else
     hipLaunchKernelGGL(ob_heck_sums_kernel<64>, grid, dim3(kHB), lds_sums, s, a);
   HK_OK(hipGetLastError());
+  if (tm) HK_OK(hipEventRecord(ev.e[3], s));
   const size_t lds = heck_solve_lds(a);
   HK_OK(hipFuncSetAttribute((const void*)ob_heck_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   hipLaunchKernelGGL(ob_heck_solve_kernel, dim3(a.n_reps), dim3(64), lds, s, a);
   HK_OK(hipGetLastError());
+  if (tm) {  // the events die with this call: read the sums pass now
+    float ms = 0.f;
+    HK_OK(hipEventSynchronize(ev.e[3]));
+    HK_OK(hipEventElapsedTime(&ms, ev.e[2], ev.e[3]));
+    tm->sums_ms += ms;
+  }
   return OB_OK;
 }
 

@@ -15,6 +15,7 @@ struct ob_heck_seg {
   int p, ks, weighted;  // ks = 1 + selection predictors; weighted: the w column is present
   // resampling: level-2 count images (NULL = every row once: the point estimate) and chunks
   const uint32_t* counts;
+  int counts_i8;  // 1: the i8 Gram's A-fragment images (ob_count_kernel<true>), 0: the f64 Gram's
   uint32_t nb_rep;
   const uint32_t* chunks;
   int n_chunks;
@@ -53,7 +54,14 @@ __host__ __device__ inline int heck_probit_len(int ks) { return ks * (ks + 1) / 
 __host__ __device__ inline int heck_row_len(int k, int ks) { return 6 + 7 * (k + 1) + ks; }
 // Largest p the register-resident sums kernel takes (13 + K <= 64).
 constexpr int kHeckMaxP = 50;
+// Kernel timings of one segment (HIP events on the segment's stream).
+struct ob_heck_times {
+  double probit_ms = 0.0;  // ob_probit_kernel, summed over the iterations
+  int probit_launches = 0;
+  double sums_ms = 0.0;    // ob_heck_sums_kernel
+};
 // Runs the probit iterations, the IMR sums and the two-step solve for one segment; on return
-// (after a stream sync) rows/ok are final. iters: the probit iterations run.
-int heckman_segment(const ob_heck_seg& h, hipStream_t s, int* iters);
+// (after a stream sync) rows/ok are final. iters: the probit iterations run; tm (optional): the
+// kernel timings, added to.
+int heckman_segment(const ob_heck_seg& h, hipStream_t s, int* iters, ob_heck_times* tm = nullptr);
 }  // namespace ob

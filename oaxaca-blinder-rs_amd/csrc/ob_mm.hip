@@ -10,9 +10,9 @@
 // statement of the same iteration). The start is primal and dual feasible (x = (1 - tau) c, beta =
 // weighted OLS, z - w = X beta - y), so every iteration only drives the complementarity gap.
 //
-// Layout: lane = fit (64 quantiles of one replicate and group per wave), so a row's design values
-// are wave-uniform (scalar loads) and the per-(fit, row) state [row][fit] is read coalesced.
-// Per iteration, three passes over the rows, each writing per-(chunk, fit) partials that are
+// Layout: lane = (fit, list row) in the A-fragment shape of v_mfma_f64_16x16x4 (below); the IPM
+// state (x, z, w) is stored per (fit, entry of the replicate's nonzero-row list), so every pass
+// streams it as dense 512-byte wave loads (state_at). Per iteration, three passes over the rows, each writing per-(chunk, fit) partials that are
 // reduced in a fixed chunk order (bitwise reproducible), and one-wave-per-fit solves:
 //   mm_assemble<K>   (apply the last step,) M = X'QX, X'Q r, gap, objective
 //   mm_affine<K>     affine direction: step-length bounds, mu_aff terms, corrector right-hand sides
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256) void mm_rows_kernel(const MmArgs a) {
 struct Blk {
   uint32_t g, gch, slot, fb, r0, n_ent;
   int wave, lane, fl, rl, s;
-  size_t F, sb;  // fit index; state index of (fit, group row 0)
+  size_t F, sb;  // fit index; state index of (this lane's fit, list entry 0)
   bool live, wave_live, any;  // any: some fit of the block is live (else the block exits)
   const double* X;
   int64_t ld;
@@ -183,8 +183,8 @@ __device__ __forceinline__ Blk blk_ctx(const MmArgs& a, uint32_t* lst, bool all_
   b.wave_live = __ballot(b.live) != 0;
   b.X = a.cols[b.g];
   b.ld = a.ld[b.g];
-  b.sb = ((size_t)b.slot * a.rep_rows + (b.g ? a.n[0] : 0u)) * a.S_pad + b.s;
   const size_t li = (size_t)b.slot * (a.nch[0] + a.nch[1]) + b.gch;
+  b.sb = (li * (a.S_pad / 64) + b.fb) * ((size_t)kRc * 64) + b.wave * 64 + b.fl;
   b.any = __syncthreads_or(b.live) != 0;
   b.n_ent = b.any ? a.nrows[li] : 0u;
   const uint32_t* L = a.rowlist + li * kRc;
@@ -220,9 +220,13 @@ __device__ __forceinline__ void xs_store(double* xs, const double (&v)[Xs<K>::St
   }
 }
 
-// State index of this lane's (fit, row) for list row e (clamped to the list).
-__device__ __forceinline__ size_t state_at(const MmArgs& a, const Blk& b, const uint32_t* lst, uint32_t e) {
-  return b.sb + (size_t)(b.r0 + (lst[min(e, b.n_ent - 1)] >> 8)) * a.S_pad;
+// State index of this lane's fit at list entry e (clamped to the list). The state is stored by
+// list entry, not by row, in units of 4 entries x the block's 64 fits: [slot][chunk][fit block]
+// [entry / 4][wave][entry % 4][fit % 16], so a wave step (4 entries x 16 fits) is one contiguous
+// 512-byte load and a block streams one dense region per pass.
+__device__ __forceinline__ size_t state_at(const Blk& b, uint32_t e) {
+  e = min(e, b.n_ent - 1);
+  return b.sb + (size_t)(e >> 2) * 256 + (e & 3u) * 16;
 }
 
 // Sum (or min) over the 4 row lanes of each fit (lanes fl, fl + 16, fl + 32, fl + 48).
@@ -392,7 +396,7 @@ __global__ __launch_bounds__(256, K <= 16 ? 2 : 1) void mm_assemble_mfma_kernel(
     double rx[kRingA], rz[kRingA], rw[kRingA];
     auto load = [&](int k, uint32_t e) {
       if (STEP) {
-        const size_t si = state_at(a, b, lst, e);
+        const size_t si = state_at(b, e);
         rx[k] = a.x[si];
         rz[k] = a.z[si];
         rw[k] = a.w[si];
@@ -437,7 +441,7 @@ __global__ __launch_bounds__(256, K <= 16 ? 2 : 1) void mm_assemble_mfma_kernel(
                 wv = cw + ad * d.dw;
                 r = f.r - ad * xdb;  // y - x_i . (bprev + ad db)
               }
-              const size_t si = b.sb + (size_t)(b.r0 + (lst[e] >> 8)) * a.S_pad;
+              const size_t si = state_at(b, e);
               a.x[si] = xv;
               a.z[si] = zv;
               a.w[si] = wv;
@@ -501,7 +505,7 @@ __device__ __forceinline__ void state_walk(const MmArgs& a, const Blk& b, const 
   xs_store<K>(xs[0], stg);
   double rx[kRing], rz[kRing], rw[kRing];
   auto load = [&](int k, uint32_t e) {
-    const size_t si = state_at(a, b, lst, e);
+    const size_t si = state_at(b, e);
     rx[k] = a.x[si];
     rz[k] = a.z[si];
     rw[k] = a.w[si];
@@ -1054,10 +1058,14 @@ void pass(int K, int which, const MmArgs& a, dim3 grid, int mode, hipStream_t s)
   switch (K) {
 #define OB_MM_K(k) \
   case k: launch_pass<k>(which, a, grid, mode, s); break;
+#ifdef OB_MM_ISA_K  // ISA inspection builds (tools/mm_isa.sh): one width only
+    OB_MM_K(OB_MM_ISA_K)
+#else
     OB_MM_K(1) OB_MM_K(2) OB_MM_K(3) OB_MM_K(4) OB_MM_K(5) OB_MM_K(6) OB_MM_K(7) OB_MM_K(8)
     OB_MM_K(9) OB_MM_K(10) OB_MM_K(11) OB_MM_K(12) OB_MM_K(13) OB_MM_K(14) OB_MM_K(15) OB_MM_K(16)
     OB_MM_K(17) OB_MM_K(18) OB_MM_K(19) OB_MM_K(20) OB_MM_K(21) OB_MM_K(22) OB_MM_K(23) OB_MM_K(24)
     OB_MM_K(25) OB_MM_K(26) OB_MM_K(27) OB_MM_K(28) OB_MM_K(29) OB_MM_K(30) OB_MM_K(31) OB_MM_K(32)
+#endif
 #undef OB_MM_K
     default: break;
   }
@@ -1242,8 +1250,10 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   const uint32_t nch0 = (p->n[0] + kRc - 1) / kRc, nch1 = (p->n[1] + kRc - 1) / kRc;
   if (nch0 > 1024 || nch1 > 1024)  // mm_shift_kernel's chunk prefix
     return ob::fail(OB_E_UNSUPPORTED, "Machado-Mata groups take at most %u rows", 1024u * kRc);
-  // replicate slots per batch: IPM state (x, z, w: 3 f64 per fit and row) within 48 GB
-  const size_t state_per_rep = 3 * rep_rows * S_pad * sizeof(double);
+  // replicate slots per batch: IPM state (x, z, w: 3 f64 per fit and list entry, kRc entries per
+  // chunk) within 48 GB
+  const size_t state_rows = (size_t)(nch0 + nch1) * kRc;
+  const size_t state_per_rep = 3 * state_rows * S_pad * sizeof(double);
   const uint64_t want = std::max<uint64_t>(n_reps, 1);
   const uint32_t rb_cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({want, 256, (48ull << 30) / state_per_rep}));
   const size_t fits = (size_t)rb_cap * 2 * S_pad;
@@ -1253,7 +1263,7 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
     p->mm_ws_free = free_workspace;
   }
   Buffers& b = *static_cast<Buffers*>(p->mm_ws);
-  const size_t st_elems = (size_t)rb_cap * rep_rows * S_pad;
+  const size_t st_elems = (size_t)rb_cap * state_rows * S_pad;
   const uint32_t nt1 = (p->n[1] + OB_TILE_ROWS - 1) / OB_TILE_ROWS;
   const size_t d8 = sizeof(double), u4 = sizeof(uint32_t);
   const size_t need[Buffers::kSlots] = {d8 * st_elems, d8 * st_elems, d8 * st_elems, d8 * fits * K,
