@@ -30,6 +30,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 F64_MFMA_PEAK_TFLOPS = 78.6  # MI355X dense FP64 matrix peak (v_mfma_f64_16x16x4_f64, 2.4 GHz)
+F64_VALU_PEAK_TFLOPS = 78.6  # MI355X FP64 vector peak (spec): 32 FLOP/clk/SIMD, the same rate as the f64 MFMA
 I8_MFMA_PEAK_TOPS = 5000.0  # dense I8 MFMA: 2x the ~2.5 PF dense BF16 rate per clock (MI355X_MICROARCH.md, Matrix cores)
 OZ_SLICES = 7  # ob_gram_i8.hip: balanced 8-bit digits per pair product (54-bit fixed point)
 OZ_PAIRS_PER_TILE = 32
@@ -260,13 +261,15 @@ def bench_heckman(args, world, rank, local, dist):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    tm_sum = {"gram_ms": 0.0, "heckman_ms": 0.0, "level1_ms": 0.0, "counts_ms": 0.0}
-    iters = 0
+    tm_sum = {"gram_ms": 0.0, "heckman_ms": 0.0, "probit_ms": 0.0, "heck_sums_ms": 0.0, "level1_ms": 0.0,
+              "counts_ms": 0.0}
+    iters, launches = 0, 0
     for i in range(args.steps):
         tm = step(args.warmup + i)
         for k_ in tm_sum:
             tm_sum[k_] += tm[k_]
         iters = max(iters, tm["probit_iterations"])
+        launches += tm["probit_launches"]
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -277,10 +280,11 @@ def bench_heckman(args, world, rank, local, dist):
     if rank != 0:
         pr.close()
         return
-    k = args.preds + 1  # selected-row X'X, X'y: the extended Gram with weight column [s == 1]
-    flops_rep = 2.0 * args.rows * (k * (k + 1) / 2 + k)
-    gram_launch_ms = tm_sum["gram_ms"] / args.steps
-    achieved = flops_rep * B / (gram_launch_ms * 1e-3) / 1e12
+    ks = 1 + len(zs)
+    probit_ms = tm_sum["probit_ms"] / max(1, launches)  # per ob_probit_kernel launch, HIP events
+    pmc = load_probit_pmc(args.rows, args.preds, B, ks)
+    flops_launch = pmc.get("f64_flops_per_dispatch") if pmc else None
+    achieved = flops_launch / (probit_ms * 1e-3) / 1e12 if flops_launch else None
     okh = ok.cpu().numpy()
     out = {
         "metric": "Heckman two-step bootstrap replicates/sec (configs[1] panel + selection equation)",
@@ -291,13 +295,17 @@ def bench_heckman(args, world, rank, local, dist):
         "config": {"workload": "heckman_selection(s, [z1, z2, x4]), GroupA reference coefficients",
                    "rows": args.rows, "predictors": args.preds, "selection_predictors": len(zs),
                    "replicates_per_gpu_per_step": B, "parallelism": f"replicates sharded x{world}"},
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": F64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / F64_MFMA_PEAK_TFLOPS, "traffic": None, "kernel": "ob_gram_kernel",
-                     "avg_launch_ms": gram_launch_ms, "flops_per_replicate": flops_rep},
+        # the dominant kernel: one Fisher-scoring pass of the probit (erfc, exp, reciprocals and the
+        # Hessian/score FMAs per (replicate, row) with a nonzero count), bound by the f64 VALU
+        "roofline": {"bound": "valu-f64", "achieved": achieved, "peak": F64_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / F64_VALU_PEAK_TFLOPS if achieved else None, "traffic": None,
+                     "kernel": f"ob_probit_kernel<{ks}>", "avg_launch_ms": probit_ms, "launches": launches,
+                     "f64_flops_per_launch": flops_launch,
+                     "flops_source": "rocprofv3 SQ_INSTS_VALU_{ADD,MUL,FMA,TRANS}_F64 x 64 lanes "
+                                     "(profiles/pmc_probit.json, tools/pmc_f64.py)",
+                     "share_of_step": tm_sum["probit_ms"] / (elapsed * 1e3)},
         "breakdown_ms_per_step": {k_: v / args.steps for k_, v in tm_sum.items()},
-        "dominant": {"phase": "probit Fisher scoring + IMR sums (ob_probit_kernel, ob_heck_sums_kernel)",
-                     "share_of_step": tm_sum["heckman_ms"] / (elapsed * 1e3),
-                     "bound": "f64 VALU: erfc, exp and a division per live (replicate, row) per iteration"},
+        "gram_path": "i8 MFMA (exact slices)" if tm["gram_path"] == 2 else "f64 MFMA",
         "max_probit_iterations": iters,
         "cpu_baseline": None,
         "check": {"ok_replicates": int(okh.sum()), "explained_mean": float(rows[:, 0].mean().item())},
@@ -341,6 +349,18 @@ def cpu_baseline_heckman(frame, names, zs, target_s, threads):
     return {"value": n / dt, "unit": "replicates/s", **host_info(threads), "kind": "port",
             "sample": f"{n} replicates of the same panel through oracle.heckman_single_pass (numpy), "
                       f"{threads} threads, {dt:.1f} s"}
+
+
+def load_probit_pmc(rows, preds, reps, ks):
+    """f64 FLOPs per ob_probit_kernel launch from the committed PMC summary (tools/pmc_f64.py)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_probit.json")) as f:
+            j = json.load(f)
+        if (j.get("rows"), j.get("preds"), j.get("reps"), j.get("ks")) == (rows, preds, reps, ks):
+            return j
+    except (OSError, ValueError):
+        pass
+    return None
 
 
 def load_traffic(rows, preds, reps, gram_path=1):
