@@ -352,7 +352,7 @@ void ob_matrices_free(ob_matrices* m);
    [first_rep, first_rep + n_reps). rows: (with_point + n_reps) x 3 n_quantiles host doubles,
    [gap, characteristics, coefficients] per quantile; ok[r] = 0 where the pass failed (fewer than
    simulations / 2 successful fits in a group, :231-236). panel: unweighted, one outcome, at most
-   15 predictor columns. Replaces run_single_pass + the bootstrap loop (:173-354). */
+   31 predictor columns. Replaces run_single_pass + the bootstrap loop (:173-354). */
 int ob_mm_run(ob_panel* panel, uint64_t seed, int32_t simulations, const double* quantiles,
               int32_t n_quantiles, uint64_t first_rep, uint64_t n_reps, int32_t with_point, double* rows,
               uint8_t* ok);
