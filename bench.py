@@ -455,29 +455,54 @@ def main():
     per_rank = -(-total // world)
     rl, ny = panel.row_len, panel.n_y
     dev = torch.device("cuda", local)
-    rows = torch.empty((ny * total, rl), dtype=torch.float64, device=dev)
-    ok = torch.empty(ny * total, dtype=torch.uint8, device=dev)
     kd = panel.k + panel.n_base
     ns = 6 + 2 * kd  # every reported component (+ total_gap): the only columns the aggregation reads
     stat_cols = np.arange(ns, dtype=np.int32)
     seed = 0x0B5EED
+    # Two row buffers: step i's replicates run on the GPU while rank 0 aggregates step i - 1's on
+    # the host (builder.rs:841-930 after the loop of :816-839); the component columns come back
+    # on a copy stream, overlapping the next step's kernels.
+    rows = [torch.empty((ny * total, rl), dtype=torch.float64, device=dev) for _ in range(2)]
+    ok = [torch.empty(ny * total, dtype=torch.uint8, device=dev) for _ in range(2)]
+    h_rows = [torch.empty((ny * total, ns), dtype=torch.float64, pin_memory=True) for _ in range(2)]
+    h_ok = [torch.empty(ny * total, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+    copy_stream = torch.cuda.Stream(dev)
+    booted = [torch.cuda.Event() for _ in range(2)]
+    copied = [torch.cuda.Event() for _ in range(2)]
+    pending = []  # buffers whose rows await aggregation on rank 0
+
+    def aggregate(b):  # per outcome: bootstrap_stats over that outcome's block, in replicate order
+        copied[b].synchronize()
+        hr = h_rows[b].numpy().reshape(ny, total, ns)
+        hk = h_ok[b].numpy().reshape(ny, total)
+        return [ob.aggregate(np.ascontiguousarray(hr[t]), np.ascontiguousarray(hk[t]), stat_cols) for t in range(ny)][0]
 
     def step(i):
-        stream = torch.cuda.current_stream(dev).cuda_stream
-        panel.boot_sharded_device(seed, i * total, total, rows.data_ptr(), ok.data_ptr(), args.ref, stream=stream)
-        if rank == 0:  # per outcome: builder.rs:841-930 over that outcome's block, in replicate order
-            h_rows = rows[:, :ns].cpu().numpy().reshape(ny, total, ns)
-            h_ok = ok.cpu().numpy().reshape(ny, total)
-            stats = [ob.aggregate(np.ascontiguousarray(h_rows[t]), np.ascontiguousarray(h_ok[t]), stat_cols)
-                     for t in range(ny)][0]
-        else:
-            torch.cuda.current_stream(dev).synchronize()
-            stats = None
+        b = i % 2
+        cur = torch.cuda.current_stream(dev)
+        cur.wait_event(copied[b])  # step i - 2's copy out of this buffer is done
+        panel.boot_sharded_device(seed, i * total, total, rows[b].data_ptr(), ok[b].data_ptr(), args.ref,
+                                  stream=cur.cuda_stream)
+        stats = None
+        if rank == 0:
+            booted[b].record(cur)
+            with torch.cuda.stream(copy_stream):
+                copy_stream.wait_event(booted[b])
+                h_rows[b].copy_(rows[b][:, :ns], non_blocking=True)
+                h_ok[b].copy_(ok[b], non_blocking=True)
+                copied[b].record(copy_stream)
+            if pending:
+                stats = aggregate(pending.pop())
+            pending.append(b)
         panel.sync()
         return stats, panel.timing()
 
+    def drain():
+        return aggregate(pending.pop()) if pending else None
+
     for i in range(args.warmup):
         step(i)
+    drain()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -487,11 +512,13 @@ def main():
     stats = None
     gram_path = 1
     for i in range(args.steps):
-        stats, tm = step(args.warmup + i)
+        s_, tm = step(args.warmup + i)
+        stats = s_ if s_ is not None else stats
         for k_ in sums:
             sums[k_] += tm[k_]
         launches += tm["gram_launches"]
         gram_path = tm["gram_path"]
+    stats = drain() if rank == 0 else None  # the last step's aggregation, inside the timed region
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -560,7 +587,8 @@ def main():
         else:
             out["cpu_baseline"] = None
         out["check"] = {"explained_se": float(stats[0][0]), "unexplained_se": float(stats[1][0]),
-                        "ok_replicates": int(ok.sum().item()), "quantiles": taus or None}
+                        "ok_replicates": int(ok[(args.warmup + args.steps - 1) % 2].sum().item()),
+                        "quantiles": taus or None}
         print(json.dumps(out), flush=True)
     panel.close()
     if dist:

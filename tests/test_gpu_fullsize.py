@@ -142,3 +142,33 @@ def test_near_singular_failure_rule(ob, O, eps):
         assert resolved == 256 and ok.all()
     if eps <= 1e-7:
         assert resolved == 0  # every replicate is inside the band: no mask comparison is meaningful
+
+
+@pytest.mark.parametrize("ref", [0, 2])
+def test_configs1_scale_normalized_categorical(ob, O, ref):
+    """configs[1] scale with a normalized categorical (normalization.rs:5-51, builder.rs:547-590):
+    1M rows, 15 numeric predictors + a 6-level categorical (5 dummies, normalized), WLS, GroupA
+    and Pooled; every row and the SE/CI/p of every reported column vs the oracle (1e-6)."""
+    n = 1_000_000
+    d = O.synthetic_panel(n, 15, True, seed=31)
+    rng = np.random.default_rng(31)
+    lev_a = rng.integers(0, 6, d["xa"].shape[0])
+    lev_b = np.minimum(rng.integers(0, 7, d["xb"].shape[0]), 5)  # a different level mix in B
+    dum = lambda lv: np.column_stack([lv == j for j in range(1, 6)]).astype(float)
+    xa = np.hstack([d["xa"], dum(lev_a)])
+    xb = np.hstack([d["xb"], dum(lev_b)])
+    norm = {"start": [0, 5], "idx": [16, 17, 18, 19, 20], "m": [6], "pstart": [0, 5],
+            "pidx": [17, 18, 19, 20, 21], "has_base": [1]}
+    panel = ob.Panel(xa, d["ya"], xb, d["yb"], d["wa"], d["wb"], n_num=15, norm=norm)
+    try:
+        rows, ok = panel.boot(SEED, 0, 128, ref)
+    finally:
+        panel.close()
+    cfg = O.PassConfig(21, 15, O.REF_FROM_ENUM[ref], True, norm)
+    orows, ook = O.boot_ref(cfg, O.with_intercept(xa), d["ya"], d["wa"], O.with_intercept(xb), d["yb"], d["wb"],
+                            SEED, 0, 128, threads=_threads(), full=False)
+    assert ook.all()
+    gap = abs(float(np.nanmedian(orows[:, 5])))
+    _stats_close(rows, ok, orows, ook, list(range(orows.shape[1])), gap, ob, O)
+    scale = np.maximum(np.abs(orows), gap)
+    assert np.all(np.abs(rows - orows) <= RTOL * scale)
