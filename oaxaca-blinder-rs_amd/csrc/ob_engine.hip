@@ -38,7 +38,9 @@ constexpr int kBlock = 256;
 constexpr int kCntStride = OB_TILE_ROWS / 4 + 1;  // u32 words per replicate row of the u8 count image (+1 pad)
 constexpr uint64_t kSegReps = 16384;
 constexpr uint64_t kCountBudget = 24ull << 30;  // bytes of level-2 count images per segment
-constexpr int64_t kMaxGroupRows = (160 * 1024 / 4) * (int64_t)OB_TILE_ROWS;  // 40960 tiles: the 160 KB LDS histogram
+// rows per group: 2^20 tiles (level 1 walks groups past 40960 tiles as subtrees, whose LDS
+// buffers are bounded; the count images then cap a segment's replicates via kCountBudget)
+constexpr int64_t kMaxGroupRows = (int64_t)1 << 28;
 constexpr size_t kSegEvents = 6;
 constexpr int kColStride = 96;  // doubles per staged column: 64 rows rotated by (c mod 32), wrap duplicated
 
@@ -85,9 +87,26 @@ struct GramArgs {
 static_assert(kBlock == 256, "level 1 maps 256 threads onto the top tree levels");
 __host__ __device__ inline uint32_t l1_depth(uint32_t ntiles) { return ntiles > 1 ? 32u - __builtin_clz(ntiles - 1) : 0u; }
 __host__ __device__ inline bool l1_small(uint32_t ntiles) { return ntiles <= 256u; }
-__host__ __device__ inline uint32_t l1_buf0_words(uint32_t ntiles) { return l1_small(ntiles) ? 256u : (ntiles + 3) / 4; }
+// Groups of more than kL1FlatTiles tiles run the tree as subtrees of depth kL1SubDepth under the
+// nodes of level J = D - kL1SubDepth (the "top", at most 2^J <= 512 nodes): the per-level LDS
+// buffers then hold one subtree at a time. Node streams depend on (round, level, global index)
+// only, so the order subtrees are walked in does not change a count.
+constexpr uint32_t kL1FlatTiles = 40960;
+constexpr uint32_t kL1SubDepth = 15;
+constexpr uint32_t kL1TopWords = 512;
+__host__ __device__ inline uint32_t l1_top_levels(uint32_t ntiles) {
+  return ntiles > kL1FlatTiles ? l1_depth(ntiles) - kL1SubDepth : 0u;
+}
+__host__ __device__ inline uint32_t l1_sub_tiles(uint32_t ntiles) {
+  return ntiles > kL1FlatTiles ? (1u << kL1SubDepth) : ntiles;
+}
+__host__ __device__ inline uint32_t l1_buf0_words(uint32_t ntiles) {
+  return l1_small(ntiles) ? 256u : (l1_sub_tiles(ntiles) + 3) / 4;
+}
 __host__ __device__ inline uint32_t l1_lds_words(uint32_t ntiles) {
-  return l1_small(ntiles) ? 256u + 128u + 256u : (ntiles + 3) / 4 + (ntiles + 1) / 2;
+  if (l1_small(ntiles)) return 256u + 128u + 256u;
+  const uint32_t t = l1_sub_tiles(ntiles);
+  return (t + 3) / 4 + (t + 1) / 2 + (ntiles > kL1FlatTiles ? 2 * kL1TopWords : 0u);
 }
 
 __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t n1, uint32_t tiles0,
@@ -98,10 +117,11 @@ __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t
   const uint32_t g = blockIdx.y, rl = blockIdx.x, rep = first_rep + rl, tid = threadIdx.x;
   const uint32_t n = g ? n1 : n0;
   if (n == 0) return;
-  const uint32_t T = (n + OB_TILE_ROWS - 1) >> OB_TILE_SHIFT, D = l1_depth(T);
+  const uint32_t T = (n + OB_TILE_ROWS - 1) >> OB_TILE_SHIFT, D = l1_depth(T), J = l1_top_levels(T);
   const uint32_t tail = n - (T - 1) * OB_TILE_ROWS;
   const bool small = l1_small(T), partial = tail < OB_TILE_ROWS;
   uint32_t* buf[2] = {l1s, l1s + l1_buf0_words(T)};
+  uint32_t* top[2] = {buf[1] + (l1_sub_tiles(T) + 1) / 2, buf[1] + (l1_sub_tiles(T) + 1) / 2 + kL1TopWords};
   uint32_t* mt = l1s + 256u + 128u;  // small: running tile counts
   uint32_t* mcol = m1 + (size_t)rl * stride + (g ? tiles0 : 0u);  // [rep][tile]: one row per block
   const uint32_t tail_owner = ((T - 1) >> 1) & (kBlock - 1);
@@ -109,7 +129,8 @@ __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t
   uint32_t todo = n;
   for (uint32_t round = 0;; ++round) {
     if (tid == 0) {
-      buf[D & 1][0] = todo;
+      if (J) top[0][0] = todo;
+      else buf[D & 1][0] = todo;
       s_rej = 0;
       s_tail = 0;
       s_acc = 0;
@@ -122,47 +143,66 @@ __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t
       else if (round == 0) mcol[t] = c;
       else if (c) mcol[t] += c;
     };
-    for (uint32_t l = 0; l < D; ++l) {
-      const uint32_t* cur = buf[(D - l) & 1];
-      uint32_t* nxt = buf[(D - l - 1) & 1];
+    // Level l over `nodes` nodes starting at global index kb (cur: their counts, local index),
+    // children into nxt (local 2k, 2k + 1) or rejected past the last tile; ll = the level within
+    // the current (sub)tree decides the thread mapping (at most 2^ll nodes).
+    auto level = [&](uint32_t l, uint32_t ll, uint32_t kb, uint32_t nodes, const uint32_t* cur, uint32_t* nxt) {
       const uint32_t span = 1u << (D - l - 1);  // tiles per child
-      const uint32_t nodes = (T + 2 * span - 1) / (2 * span), nnext = (T + span - 1) / span;
+      const uint32_t nnext = (T + span - 1) / span;
       const uint32_t tag = OB_TAG_L1T + (round << 5) + l;
-      if (l < 8) {  // nodes <= 2^l: 256 >> l threads per node; never the large last level
-        const uint32_t sh = 8 - l, k = tid >> sh, j = tid & ((1u << sh) - 1);
+      if (ll < 8) {  // nodes <= 2^ll: 256 >> ll threads per node; never the large last level
+        const uint32_t sh = 8 - ll, k = tid >> sh, j = tid & ((1u << sh) - 1);
         if (j == 0 && k < nodes) nxt[2 * k] = 0;
         __syncthreads();
         if (k < nodes) {
           const uint32_t c = cur[k];
           uint32_t left = 0;
-          for (uint32_t q = j; 128 * q < c; q += 1u << sh) left += ob_l1_split_bits(q, c, rep, (k << 1) | g, tag, key0, key1);
+          for (uint32_t q = j; 128 * q < c; q += 1u << sh)
+            left += ob_l1_split_bits(q, c, rep, ((kb + k) << 1) | g, tag, key0, key1);
           if (left) atomicAdd(&nxt[2 * k], left);
         }
         __syncthreads();
         if (j == 0 && k < nodes) {
           const uint32_t c = cur[k], right = c - nxt[2 * k];
-          if (2 * k + 1 < nnext) nxt[2 * k + 1] = right;
+          if (2 * (kb + k) + 1 < nnext) nxt[2 * k + 1] = right;
           else rej += right;
         }
         __syncthreads();
       } else {
         const bool to_m1 = l + 1 == D && !small;
         for (uint32_t k = tid; k < nodes; k += kBlock) {
-          const uint32_t c = cur[k];
+          const uint32_t c = cur[k], kg = kb + k;
           uint32_t left = 0;
-          for (uint32_t q = 0; 128 * q < c; ++q) left += ob_l1_split_bits(q, c, rep, (k << 1) | g, tag, key0, key1);
+          for (uint32_t q = 0; 128 * q < c; ++q) left += ob_l1_split_bits(q, c, rep, (kg << 1) | g, tag, key0, key1);
           const uint32_t right = c - left;
           if (to_m1) {
-            emit(2 * k, left);
-            if (2 * k + 1 < T) emit(2 * k + 1, right);
+            emit(2 * kg, left);
+            if (2 * kg + 1 < T) emit(2 * kg + 1, right);
             else rej += right;
           } else {
             nxt[2 * k] = left;
-            if (2 * k + 1 < nnext) nxt[2 * k + 1] = right;
+            if (2 * kg + 1 < nnext) nxt[2 * k + 1] = right;
             else rej += right;
           }
         }
         __syncthreads();
+      }
+    };
+    for (uint32_t l = 0; l < J; ++l) {  // the top of a large tree: every node of levels 0 .. J - 1
+      const uint32_t span2 = 2u << (D - l - 1);
+      level(l, l, 0, (T + span2 - 1) / span2, top[l & 1], top[(l + 1) & 1]);
+    }
+    // one subtree per node of level J (the whole tree when J = 0)
+    const uint32_t nsub = J ? (T + (1u << (D - J)) - 1) >> (D - J) : 1u;
+    for (uint32_t K = 0; K < nsub; ++K) {
+      if (J) {
+        if (tid == 0) buf[(D - J) & 1][0] = top[J & 1][K];
+        __syncthreads();
+      }
+      for (uint32_t l = J; l < D; ++l) {
+        const uint32_t ll = l - J, kb = K << ll, span2 = 2u << (D - l - 1);
+        const uint32_t nodes = min(1u << ll, (T + span2 - 1) / span2 - kb);
+        level(l, ll, kb, nodes, buf[(D - l) & 1], buf[(D - l - 1) & 1]);
       }
     }
     if (small) {  // tile level D is buf[0]
@@ -1505,7 +1545,7 @@ int ob_panel_create(ob_ctx* ctx, const ob_panel_desc* d, ob_panel** out) {
         return ob::fail(OB_E_INVALID, "missing selection column pointer");
   }
   for (int g = 0; g < 2; ++g) {
-    if (gd[g]->n < 0 || gd[g]->n > kMaxGroupRows)  // level 1 keeps one u32 per 256-row tile in LDS
+    if (gd[g]->n < 0 || gd[g]->n > kMaxGroupRows)
       return ob::fail(OB_E_UNSUPPORTED, "group rows must be in [0, %lld]", (long long)kMaxGroupRows);
     if (gd[g]->n > 0 && ((d->p > 0 && !gd[g]->x) || !gd[g]->y || (d->weighted && !gd[g]->w)))
       return ob::fail(OB_E_INVALID, "missing column pointer");
@@ -1692,7 +1732,7 @@ int ob_boot_run_device(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t 
   if (p->n[0] == 0 || p->n[1] == 0)
     return ob::fail(OB_E_GROUP, "%sOne group has no data", ob::error_prefix(OB_E_GROUP));
   if (p->ntiles[0] > kMaxGroupRows / OB_TILE_ROWS || p->ntiles[1] > kMaxGroupRows / OB_TILE_ROWS)
-    return ob::fail(OB_E_UNSUPPORTED, "group too large for the LDS level-1 histogram");
+    return ob::fail(OB_E_UNSUPPORTED, "groups take at most %lld rows", (long long)kMaxGroupRows);
   return ob::engine_boot(p, seed, first_rep, n_reps, ref_mode, d_rows, d_ok,
                          reinterpret_cast<hipStream_t>(hip_stream));
 }

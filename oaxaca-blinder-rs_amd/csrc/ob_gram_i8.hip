@@ -11,7 +11,7 @@
 // (|d_0| <= 64), so |P - m 2^(E-54)| <= 2^(E-55) <= 2^-54 max |P| -- finer than f64's own
 // rounding of the chunk's largest product. Then
 //     sum_i c_i P_i = 2^(E-54) sum_s 2^(8 (6 - s)) sum_i c_i d_{s,i},
-// each inner sum an exact int32 (|c| <= 127, |d| <= 128, sum_i c_i <= n_g <= 10,485,760, so
+// each inner sum an exact int32 (|c| <= 127, |d| <= 128, sum_i c_i <= n_g < 2^24 (oz_prepare), so
 // |sum| < 2^31). The slices meet in int64, two f64 roundings per chunk partial, so the Gram
 // equals the f64 MFMA Gram to ~1e-15 relative (tests/test_gpu_gram_i8.py holds it to 1e-12).
 //
@@ -402,6 +402,11 @@ namespace ob {
 // caller keeps the f64 MFMA Gram).
 int oz_prepare(ob_panel* p, const std::vector<uint32_t>& chunks) {
   if (p->oz_state != 0) return OB_OK;
+  // exact int32 slice sums need 128 x (a chunk's draws) < 2^31: a group's draws bound a chunk's
+  if (p->n[0] >= (1u << 24) || p->n[1] >= (1u << 24)) {
+    p->oz_state = -1;
+    return OB_OK;
+  }
   const int n_chunks = (int)(chunks.size() / 3);
   const int n_ct = (p->e + kPairsPerTile - 1) / kPairsPerTile;
   const int npp = n_ct * kPairsPerTile;

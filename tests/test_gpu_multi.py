@@ -71,6 +71,22 @@ def test_counts_bitwise_500k_group(ob, O):
         panel.close()
 
 
+@pytest.mark.parametrize("n", [40961 * 256 + 77, 24_000_001])
+def test_counts_bitwise_subtree_level1(ob, O, n):
+    """Groups past 40,960 tiles run level 1 as subtrees under the top levels:
+    tile counts and per-row counts must still equal the oracle's single-tree stream bitwise."""
+    panel = _panel(ob, O, n, 4096)
+    try:
+        l1, rc = panel.debug_counts(SEED, 7, 2, 0)
+        for r in range(2):
+            want_l1 = O.level1_counts(SEED, 7 + r, 0, n)
+            assert np.array_equal(l1[r], want_l1), f"level 1, rep {7 + r}"
+            idx = O.resample_indices(SEED, 7 + r, 0, n)
+            assert np.array_equal(rc[r], np.bincount(idx, minlength=n).astype(np.uint8)), f"rows, rep {7 + r}"
+    finally:
+        panel.close()
+
+
 def test_rank_context_world1_sharded_equals_boot(ob, O, N):
     """ob_ctx_create_rank(world 1) + ob_boot_run_sharded: the RCCL all-gather runs and returns
     exactly ob_boot_run's rows (one outcome and three outcomes, odd replicate counts)."""

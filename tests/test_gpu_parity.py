@@ -425,10 +425,12 @@ def test_full_size_panel_properties(ob, O):
     assert 0.5 < se_gap / (sd * np.sqrt(2 / 500_000)) < 2.0
 
 
-def test_largest_group_and_the_limit(ob, O, N):
-    """n_g = 10,485,760 rows (40,960 tiles, D = 16, 37.5 % of round 0 padding) runs, and its
-    bootstrap rows match the oracle's reference algorithm; one more row is refused up front."""
-    n = 40960 * 256
+@pytest.mark.parametrize("n", [40960 * 256, 40961 * 256 + 77, 24_000_001])
+def test_large_groups_and_the_limit(ob, O, N, n):
+    """Large groups: 10,485,760 rows (40,960 tiles, the largest flat level-1 tree), 40,962 tiles
+    (level 1 as two subtrees under level 1, partial tail) and 24,000,001 rows (93,751 tiles, D = 17,
+    three subtrees under level 2; past the i8 Gram's 2^24-row range, so the f64 MFMA Gram runs).
+    Bootstrap rows match the oracle's reference algorithm; 2^28 + 1 rows are refused up front."""
     rng = np.random.default_rng(3)
     x = rng.normal(size=(n, 1))
     y = 1.0 + 0.5 * x[:, 0] + rng.normal(size=n)
@@ -436,15 +438,18 @@ def test_largest_group_and_the_limit(ob, O, N):
     panel = ob.Panel(x, y, xb, yb)
     try:
         rows, ok = panel.boot(SEED, 0, 2, 0)
+        assert panel.timing()["gram_path"] == (1 if n >= 1 << 24 else 2)
     finally:
         panel.close()
     cfg = O.PassConfig(2, 1, 0, False)
     orows, ook = O.boot_ref(cfg, O.with_intercept(x), y, None, O.with_intercept(xb), yb, None, SEED, 0, 2,
                             threads=8, full=False)
     assert ok.all() and ook.all() and close(rows, orows, abs(orows[0, 5]))[0]
-    with pytest.raises(N.OaxacaError) as e:
-        ob.Panel(np.zeros((n + 1, 1)), np.zeros(n + 1), xb, yb)
-    assert e.value.code == N.OB_E_UNSUPPORTED
+    if n == 40960 * 256:
+        big = (1 << 28) + 1
+        with pytest.raises(N.OaxacaError) as e:
+            ob.Panel(np.empty((big, 1)), np.empty(big), xb, yb)
+        assert e.value.code == N.OB_E_UNSUPPORTED
 
 
 @pytest.mark.parametrize("na,nb", [(65536, 256), (65537, 300), (131372, 1000), (200000, 70000), (257, 65535)])
