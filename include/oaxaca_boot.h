@@ -164,6 +164,8 @@ typedef struct {
   double probit_ms;          /* Heckman panels: ob_probit_kernel time (HIP events), summed over iterations */
   int32_t probit_launches;   /* Heckman panels: ob_probit_kernel launches in those ms */
   double heck_sums_ms;       /* Heckman panels: ob_heck_sums_kernel (IMR sums) time */
+  int32_t mm_reduced;        /* ob_mm_run: 1 if the row reduction ran (subsample, bands, reduced LPs) */
+  int64_t mm_retried;        /* ob_mm_run: fits the reduction solved again on all rows (phase 3) */
 } ob_timing;
 int ob_panel_last_timing(const ob_panel* panel, ob_timing* out);
 /* Synchronize the stream used by the last *_device call and collect its timings. */

@@ -74,7 +74,8 @@ class ob_timing(C.Structure):
                 ("heckman_ms", C.c_double), ("probit_iterations", C.c_int32),
                 ("mm_assemble_ms", C.c_double), ("mm_fit_rows", C.c_double), ("mm_iterations", C.c_int32),
                 ("mm_ms", C.c_double), ("gather_ms", C.c_double), ("gram_path", C.c_int32),
-                ("probit_ms", C.c_double), ("probit_launches", C.c_int32), ("heck_sums_ms", C.c_double)]
+                ("probit_ms", C.c_double), ("probit_launches", C.c_int32), ("heck_sums_ms", C.c_double),
+                ("mm_reduced", C.c_int32), ("mm_retried", C.c_int64)]
 
 
 class ob_unique_id(C.Structure):

@@ -19,6 +19,17 @@
 //   mm_final<K>      corrector direction, step-length bounds; stores the direction
 //   mm_finish        per replicate: successful fits in quantile order, MM-1 row picks (through
 //                    the count images for resamples), predictions, LDS bitonic sorts, quantiles
+//
+// Row reduction (large groups; Portnoy & Koenker 1997, "the Gaussian hare and the Laplacian
+// tortoise"; tools/qr_pk_proto.py). Phase 1 solves every fit on a fixed subsample (every 8th row,
+// relative gap 1e-6) -> beta_hat. mm_band_kernel takes the residual band [lo, hi] of each fit at
+// the tau -/+ delta quantiles of 4096 sampled residuals (delta = 4 sqrt(tau (1 - tau) K / m) +
+// 0.01). mm_classify_kernel keeps, per 64-fit block, the rows inside some fit's band and fixes the
+// others at their optimal bound (x_i = c_i above the band, 0 below), folding them into each fit's
+// right-hand side b = (1 - tau) X'c - sum_above c_i x_i. Phase 2 solves the reduced LPs
+// (X'x = b, infeasible centred start). mm_verify_kernel checks every fixed row's residual sign at
+// the reduced optimum; a fit with a wrong sign (or a phase-2 failure) is solved again on all rows
+// (phase 3). When every sign holds, the reduced optimum is the full LP's optimum.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -38,10 +49,20 @@ namespace {
 
 constexpr double kEta = 0.99995;  // fraction of the distance to the boundary per step
 constexpr double kTol = 1e-12;    // relative duality gap at convergence
-constexpr uint32_t kDone = 1u, kFailed = 2u;
-constexpr uint32_t kRc = 2048;  // rows per chunk (a function of the panel only: determinism)
+constexpr uint32_t kDone = 1u, kFailed = 2u, kRetry = 4u;
+constexpr uint32_t kRc = 2048;  // rows (list entries) per chunk (a function of the panel only: determinism)
+constexpr uint32_t kSubStride = 8;   // phase 1 of the row reduction: every 8th row ...
+constexpr uint32_t kRc1 = kRc * kSubStride / 4;  // ... in chunks of 4096 rows (512 candidates: short walks)
+constexpr double kPhase1Tol = 1e-6;  // phase-1 relative gap (beta_hat only centres the bands)
+constexpr double kBandKappa = 4.0;   // band half-width in rank units: kappa sqrt(tau (1 - tau) K / m) + 0.01
+constexpr int kBandSamples = 4096;   // residuals per fit behind its band quantiles
 
-enum { FS_TAU, FS_GAP, FS_OBJ, FS_MU, FS_SIGMU, FS_AP, FS_AD, FS_NACT, FS_DELTA, kFs };
+enum { FS_TAU, FS_GAP, FS_OBJ, FS_MU, FS_SIGMU, FS_AP, FS_AD, FS_NACT, FS_DELTA, FS_LO, FS_HI, FS_EXT, FS_OBJFIX, kFs };
+
+// Assemble partial layout per fit: NP pairs of X'QX, X'Q r (K), gap, objective, X'x (K; phase 2).
+__host__ __device__ constexpr int nv_asm(int K) { return K * (K + 1) / 2 + 2 * K + 2; }
+// Classify partial layout per fit: sum_above c x (K), sum_all c x (K), sum_above c y, kept rows.
+__host__ __device__ constexpr int nv_cls(int K) { return 2 * K + 2; }
 
 #define MM_OK(expr)                                                                      \
   do {                                                                                   \
@@ -79,6 +100,20 @@ struct MmArgs {
   uint32_t* lane_of;                 // [slot][group][simulation] -> fit lane (lanes in ascending tau)
   uint32_t* rowlist;                 // [slot][chunk (A then B)][kRc] nonzero-count rows (mm_rows_kernel)
   uint32_t* nrows;                   // [slot][chunk] list lengths
+  uint32_t rc;                       // rows per chunk of this phase (kRc; kRc * kSubStride in phase 1)
+  uint32_t stride;                   // mm_rows_kernel: every stride-th row (phase 1) or all (1)
+  uint32_t block_lists;              // lists per (slot, chunk, fit block) (phase 2/3) instead of per chunk
+  int rp;                            // X'x = b per fit (phase 2/3): primal residual in the solves
+  double tol;                        // relative duality gap at convergence
+  uint32_t* blist;                   // mm_classify_kernel output: [slot][chunk][fit block][kRc]
+  uint32_t* bnrows;                  // [slot][chunk][fit block]
+  double *bvec, *rpv, *bhat;         // [fit][K]: b, b - X'x of the iterate, phase-1 beta (band centres)
+  uint32_t* samp;                    // [slot][group][2][kBandSamples]: sampled rows, counts
+  uint32_t* nsamp;                   // [slot][group]
+  double* gchol;                     // [slot][group][K * K + 1]: Cholesky factor of the phase-1 OLS Gram, sum c
+  double* lev;                       // [slot][chunk][kRc]: leverage sqrt(n x_i' G^-1 x_i) per full-list entry
+  uint32_t* xmask;                   // [slot][chunk][fit block][kRc / 32]: rows added to the block's list
+                                     // after a wrong-signed verification (mm_verify)
   uint32_t key0, key1;
   int n_q;
   const double* quantiles;
@@ -128,16 +163,18 @@ static_assert(kRc % 256 == 0 && kRc / 256 == 8, "mm_rows_kernel: 8 rows per thre
 static_assert(16 % kRing == 0, "ring slots are static per unrolled step");
 
 // Nonzero-count rows of each (slot, chunk) in ascending order: (row - chunk start) << 8 | count.
+// A chunk spans a.rc rows, of which every a.stride-th is a candidate (kRc candidates per chunk).
 __global__ __launch_bounds__(256) void mm_rows_kernel(const MmArgs a) {
   __shared__ uint32_t scan[256];
   const uint32_t gch = blockIdx.x, slot = blockIdx.z, nch = a.nch[0] + a.nch[1];
   const uint32_t g = gch >= a.nch[0] ? 1u : 0u;
-  const uint32_t r0 = (gch - (g ? a.nch[0] : 0u)) * kRc, nr = min(a.n[g] - r0, kRc);
+  const uint32_t r0 = (gch - (g ? a.nch[0] : 0u)) * a.rc, nr = min(a.n[g] - r0, a.rc);
   const uint32_t i0 = threadIdx.x * 8;
   uint32_t c[8], k = 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    c[i] = i0 + i < nr ? row_count(a, slot, g, r0 + i0 + i) : 0u;
+    const uint32_t off = (i0 + i) * a.stride;
+    c[i] = off < nr ? row_count(a, slot, g, r0 + off) : 0u;
     k += c[i] != 0u;
   }
   scan[threadIdx.x] = k;
@@ -152,7 +189,7 @@ __global__ __launch_bounds__(256) void mm_rows_kernel(const MmArgs a) {
   uint32_t* L = a.rowlist + ((size_t)slot * nch + gch) * kRc;
 #pragma unroll
   for (int i = 0; i < 8; ++i)
-    if (c[i]) L[o++] = ((i0 + i) << 8) | c[i];
+    if (c[i]) L[o++] = (((i0 + i) * a.stride) << 8) | c[i];
   if (threadIdx.x == 255) a.nrows[(size_t)slot * nch + gch] = scan[255];
 }
 
@@ -176,7 +213,7 @@ __device__ __forceinline__ Blk blk_ctx(const MmArgs& a, uint32_t* lst, bool all_
   b.fb = blockIdx.y;
   b.slot = blockIdx.z;
   b.g = b.gch >= a.nch[0] ? 1u : 0u;
-  b.r0 = (b.gch - (b.g ? a.nch[0] : 0u)) * kRc;
+  b.r0 = (b.gch - (b.g ? a.nch[0] : 0u)) * a.rc;
   b.s = (int)b.fb * 64 + b.wave * 16 + b.fl;
   b.F = fit_index(a, b.slot, b.g, b.s);
   b.live = all_live ? b.s < a.S_pad : (b.s < a.S && !(a.fstat[b.F] & (kDone | kFailed)));
@@ -186,8 +223,9 @@ __device__ __forceinline__ Blk blk_ctx(const MmArgs& a, uint32_t* lst, bool all_
   const size_t li = (size_t)b.slot * (a.nch[0] + a.nch[1]) + b.gch;
   b.sb = (li * (a.S_pad / 64) + b.fb) * ((size_t)kRc * 64) + b.wave * 64 + b.fl;
   b.any = __syncthreads_or(b.live) != 0;
-  b.n_ent = b.any ? a.nrows[li] : 0u;
-  const uint32_t* L = a.rowlist + li * kRc;
+  const size_t lli = a.block_lists ? li * (a.S_pad / 64) + b.fb : li;  // this block's row list
+  b.n_ent = b.any ? a.nrows[lli] : 0u;
+  const uint32_t* L = a.rowlist + lli * kRc;
   for (uint32_t i = threadIdx.x; i < b.n_ent; i += 256) lst[i] = L[i];
   return b;
 }
@@ -336,12 +374,15 @@ __device__ __forceinline__ Corrector corrector_row(const Affine& f, double xd, d
 // mm_assemble: mode 0: weighted OLS of the replicate (q = c, rho = y) -> M, X'Cy, sum c y^2, n_act;
 // mode 1: start point (x = (1 - tau) c, z/w from the OLS residual) + assemble; mode 2 (STEP): replay
 // the last corrector direction from (bprev, dba, db, sigma mu) and take the step (x += ap dx,
-// z += ad dz, w += ad dw) + assemble. Only x, z, w cross HBM. M = X'QX and X'Q r on f64 MFMA:
-// column block cb < NCB has B = x_i x_j of pair columns cb*16.. (ob_pair_index order), block NCB
-// has A = q r and B = x.
+// z += ad dz, w += ad dw) + assemble; mode 3: centred start at beta (phase 2/3 of the row
+// reduction: z/w from the residual, x = c w / (z + w), so x z = s w) + assemble. Only x, z, w
+// cross HBM. M = X'QX and X'Q r on f64 MFMA: column block cb < NCB has B = x_i x_j of pair
+// columns cb*16.. (ob_pair_index order), block NCB has A = q r and B = x; with a.rp, the start
+// point's X'x too (a Newton step keeps X'dx = b - X'x, so afterwards b - X'x shrinks by 1 - ap
+// per step and is tracked per fit, not reassembled).
 template <int K, bool STEP>
 __global__ __launch_bounds__(256, K <= 16 ? 2 : 1) void mm_assemble_mfma_kernel(const MmArgs a, int mode) {
-  constexpr int NP = K * (K + 1) / 2, NV = NP + K + 2;
+  constexpr int NP = K * (K + 1) / 2, NV = nv_asm(K);
   constexpr int NCB = (NP + 15) / 16;
   constexpr int NXB = Xs<K>::NXB;  // X'Q r column blocks
   __shared__ __attribute__((aligned(16))) double xs[2][kSub * Xs<K>::S];
@@ -386,6 +427,10 @@ __global__ __launch_bounds__(256, K <= 16 ? 2 : 1) void mm_assemble_mfma_kernel(
   mm_d4 acc[NCB + NXB];
 #pragma unroll
   for (int cb = 0; cb < NCB + NXB; ++cb) acc[cb] = (mm_d4){0.0, 0.0, 0.0, 0.0};
+  mm_d4 axx[NXB];  // X'x (a.rp)
+#pragma unroll
+  for (int xb = 0; xb < NXB; ++xb) axx[xb] = (mm_d4){0.0, 0.0, 0.0, 0.0};
+  const bool rp = !STEP && a.rp != 0;  // X'x of the start point (later steps track b - X'x exactly)
   double gap = 0.0, obj = 0.0;
   __syncthreads();  // lst
   const uint32_t nsub = (b.n_ent + kSub - 1) / kSub;
@@ -418,7 +463,7 @@ __global__ __launch_bounds__(256, K <= 16 ? 2 : 1) void mm_assemble_mfma_kernel(
           const double c = valid ? (double)(lst[e] & 255u) : 0.0;
           const double* xr = X + (4 * j + b.rl) * Xs<K>::S;
           const double y = xr[Xs<K>::Y];
-          double q = 0.0, qr = 0.0;
+          double q = 0.0, qr = 0.0, xq = 0.0;
           if (valid) {
             if (mode == 0) {
               q = c;
@@ -429,9 +474,9 @@ __global__ __launch_bounds__(256, K <= 16 ? 2 : 1) void mm_assemble_mfma_kernel(
               double xv, zv, wv, r;
               if (!STEP) {
                 r = y - dots[0][j & 3];
-                xv = (1.0 - tau) * c;
                 zv = fmax(-r, 0.0) + delta;
                 wv = fmax(r, 0.0) + delta;
+                xv = mode == 3 ? c * wv / (zv + wv) : (1.0 - tau) * c;
               } else {
                 const Affine f = affine_row(cx, cz, cw, c, y, dots[0][j & 3], dots[NDOT > 1 ? 1 : 0][j & 3]);
                 const double xdb = dots[NDOT > 2 ? 2 : 0][j & 3];
@@ -448,6 +493,7 @@ __global__ __launch_bounds__(256, K <= 16 ? 2 : 1) void mm_assemble_mfma_kernel(
               const double sv = c - xv;
               q = xv * sv * mm_rcp(zv * sv + wv * xv);  // 1 / (z/x + w/s)
               qr = q * r;                          // rho_aff = r_d + w - z = y - X beta
+              xq = xv;
               gap += xv * zv + sv * wv;
               obj += y * xv;
             }
@@ -458,6 +504,10 @@ __global__ __launch_bounds__(256, K <= 16 ? 2 : 1) void mm_assemble_mfma_kernel(
 #pragma unroll
           for (int xb = 0; xb < NXB; ++xb)
             acc[NCB + xb] = __builtin_amdgcn_mfma_f64_16x16x4f64(qr, xr[16 * xb + b.fl], acc[NCB + xb], 0, 0, 0);
+          if (rp)
+#pragma unroll
+            for (int xb = 0; xb < NXB; ++xb)
+              axx[xb] = __builtin_amdgcn_mfma_f64_16x16x4f64(xq, xr[16 * xb + b.fl], axx[xb], 0, 0, 0);
       };
       // the next sub-tile's values go to the other buffer after a few steps (registers freed)
       if (b.wave_live)
@@ -483,6 +533,12 @@ __global__ __launch_bounds__(256, K <= 16 ? 2 : 1) void mm_assemble_mfma_kernel(
       const int xc = (cb - NCB) * 16 + b.fl;
       if (cb >= NCB && xc < K) P[fit * NV + NP + xc] = acc[cb][r];
     }
+  if (rp)
+#pragma unroll
+    for (int xb = 0; xb < NXB; ++xb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (16 * xb + b.fl < K) P[(fw + b.rl + 4 * r) * NV + NP + K + 2 + 16 * xb + b.fl] = axx[xb][r];
   gap = rows_sum(gap);
   obj = rows_sum(obj);
   if (b.rl == 0) {
@@ -654,7 +710,7 @@ __global__ __launch_bounds__(64) void mm_start_kernel(const MmArgs a, int K) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int lane = threadIdx.x;
   const uint32_t slot = blockIdx.x >> 1, g = blockIdx.x & 1;
-  const int NP = K * (K + 1) / 2, NV = NP + K + 2;
+  const int NP = K * (K + 1) / 2, NV = nv_asm(K);
   const double* R = a.red + (((size_t)slot * 2 + g) * a.S_pad) * NV;  // fit 0 holds the sums
   double* M = sm;
   double* v = sm + K * K;
@@ -667,6 +723,11 @@ __global__ __launch_bounds__(64) void mm_start_kernel(const MmArgs a, int K) {
   const bool chol = wave_cholesky(M, K, lane);
   if (chol) wave_chol_solve(M, K, v, lane);
   __syncthreads();
+  if (a.gchol) {  // the row reduction's leverages (mm_lev_kernel)
+    double* gc = a.gchol + ((size_t)slot * 2 + g) * (K * K + 1);
+    for (int i = lane; i < K * K; i += 64) gc[i] = M[i];
+    if (lane == 0) gc[K * K] = chol ? R[0] : 0.0;
+  }
   double delta = 0.0;
   if (chol) {
     double bv = 0.0;
@@ -768,7 +829,7 @@ __global__ __launch_bounds__(1024) void mm_shift_kernel(const MmArgs a, int K) {
         else hi = mid;
       }
       const uint32_t ent = a.rowlist[(li0 + lo) * kRc + (e - pre[lo])];
-      const uint32_t row = lo * kRc + (ent >> 8);
+      const uint32_t row = lo * a.rc + (ent >> 8);
       const double* X = a.cols[g];
       double xb = beta[0];
       for (int k = 1; k < K; ++k) xb += X[(size_t)(k - 1) * a.ld[g] + row] * beta[k];
@@ -820,34 +881,46 @@ __global__ __launch_bounds__(1024) void mm_shift_kernel(const MmArgs a, int K) {
   }
 }
 
-// Convergence test, Cholesky of M, affine direction (wave per fit).
-__global__ __launch_bounds__(64) void mm_solve_affine_kernel(const MmArgs a, int K) {
+// Convergence test, Cholesky of M, affine direction (wave per fit). rp_mode (phase 2/3, X'x = b):
+// 1 = primal residual b - X'x from the start assemble, 2 = the last one times (1 - ap).
+__global__ __launch_bounds__(64) void mm_solve_affine_kernel(const MmArgs a, int K, int rp_mode) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int lane = threadIdx.x;
   const size_t F = blockIdx.x;
   if (a.fstat[F] & (kDone | kFailed)) return;
-  const int NP = K * (K + 1) / 2, NV = NP + K + 2;
+  const int NP = K * (K + 1) / 2, NV = nv_asm(K);
   const double* R = a.red + F * NV;
   double* f = a.fs + F * kFs;
-  const double gap = R[NP + K], obj = R[NP + K + 1];
+  const double gap = R[NP + K], obj = R[NP + K + 1] + (rp_mode ? f[FS_OBJFIX] : 0.0);
+  double rpk = 0.0, bk = 0.0;  // lane k < K: b_k - (X'x)_k, b_k
+  if (rp_mode && lane < K) {
+    bk = a.bvec[F * K + lane];
+    rpk = rp_mode == 1 ? bk - R[NP + K + 2 + lane] : (1.0 - f[FS_AP]) * a.rpv[F * K + lane];
+  }
+  double rpm = fabs(rpk), bm = fabs(bk);
+  for (int o = 32; o > 0; o >>= 1) {
+    rpm = fmax(rpm, __shfl_xor(rpm, o));
+    bm = fmax(bm, __shfl_xor(bm, o));
+  }
   if (lane == 0) {
     f[FS_GAP] = gap;
     f[FS_OBJ] = obj;
   }
-  if (gap < kTol * (1.0 + fabs(obj))) {  // converged: beta is the QR solution
+  if (gap < a.tol * (1.0 + fabs(obj)) && rpm <= 1e-10 * (1.0 + bm)) {  // converged: beta is the QR solution
     if (lane == 0) a.fstat[F] = kDone;
     return;
   }
+  if (rp_mode && lane < K) a.rpv[F * K + lane] = rpk;
   double* M = sm;
   double* v = sm + K * K;
   for (int i = lane; i < K * K; i += 64) {
     const int r = i % K, c = i / K;
     M[i] = R[r <= c ? ob_pair_index(r, c, K) : ob_pair_index(c, r, K)];
   }
-  for (int i = lane; i < K; i += 64) v[i] = R[NP + i];
+  for (int i = lane; i < K; i += 64) v[i] = R[NP + i] - rpk;  // M dba = X'Q rho_aff - (b - X'x)
   __syncthreads();
   if (!wave_cholesky(M, K, lane)) {  // the normal matrix lost rank: accept a near-optimal point
-    if (lane == 0) a.fstat[F] = gap < 1e-9 * (1.0 + fabs(obj)) ? kDone : (kDone | kFailed);
+    if (lane == 0) a.fstat[F] = gap < 1e-9 * (1.0 + fabs(obj)) && rpm <= 1e-9 * (1.0 + bm) ? kDone : (kDone | kFailed);
     return;
   }
   wave_chol_solve(M, K, v, lane);
@@ -878,7 +951,7 @@ __global__ __launch_bounds__(64) void mm_solve_corrector_kernel(const MmArgs a, 
   double* Lm = sm;
   double* v = sm + K * K;
   for (int i = lane; i < K * K; i += 64) Lm[i] = a.L[F * K * K + i];
-  for (int i = lane; i < K; i += 64) v[i] = R[5 + i] + sigmu * R[5 + K + i];
+  for (int i = lane; i < K; i += 64) v[i] = R[5 + i] + sigmu * R[5 + K + i] - (a.rp ? a.rpv[F * K + i] : 0.0);
   __syncthreads();
   wave_chol_solve(Lm, K, v, lane);
   for (int i = lane; i < K; i += 64) a.db[F * K + i] = v[i];
@@ -897,6 +970,360 @@ __global__ __launch_bounds__(256) void mm_step_kernel(const MmArgs a, int K, siz
   }
   a.fs[F * kFs + FS_AP] = ap;
   a.fs[F * kFs + FS_AD] = ad;
+}
+
+// ---- row reduction (phases 2 and 3) ----
+
+// kBandSamples list entries of each (slot, group) at a fixed stride over the full nonzero-row lists:
+// the rows behind every fit's band quantiles (a function of the replicate alone).
+__global__ __launch_bounds__(1024) void mm_sample_kernel(const MmArgs a) {
+  __shared__ uint32_t pre[1024 + 1];
+  const uint32_t slot = blockIdx.x >> 1, g = blockIdx.x & 1;
+  const uint32_t nch = a.nch[0] + a.nch[1], c0 = g ? a.nch[0] : 0u, ncg = a.nch[g];
+  const size_t li0 = (size_t)slot * nch + c0;
+  for (uint32_t c = threadIdx.x; c < ncg; c += blockDim.x) pre[c + 1] = a.nrows[li0 + c];
+  if (threadIdx.x == 0) pre[0] = 0;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (uint32_t c = 1; c <= ncg; ++c) pre[c] += pre[c - 1];
+  __syncthreads();
+  const uint32_t tot = pre[ncg];
+  const uint32_t m = min<uint32_t>(tot, (uint32_t)kBandSamples);
+  uint32_t* out = a.samp + ((size_t)slot * 2 + g) * 2 * kBandSamples;
+  for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
+    const uint32_t e = (uint32_t)(((uint64_t)j * tot) / m);
+    uint32_t lo = 0, hi = ncg;  // chunk with pre[lo] <= e < pre[lo + 1]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (pre[mid] <= e) lo = mid;
+      else hi = mid;
+    }
+    const uint32_t ent = a.rowlist[(li0 + lo) * kRc + (e - pre[lo])];
+    out[j] = lo * a.rc + (ent >> 8);
+    out[kBandSamples + j] = ent & 255u;
+  }
+  if (threadIdx.x == 0) a.nsamp[(size_t)slot * 2 + g] = m;
+}
+
+// Leverage of every full-list entry: lev_i = sqrt(n x_i' G^-1 x_i) with G = X'CX of the phase-1
+// subsample and n = its sum of counts (about sqrt(K) for a typical row). The error of beta_hat
+// moves a row's residual in proportion to it, so the bands widen for high-leverage rows.
+__global__ __launch_bounds__(256) void mm_lev_kernel(const MmArgs a, int K) {
+  __shared__ double L[ob::kMmMaxK * ob::kMmMaxK];
+  const uint32_t gch = blockIdx.x, slot = blockIdx.z, nch = a.nch[0] + a.nch[1];
+  const uint32_t g = gch >= a.nch[0] ? 1u : 0u;
+  const double* gc = a.gchol + ((size_t)slot * 2 + g) * (K * K + 1);
+  for (int i = threadIdx.x; i < K * K; i += 256) L[i] = gc[i];
+  __syncthreads();
+  const double n = gc[K * K];
+  const size_t li = (size_t)slot * nch + gch;
+  const uint32_t ne = a.nrows[li], r0 = (gch - (g ? a.nch[0] : 0u)) * a.rc;
+  const double* X = a.cols[g];
+  for (uint32_t e = threadIdx.x; e < ne; e += 256) {
+    const uint32_t row = r0 + (a.rowlist[li * kRc + e] >> 8);
+    double v[ob::kMmMaxK], q = 0.0;
+    for (int i = 0; i < K; ++i) {  // L v = x (forward substitution), q = |v|^2
+      double t = i ? X[(size_t)(i - 1) * a.ld[g] + row] : 1.0;
+      for (int j = 0; j < i; ++j) t -= L[i + j * K] * v[j];
+      v[i] = t / L[i + i * K];
+      q += v[i] * v[i];
+    }
+    a.lev[li * kRc + e] = n > 0.0 ? sqrt(n * q) : sqrt((double)K);
+  }
+}
+
+// Per fit (block of 256): beta_hat <- the phase-1 beta (zero if not finite), and the residual band
+// [lo, hi] = the count-weighted tau -/+ delta quantiles of the sampled residuals at beta_hat, with
+// delta = kappa sqrt(tau (1 - tau) K / m) + 0.01 (m = the phase-1 sample's rows). A fit whose
+// phase 1 failed keeps every row (band = the real line); padding fits keep none.
+__global__ __launch_bounds__(256) void mm_band_kernel(const MmArgs a, int K) {
+  __shared__ double key[kBandSamples];
+  __shared__ double wt[kBandSamples];
+  __shared__ double beta[ob::kMmMaxK];
+  __shared__ double part[256];
+  __shared__ int finite;
+  const size_t F = blockIdx.x;
+  const uint32_t slot = (uint32_t)(F / (2 * (size_t)a.S_pad)), g = (uint32_t)((F / a.S_pad) & 1);
+  const int s = (int)(F % a.S_pad), t = threadIdx.x;
+  double* f = a.fs + F * kFs;
+  if (s >= a.S) {
+    if (t == 0) {
+      f[FS_LO] = INFINITY;
+      f[FS_HI] = -INFINITY;
+      f[FS_EXT] = 0.0;
+    }
+    return;
+  }
+  if (t == 0) finite = 1;
+  __syncthreads();
+  if (t < K) {
+    beta[t] = a.beta[F * K + t];
+    if (!isfinite(beta[t])) finite = 0;
+  }
+  __syncthreads();
+  if (t < K) {
+    if (!finite) beta[t] = 0.0;
+    a.bhat[F * K + t] = beta[t];
+  }
+  const double tau = f[FS_TAU];
+  const double delta = kBandKappa * sqrt(tau * (1.0 - tau) * K / fmax(f[FS_NACT], 1.0)) + 0.01;
+  if ((a.fstat[F] & kFailed) || (tau - delta <= 0.0 && tau + delta >= 1.0)) {
+    if (t == 0) {
+      f[FS_LO] = -INFINITY;
+      f[FS_HI] = INFINITY;
+      f[FS_EXT] = 0.0;
+    }
+    return;
+  }
+  __syncthreads();
+  const uint32_t ns = a.nsamp[(size_t)slot * 2 + g];
+  const uint32_t* sr = a.samp + ((size_t)slot * 2 + g) * 2 * kBandSamples;
+  const double* X = a.cols[g];
+  const int64_t ld = a.ld[g];
+  for (int j = t; j < kBandSamples; j += 256) {
+    double r = INFINITY, c = 0.0;
+    if ((uint32_t)j < ns) {
+      const uint32_t row = sr[j];
+      double xb = beta[0];
+      for (int k = 1; k < K; ++k) xb += X[(size_t)(k - 1) * ld + row] * beta[k];
+      r = X[(size_t)a.p * ld + row] - xb;
+      c = (double)sr[kBandSamples + j];
+    }
+    key[j] = r;
+    wt[j] = c;
+  }
+  __syncthreads();
+  for (int k = 2; k <= kBandSamples; k <<= 1)  // bitonic sort by residual, weights along
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = t; i < kBandSamples; i += 256) {
+        const int l = i ^ j;
+        if (l > i) {
+          const bool up = (i & k) == 0;
+          const double x = key[i], y = key[l];
+          if ((x > y) == up) {
+            key[i] = y;
+            key[l] = x;
+            const double w = wt[i];
+            wt[i] = wt[l];
+            wt[l] = w;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  constexpr int kPer = kBandSamples / 256;  // inclusive prefix of the weights: 16 per thread
+  double run = 0.0;
+  for (int i = 0; i < kPer; ++i) run += wt[t * kPer + i];
+  part[t] = run;
+  __syncthreads();
+  if (t == 0)
+    for (int i = 1; i < 256; ++i) part[i] += part[i - 1];
+  __syncthreads();
+  run = t ? part[t - 1] : 0.0;
+  for (int i = 0; i < kPer; ++i) {
+    run += wt[t * kPer + i];
+    wt[t * kPer + i] = run;
+  }
+  __syncthreads();
+  if (t == 0) {
+    const int m = (int)ns;
+    const double W = m ? wt[m - 1] : 0.0;
+    auto quant = [&](double target) {  // first i with wt[i] >= target
+      int lo = 0, hi = m - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (wt[mid] >= target) hi = mid;
+        else lo = mid + 1;
+      }
+      return key[lo];
+    };
+    const double lo = (m && tau - delta > 0.0) ? quant((tau - delta) * W) : -INFINITY;
+    const double hi = (m && tau + delta < 1.0) ? quant((tau + delta) * W) : INFINITY;
+    const double mid = m ? quant(tau * W) : 0.0;
+    // residual units per rank unit (1 / density at the quantile), from the band's finite sides
+    const double slope = isfinite(lo) && isfinite(hi) ? (hi - lo) / (2.0 * delta)
+                         : isfinite(hi)               ? (hi - mid) / delta
+                         : isfinite(lo)               ? (mid - lo) / delta
+                                                      : 0.0;
+    f[FS_LO] = lo;
+    f[FS_HI] = hi;
+    // per unit of leverage above sqrt(K): kappa standard errors of x_i beta_hat
+    f[FS_EXT] = kBandKappa * sqrt(tau * (1.0 - tau) / fmax(f[FS_NACT], 1.0)) * slope;
+  }
+}
+
+// One walk over a chunk's full nonzero-row list per 64-fit block. Each lane's fit classifies its
+// rows at beta_hat: inside the band [lo, hi] (kept: the row joins the block's reduced list if any
+// fit of the block keeps it), above (x_i = c_i) or below (x_i = 0).
+// !VERIFY: writes the block's list and per-fit partials: sum_above c x, sum_all c x, sum_above c y
+//          (the fixed rows' objective), the kept entries (nv_cls layout).
+// VERIFY:  at the reduced optimum beta, a fixed row whose residual has the wrong sign flags its fit
+//          for phase 3 (kRetry).
+template <int K, bool VERIFY>
+__global__ __launch_bounds__(256) void mm_classify_kernel(const MmArgs a) {
+  constexpr int NXB = Xs<K>::NXB, S = Xs<K>::S, NVC = nv_cls(K), ND = VERIFY ? 2 : 1;
+  __shared__ __attribute__((aligned(16))) double xs[kSub * S];
+  __shared__ uint32_t lst[kRc];
+  __shared__ uint32_t keep[kSub];
+  __shared__ uint32_t nkeep;
+  const Blk b = blk_ctx(a, lst, true);
+  const bool part = b.s < a.S;
+  double lo = INFINITY, hi = -INFINITY, ext = 0.0;
+  if (part) {
+    lo = a.fs[b.F * kFs + FS_LO];
+    hi = a.fs[b.F * kFs + FS_HI];
+    ext = a.fs[b.F * kFs + FS_EXT];
+  }
+  const double sqk = sqrt((double)K);
+  const size_t li = (size_t)b.slot * (a.nch[0] + a.nch[1]) + b.gch;
+  double fb[ND][(K + 3) / 4];
+  bfrag<K>(a.bhat, b, part, fb[0]);
+  if (VERIFY) bfrag<K>(a.beta, b, part, fb[ND - 1]);
+  mm_d4 A[NXB], T[NXB];
+#pragma unroll
+  for (int xb = 0; xb < NXB; ++xb) A[xb] = T[xb] = (mm_d4){0.0, 0.0, 0.0, 0.0};
+  double objfix = 0.0;
+  bool bad = false;
+  uint32_t cnt = 0;  // wave 0: entries of the block's list so far
+  const size_t oi = li * (a.S_pad / 64) + b.fb;
+  uint32_t* out = a.blist + oi * kRc;
+  uint32_t* xm = a.xmask + oi * (kRc / 32);
+  const bool check = VERIFY && part && lo <= hi;  // fits of this round (the others have empty bands)
+  __syncthreads();  // lst
+  const uint32_t nsub = (b.n_ent + kSub - 1) / kSub;
+  for (uint32_t t = 0; t < nsub; ++t) {
+    if (threadIdx.x < kSub) keep[threadIdx.x] = 0u;
+    double stg[Xs<K>::Stage];
+    xs_load<K>(a, b, lst, t, stg);
+    xs_store<K>(xs, stg);
+    __syncthreads();
+    uint32_t side = 0;
+    double rv[16];
+    mm_d4 dots[ND];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if ((j & 3) == 0) group_dots<K, ND>(xs, j >> 2, b, fb, dots);
+      const uint32_t e = t * kSub + 4 * j + b.rl;
+      const bool valid = part && e < b.n_ent;
+      const double y = xs[(4 * j + b.rl) * S + Xs<K>::Y];
+      const double rh = y - dots[0][j & 3];
+      const double x = valid ? ext * fmax(a.lev[li * kRc + e] - sqk, 0.0) : 0.0;  // leverage widening
+      const bool in = valid && rh >= lo - x && rh <= hi + x;
+      side |= (in ? 1u : (rh > hi + x ? 2u : 0u)) << (2 * j);
+      // rows added after an earlier verification are in the list too (a row flagged in this pass
+      // is set after the barrier below, so within a sub-tile the bits read here are the old ones)
+      if (in || (e < b.n_ent && ((xm[e >> 5] >> (e & 31u)) & 1u))) keep[4 * j + b.rl] = 1u;
+      rv[j] = VERIFY ? y - dots[ND - 1][j & 3] : 0.0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t e = t * kSub + 4 * j + b.rl;
+      const bool valid = part && e < b.n_ent;
+      const bool kept = keep[4 * j + b.rl] != 0u;
+      const uint32_t sd = (side >> (2 * j)) & 3u;
+      const double* xr = xs + (4 * j + b.rl) * S;
+      const double y = xr[Xs<K>::Y];
+      if (!VERIFY) {
+        const double c = valid ? (double)(lst[e] & 255u) : 0.0;
+        const double ab = (!kept && sd == 2u) ? c : 0.0;
+        objfix += ab * y;
+#pragma unroll
+        for (int xb = 0; xb < NXB; ++xb) {
+          const double bx = xr[16 * xb + b.fl];
+          A[xb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ab, bx, A[xb], 0, 0, 0);
+          T[xb] = __builtin_amdgcn_mfma_f64_16x16x4f64(c, bx, T[xb], 0, 0, 0);
+        }
+      } else if (check && valid && !kept && sd != 1u) {
+        const double eps = 1e-9 * (1.0 + fabs(y));
+        if (sd == 2u ? rv[j] < -eps : rv[j] > eps) {  // the row joins the block's list next round
+          bad = true;
+          atomicOr(&xm[e >> 5], 1u << (e & 31u));
+        }
+      }
+    }
+    if (!VERIFY && b.wave == 0) {  // the kept rows of this sub-tile, in row order
+      const uint32_t e = t * kSub + b.lane;
+      const bool f = e < b.n_ent && keep[b.lane] != 0u;
+      const unsigned long long m = __ballot(f);
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+      if (f) out[cnt + below] = lst[e];
+      cnt += (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+  }
+  if (!VERIFY) {
+    if (threadIdx.x == 0) {
+      a.bnrows[oi] = cnt;
+      nkeep = cnt;
+    }
+    __syncthreads();
+    double* P = a.partial + li * a.S_pad * NVC;
+    const size_t fw = (size_t)b.fb * 64 + b.wave * 16;
+#pragma unroll
+    for (int xb = 0; xb < NXB; ++xb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const size_t fit = fw + b.rl + 4 * r;
+        const int col = 16 * xb + b.fl;
+        if (col < K) {
+          P[fit * NVC + col] = A[xb][r];
+          P[fit * NVC + K + col] = T[xb][r];
+        }
+      }
+    objfix = rows_sum(objfix);
+    if (b.rl == 0) {
+      P[(fw + b.fl) * NVC + 2 * K] = objfix;
+      P[(fw + b.fl) * NVC + 2 * K + 1] = (double)nkeep;
+    }
+  } else {
+    bad = rows_sum(bad ? 1.0 : 0.0) != 0.0;
+    if (b.rl == 0 && part && bad) atomicOr(&a.fstat[b.F], kRetry);
+  }
+}
+
+// Reduced right-hand sides from the classify partials (thread per fit): b = (1 - tau) X'c -
+// sum_above c x; the fixed rows' objective; the reduced problem's rows. reset (phase 2): every fit
+// restarts at beta_hat; a reduced list too short to hold a fit goes straight to phase 3.
+__global__ __launch_bounds__(256) void mm_bvec_kernel(const MmArgs a, int K, size_t n_fits, int reset) {
+  const size_t F = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (F >= n_fits || (int)(F % a.S_pad) >= a.S) return;
+  const double* R = a.red + F * nv_cls(K);
+  double* f = a.fs + F * kFs;
+  const double tau = f[FS_TAU];
+  for (int k = 0; k < K; ++k) a.bvec[F * K + k] = (1.0 - tau) * R[K + k] - R[k];
+  f[FS_OBJFIX] = R[2 * K];
+  f[FS_NACT] = R[2 * K + 1];
+  if (reset) {
+    a.fstat[F] = R[2 * K + 1] < (double)(2 * K) ? (kDone | kFailed) : 0u;
+    for (int k = 0; k < K; ++k) a.beta[F * K + k] = a.bhat[F * K + k];
+  }
+  if (a.fstat[F] == 0u) {
+    f[FS_AP] = f[FS_AD] = 0.0;
+    atomicAdd(a.active_rows, (unsigned long long)R[2 * K + 1]);
+  }
+}
+
+// After a reduced round and mm_verify: a fit with a wrong-signed fixed row or a failure restarts at
+// beta_hat, after round 0 with its band plus the wrong-signed rows (mm_verify's xmask; the
+// Portnoy-Koenker fix-up), after round 1 on all its rows (band = the real line); the others keep
+// their result and an empty band.
+__global__ __launch_bounds__(256) void mm_retry_kernel(const MmArgs a, int K, size_t n_fits, int all_rows) {
+  const size_t F = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (F >= n_fits || (int)(F % a.S_pad) >= a.S) return;
+  double* f = a.fs + F * kFs;
+  if (a.fstat[F] == kDone) {
+    f[FS_LO] = INFINITY;
+    f[FS_HI] = -INFINITY;
+    return;
+  }
+  a.fstat[F] = 0u;
+  if (all_rows) {
+    f[FS_LO] = -INFINITY;
+    f[FS_HI] = INFINITY;
+  }
+  for (int k = 0; k < K; ++k) a.beta[F * K + k] = a.bhat[F * K + k];
+  atomicAdd(a.active, 1u);
 }
 
 __global__ __launch_bounds__(256) void mm_expire_kernel(const MmArgs a, size_t n_fits) {
@@ -1042,16 +1469,25 @@ struct Kernels {
   static void final_(const MmArgs& a, dim3 grid, hipStream_t s) {
     hipLaunchKernelGGL(mm_final_kernel<K>, grid, dim3(256), 0, s, a);
   }
+  static void classify(const MmArgs& a, dim3 grid, bool verify, hipStream_t s) {
+    if (verify)
+      hipLaunchKernelGGL((mm_classify_kernel<K, true>), grid, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((mm_classify_kernel<K, false>), grid, dim3(256), 0, s, a);
+  }
 };
 
+// which: 0 assemble (mode), 1 affine, 2 final, 3 classify, 4 verify
 template <int K>
 void launch_pass(int which, const MmArgs& a, dim3 grid, int mode, hipStream_t s) {
   if (which == 0)
     Kernels<K>::assemble(a, grid, mode, s);
   else if (which == 1)
     Kernels<K>::affine(a, grid, s);
-  else
+  else if (which == 2)
     Kernels<K>::final_(a, grid, s);
+  else
+    Kernels<K>::classify(a, grid, which == 4, s);
 }
 
 void pass(int K, int which, const MmArgs& a, dim3 grid, int mode, hipStream_t s) {
@@ -1081,13 +1517,19 @@ struct Buffers {
            *nrows = nullptr;
   unsigned long long* active_rows = nullptr;
   uint8_t* ok = nullptr;
-  static constexpr int kSlots = 21;
+  double *bvec = nullptr, *rpv = nullptr, *bhat = nullptr;  // row reduction
+  uint32_t *samp = nullptr, *nsamp = nullptr;
+  double *gchol = nullptr, *lev = nullptr;
+  uint32_t* xmask = nullptr;
+  static constexpr int kSlots = 29;
   size_t cap[kSlots] = {};
   void** slot(int i) {
     void** v[kSlots] = {(void**)&x, (void**)&z, (void**)&w, (void**)&beta, (void**)&bprev,
                     (void**)&dba, (void**)&db, (void**)&L, (void**)&fs, (void**)&partial, (void**)&red,
                     (void**)&quant, (void**)&rows, (void**)&fstat, (void**)&active, (void**)&active_rows,
-                    (void**)&tprefix, (void**)&lane_of, (void**)&rowlist, (void**)&nrows, (void**)&ok};
+                    (void**)&tprefix, (void**)&lane_of, (void**)&rowlist, (void**)&nrows, (void**)&ok,
+                    (void**)&bvec, (void**)&rpv, (void**)&bhat, (void**)&samp, (void**)&nsamp,
+                    (void**)&gchol, (void**)&lev, (void**)&xmask};
     return v[i];
   }
   // bytes[i] for slot i; reallocates the slots that are too small
@@ -1120,30 +1562,47 @@ bool trace() {
 struct MmStats {
   double assemble_ms = 0.0, fit_rows = 0.0, sync_ms = 0.0;
   int iterations = 0;
-  hipEvent_t ev[2] = {nullptr, nullptr};
+  uint64_t retried = 0;  // fits solved again on all rows (row reduction, phase 3)
+  std::vector<hipEvent_t> ev;  // pairs around the assemble launches of one ipm() call
+  hipError_t events(size_t n) {
+    while (ev.size() < n) {
+      hipEvent_t e = nullptr;
+      const hipError_t r = hipEventCreate(&e);
+      if (r != hipSuccess) return r;
+      ev.push_back(e);
+    }
+    return hipSuccess;
+  }
+  ~MmStats() {
+    for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+  }
+};
+constexpr int kCheckEvery = 3;  // iterations between host checks for live fits (extra ones are no-ops)
+
+struct Reduction {  // the row reduction's phase-1 geometry and list regions (mm_run)
+  bool on = false;
+  uint32_t nch1[2] = {0, 0};
+  uint32_t *list1 = nullptr, *nrows1 = nullptr;
+  double* gchol = nullptr;
 };
 
-// One batch of replicate slots: start, IPM iterations, finish. Rows/ok -> host.
-int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, MmStats& st) {
+hipError_t reduce_partials(const MmArgs& a, int nv, int n_min, int skip_dead, hipStream_t s) {
+  const size_t tot = (size_t)a.n_rb * 2 * a.S_pad * nv;
+  hipLaunchKernelGGL(mm_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, a, nv, n_min, skip_dead);
+  return hipGetLastError();
+}
+
+// Row lists, the OLS start per (slot, group), the tau order and the shifted start (phase 1, or the
+// whole solve without the reduction); a.active_rows <- the live (fit, row) pairs of the first assemble.
+int start_fits(const MmArgs& a, int K, hipStream_t s) {
   const uint32_t nch = a.nch[0] + a.nch[1];
-  const int NP = K * (K + 1) / 2;
-  const int nv1 = NP + K + 2, nv2 = 5 + 2 * K;
-  const size_t n_fits = (size_t)a.n_rb * 2 * a.S_pad;
-  const dim3 grid(nch, a.S_pad / 64, a.n_rb);
-  auto reduce = [&](int nv, int n_min, int skip_dead = 1) -> hipError_t {
-    const size_t tot = n_fits * nv;
-    hipLaunchKernelGGL(mm_reduce_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, a, nv, n_min,
-                       skip_dead);
-    return hipGetLastError();
-  };
   const size_t lds_solve = sizeof(double) * ((size_t)K * K + K);
-  // row lists, then the start: weighted OLS per (slot, group)
   hipLaunchKernelGGL(mm_rows_kernel, dim3(nch, 1, a.n_rb), dim3(256), 0, s, a);
   MM_OK(hipGetLastError());
   MM_OK(hipMemsetAsync(a.active_rows, 0, sizeof(unsigned long long), s));
   pass(K, 0, a, dim3(nch, 1, a.n_rb), 0, s);
   MM_OK(hipGetLastError());
-  MM_OK(reduce(nv1, 0, 0));  // the OLS sums sit in fit 0 (the statuses are not set yet)
+  MM_OK(reduce_partials(a, nv_asm(K), 0, 0, s));  // the OLS sums sit in fit 0 (the statuses are not set yet)
   hipLaunchKernelGGL(mm_start_kernel, dim3(a.n_rb * 2), dim3(64), lds_solve, s, a, K);
   MM_OK(hipGetLastError());
   int m2 = 1;
@@ -1154,59 +1613,74 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, MmS
   MM_OK(hipGetLastError());
   hipLaunchKernelGGL(mm_shift_kernel, dim3(a.n_rb * 2), dim3(1024), 0, s, a, K);
   MM_OK(hipGetLastError());
+  return OB_OK;
+}
+
+// Interior-point iterations over the live fits (first assemble in first_mode: 1 shifted start, 3
+// centred start) until none is active or kMmMaxIter; the fits still live then fail. The host
+// looks at the live count every kCheckEvery iterations (converged fits skip every kernel, so the
+// iterations past the last live fit cost only launches). a.active_rows accumulates the live
+// (fit, row) pairs of the assembles (the caller seeds it with the first one's).
+int ipm(const MmArgs& a, int K, int first_mode, hipStream_t s, MmStats& st) {
+  const uint32_t nch = a.nch[0] + a.nch[1];
+  const int nv1 = nv_asm(K), nv2 = 5 + 2 * K;
+  const size_t n_fits = (size_t)a.n_rb * 2 * a.S_pad;
+  const dim3 grid(nch, a.S_pad / 64, a.n_rb);
+  const size_t lds_solve = sizeof(double) * ((size_t)K * K + K);
+  MM_OK(st.events(2 * (size_t)ob::kMmMaxIter));
   int it = 0;
-  uint64_t live_rows = 0;  // first assemble: every fit of a group whose OLS start exists (mm_start_kernel)
-  {
-    unsigned long long v = 0;
-    MM_OK(hipMemcpyAsync(&v, a.active_rows, sizeof(v), hipMemcpyDeviceToHost, s));
-    MM_OK(hipStreamSynchronize(s));
-    live_rows = v;
-  }
   for (it = 1; it <= ob::kMmMaxIter; ++it) {
-    MM_OK(hipEventRecord(st.ev[0], s));
-    pass(K, 0, a, grid, it == 1 ? 1 : 2, s);
+    MM_OK(hipEventRecord(st.ev[2 * (it - 1)], s));
+    pass(K, 0, a, grid, it == 1 ? first_mode : 2, s);
     MM_OK(hipGetLastError());
-    MM_OK(hipEventRecord(st.ev[1], s));
-    MM_OK(reduce(nv1, 0));
+    MM_OK(hipEventRecord(st.ev[2 * (it - 1) + 1], s));
+    MM_OK(reduce_partials(a, nv1, 0, 1, s));
     MM_OK(hipMemsetAsync(a.active, 0, sizeof(uint32_t), s));
-    MM_OK(hipMemsetAsync(a.active_rows, 0, sizeof(unsigned long long), s));
-    hipLaunchKernelGGL(mm_solve_affine_kernel, dim3((unsigned)n_fits), dim3(64), lds_solve, s, a, K);
+    hipLaunchKernelGGL(mm_solve_affine_kernel, dim3((unsigned)n_fits), dim3(64), lds_solve, s, a, K,
+                       a.rp ? (it == 1 ? 1 : 2) : 0);
     MM_OK(hipGetLastError());
-    uint32_t active = 0;
-    unsigned long long arows = 0;
-    MM_OK(hipMemcpyAsync(&active, a.active, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    MM_OK(hipMemcpyAsync(&arows, a.active_rows, sizeof(arows), hipMemcpyDeviceToHost, s));
-    const auto ts = std::chrono::steady_clock::now();
-    MM_OK(hipStreamSynchronize(s));
-    st.sync_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
-    float ms = 0.f;
-    MM_OK(hipEventElapsedTime(&ms, st.ev[0], st.ev[1]));
-    st.assemble_ms += ms;
-    st.fit_rows += (double)live_rows;
-    live_rows = arows;
-    if (trace()) fprintf(stderr, "[mm] iteration %d: %u of %zu fits active\n", it, active, n_fits);
-    if (active == 0) break;
+    if (it % kCheckEvery == 0 || it == ob::kMmMaxIter) {
+      uint32_t active = 0;
+      MM_OK(hipMemcpyAsync(&active, a.active, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      const auto ts = std::chrono::steady_clock::now();
+      MM_OK(hipStreamSynchronize(s));
+      st.sync_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
+      if (trace()) fprintf(stderr, "[mm] iteration %d: %u of %zu fits active\n", it, active, n_fits);
+      if (active == 0) break;
+    }
     pass(K, 1, a, grid, 0, s);
     MM_OK(hipGetLastError());
-    MM_OK(reduce(nv2, 2));
+    MM_OK(reduce_partials(a, nv2, 2, 1, s));
     hipLaunchKernelGGL(mm_solve_corrector_kernel, dim3((unsigned)n_fits), dim3(64), lds_solve, s, a, K);
     MM_OK(hipGetLastError());
     pass(K, 2, a, grid, 0, s);
     MM_OK(hipGetLastError());
-    MM_OK(reduce(2, 2));
+    MM_OK(reduce_partials(a, 2, 2, 1, s));
     hipLaunchKernelGGL(mm_step_kernel, dim3((unsigned)((n_fits + 255) / 256)), dim3(256), 0, s, a, K, n_fits);
     MM_OK(hipGetLastError());
   }
+  {
+    unsigned long long rows = 0;
+    MM_OK(hipMemcpyAsync(&rows, a.active_rows, sizeof(rows), hipMemcpyDeviceToHost, s));
+    MM_OK(hipStreamSynchronize(s));
+    st.fit_rows += (double)rows;
+    for (int i = 0; i < std::min(it, ob::kMmMaxIter); ++i) {
+      float ms = 0.f;
+      MM_OK(hipEventElapsedTime(&ms, st.ev[2 * i], st.ev[2 * i + 1]));
+      st.assemble_ms += ms;
+    }
+  }
   if (trace()) {
-    std::vector<uint32_t> st(n_fits);
+    MM_OK(hipStreamSynchronize(s));
+    std::vector<uint32_t> fst(n_fits);
     std::vector<double> fsh(n_fits * kFs);
-    MM_OK(hipMemcpy(st.data(), a.fstat, sizeof(uint32_t) * n_fits, hipMemcpyDeviceToHost));
+    MM_OK(hipMemcpy(fst.data(), a.fstat, sizeof(uint32_t) * n_fits, hipMemcpyDeviceToHost));
     MM_OK(hipMemcpy(fsh.data(), a.fs, sizeof(double) * n_fits * kFs, hipMemcpyDeviceToHost));
     size_t done = 0, failed = 0, live = 0;
     for (size_t f = 0; f < n_fits; ++f) {
       if ((int)(f % a.S_pad) >= a.S) continue;
-      if (st[f] == kDone) ++done;
-      else if (st[f] & kFailed) ++failed;
+      if (fst[f] == kDone) ++done;
+      else if (fst[f] & kFailed) ++failed;
       else {
         if (live < 8)
           fprintf(stderr, "[mm] live fit %zu tau %.4f gap %.3e obj %.3e rel %.3e\n", f, fsh[f * kFs + FS_TAU],
@@ -1218,6 +1692,113 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, MmS
   }
   hipLaunchKernelGGL(mm_expire_kernel, dim3((unsigned)((n_fits + 255) / 256)), dim3(256), 0, s, a, n_fits);
   MM_OK(hipGetLastError());
+  st.iterations = std::max(st.iterations, std::min(it, ob::kMmMaxIter));
+  return OB_OK;
+}
+
+// Phases 2 (round 0: reduced problems from the bands) and 3 (round 1: the flagged fits on all rows).
+int reduced_round(const MmArgs& a, int K, int round, hipStream_t s, MmStats& st) {
+  const uint32_t nch = a.nch[0] + a.nch[1];
+  const size_t n_fits = (size_t)a.n_rb * 2 * a.S_pad;
+  const dim3 grid(nch, a.S_pad / 64, a.n_rb);
+  const unsigned fit_blocks = (unsigned)((n_fits + 255) / 256);
+  MM_OK(hipMemsetAsync(a.active_rows, 0, sizeof(unsigned long long), s));
+  pass(K, 3, a, grid, 0, s);  // classify: block lists + fixed-row sums
+  MM_OK(hipGetLastError());
+  MM_OK(reduce_partials(a, nv_cls(K), 0, 0, s));
+  hipLaunchKernelGGL(mm_bvec_kernel, dim3(fit_blocks), dim3(256), 0, s, a, K, n_fits, round == 0 ? 1 : 0);
+  MM_OK(hipGetLastError());
+  MmArgs a2 = a;
+  a2.block_lists = 1;
+  a2.rowlist = a.blist;
+  a2.nrows = a.bnrows;
+  a2.rp = 1;
+  return ipm(a2, K, 3, s, st);
+}
+
+// One batch of replicate slots: start, IPM iterations (with the row reduction: phase 1 on the
+// subsample, bands, phase 2 on the reduced lists, verification, phase 3 for flagged fits),
+// finish. Rows/ok -> host.
+int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, MmStats& st, const Reduction& rd) {
+  const size_t n_fits = (size_t)a.n_rb * 2 * a.S_pad;
+  const uint32_t nch = a.nch[0] + a.nch[1];
+  int m2 = 1;
+  while (m2 < a.S) m2 <<= 1;
+  if (!rd.on) {
+    OB_TRY(start_fits(a, K, s));
+    OB_TRY(ipm(a, K, 1, s, st));
+  } else {
+    hipLaunchKernelGGL(mm_rows_kernel, dim3(nch, 1, a.n_rb), dim3(256), 0, s, a);  // the full lists
+    MM_OK(hipGetLastError());
+    MmArgs a1 = a;  // phase 1: every kSubStride-th row, chunks of kRc * kSubStride rows
+    a1.rc = kRc1;
+    a1.stride = kSubStride;
+    a1.nch[0] = rd.nch1[0];
+    a1.nch[1] = rd.nch1[1];
+    a1.rowlist = rd.list1;
+    a1.nrows = rd.nrows1;
+    a1.tol = kPhase1Tol;
+    a1.gchol = rd.gchol;
+    const auto tb = std::chrono::steady_clock::now();
+    OB_TRY(start_fits(a1, K, s));
+    OB_TRY(ipm(a1, K, 1, s, st));
+    if (trace()) {
+      MM_OK(hipStreamSynchronize(s));
+      fprintf(stderr, "[mm] phase 1 done at %.1f ms\n",
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb).count());
+    }
+    hipLaunchKernelGGL(mm_sample_kernel, dim3(a.n_rb * 2), dim3(1024), 0, s, a);
+    MM_OK(hipGetLastError());
+    MmArgs al = a;
+    al.gchol = rd.gchol;
+    hipLaunchKernelGGL(mm_lev_kernel, dim3(nch, 1, a.n_rb), dim3(256), 0, s, al, K);
+    MM_OK(hipGetLastError());
+    hipLaunchKernelGGL(mm_band_kernel, dim3((unsigned)n_fits), dim3(256), 0, s, a, K);
+    MM_OK(hipGetLastError());
+    MM_OK(hipMemsetAsync(a.xmask, 0, sizeof(uint32_t) * (size_t)a.n_rb * nch * (a.S_pad / 64) * (kRc / 32), s));
+    // round 0: the bands; round 1: flagged fits, their bands plus the wrong-signed rows; round 2:
+    // fits flagged again, on all rows (no verification: nothing is fixed)
+    for (int round = 0; round < 3; ++round) {
+      OB_TRY(reduced_round(a, K, round, s, st));
+      if (round == 2) break;
+      MM_OK(hipMemsetAsync(a.active, 0, sizeof(uint32_t), s));
+      pass(K, 4, a, dim3(nch, a.S_pad / 64, a.n_rb), 0, s);  // verify the fixed rows' signs
+      MM_OK(hipGetLastError());
+      if (trace()) {  // why fits go to the next round: wrong-signed fixed rows or failures (with tau)
+        MM_OK(hipStreamSynchronize(s));
+        std::vector<uint32_t> fst(n_fits);
+        std::vector<double> fsh(n_fits * kFs);
+        MM_OK(hipMemcpy(fst.data(), a.fstat, sizeof(uint32_t) * n_fits, hipMemcpyDeviceToHost));
+        MM_OK(hipMemcpy(fsh.data(), a.fs, sizeof(double) * n_fits * kFs, hipMemcpyDeviceToHost));
+        int nv = 0, nf = 0;
+        for (size_t f = 0; f < n_fits; ++f) {
+          if ((int)(f % a.S_pad) >= a.S || fst[f] == kDone) continue;
+          const bool v = fst[f] & kRetry;
+          nv += v;
+          nf += !v;
+          if (nv + nf <= 6)
+            fprintf(stderr, "[mm]   fit %zu tau %.4f %s nact %.0f lo %.3g hi %.3g ext %.3g\n", f, fsh[f * kFs + FS_TAU],
+                    v ? "sign" : "failed", fsh[f * kFs + FS_NACT], fsh[f * kFs + FS_LO], fsh[f * kFs + FS_HI],
+                    fsh[f * kFs + FS_EXT]);
+        }
+        fprintf(stderr, "[mm] round %d at %.1f ms: %d fits with a wrong-signed fixed row, %d failures\n", round,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb).count(), nv, nf);
+      }
+      hipLaunchKernelGGL(mm_retry_kernel, dim3((unsigned)((n_fits + 255) / 256)), dim3(256), 0, s, a, K, n_fits,
+                         round == 1 ? 1 : 0);
+      MM_OK(hipGetLastError());
+      uint32_t retry = 0;
+      MM_OK(hipMemcpyAsync(&retry, a.active, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      MM_OK(hipStreamSynchronize(s));
+      st.retried += retry;
+      if (!retry) break;
+    }
+    if (trace()) {
+      MM_OK(hipStreamSynchronize(s));
+      fprintf(stderr, "[mm] batch done at %.1f ms\n",
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tb).count());
+    }
+  }
   const size_t lds_fin = (size_t)m2 * (3 * sizeof(double) + 2 * sizeof(uint16_t));
   MM_OK(hipFuncSetAttribute((const void*)mm_finish_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_fin));
   hipLaunchKernelGGL(mm_finish_kernel, dim3(a.n_rb), dim3(256), lds_fin, s, a, K, m2);
@@ -1225,7 +1806,6 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, MmS
   MM_OK(hipMemcpyAsync(rows_h, a.rows, sizeof(double) * a.n_rb * 3 * a.n_q, hipMemcpyDeviceToHost, s));
   MM_OK(hipMemcpyAsync(ok_h, a.ok, a.n_rb, hipMemcpyDeviceToHost, s));
   MM_OK(hipStreamSynchronize(s));
-  st.iterations = std::max(st.iterations, std::min(it, ob::kMmMaxIter));
   return OB_OK;
 }
 
@@ -1257,7 +1837,20 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   const uint64_t want = std::max<uint64_t>(n_reps, 1);
   const uint32_t rb_cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({want, 256, (48ull << 30) / state_per_rep}));
   const size_t fits = (size_t)rb_cap * 2 * S_pad;
-  const int nv_max = K * (K + 1) / 2 + K + 2 > 5 + 2 * K ? K * (K + 1) / 2 + K + 2 : 5 + 2 * K;
+  const int nv_max = nv_asm(K);  // >= 5 + 2 K (affine) and nv_cls(K)
+  // Row reduction: OB_MM_REDUCE=0 off, =1 on; by default on when both groups have >= 2^16 rows.
+  Reduction rd;
+  {
+    const char* e = getenv("OB_MM_REDUCE");
+    rd.on = e && *e ? (e[0] != '0') : (p->n[0] >= 65536u && p->n[1] >= 65536u);
+  }
+  const uint32_t rc1 = kRc1;
+  rd.nch1[0] = (p->n[0] + rc1 - 1) / rc1;
+  rd.nch1[1] = (p->n[1] + rc1 - 1) / rc1;
+  const size_t nfb = (size_t)S_pad / 64;
+  const size_t lists_full = (size_t)rb_cap * (nch0 + nch1), lists_blk = rd.on ? lists_full * nfb : 0,
+               lists_p1 = rd.on ? (size_t)rb_cap * (rd.nch1[0] + rd.nch1[1]) : 0;
+  const size_t n_lists = lists_full + lists_blk + lists_p1;
   if (!p->mm_ws) {
     p->mm_ws = new Buffers();
     p->mm_ws_free = free_workspace;
@@ -1271,7 +1864,10 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
                            d8 * fits * kFs, d8 * (size_t)rb_cap * (nch0 + nch1) * S_pad * nv_max,
                            d8 * fits * nv_max, d8 * n_q, d8 * rb_cap * 3 * n_q, u4 * fits, u4,
                            sizeof(unsigned long long), u4 * rb_cap * 2 * (p->ntiles[0] + 1 + nt1 + 1), u4 * fits,
-                           u4 * (size_t)rb_cap * (nch0 + nch1) * kRc, u4 * (size_t)rb_cap * (nch0 + nch1), rb_cap};
+                           u4 * n_lists * kRc, u4 * n_lists, rb_cap, d8 * fits * K, d8 * fits * K,
+                           d8 * fits * K, u4 * (size_t)rb_cap * 2 * 2 * kBandSamples, u4 * (size_t)rb_cap * 2,
+                           d8 * (size_t)rb_cap * 2 * (K * K + 1), d8 * lists_full * kRc,
+                           u4 * (lists_blk ? lists_blk : 1) * (kRc / 32)};
   MM_OK(b.reserve(need));
   MM_OK(hipMemcpy(b.quant, quantiles, sizeof(double) * n_q, hipMemcpyHostToDevice));
 
@@ -1306,6 +1902,21 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   a.lane_of = b.lane_of;
   a.rowlist = b.rowlist;
   a.nrows = b.nrows;
+  a.rc = kRc;
+  a.stride = 1;
+  a.tol = kTol;
+  a.blist = b.rowlist + lists_full * kRc;
+  a.bnrows = b.nrows + lists_full;
+  rd.list1 = b.rowlist + (lists_full + lists_blk) * kRc;
+  rd.nrows1 = b.nrows + lists_full + lists_blk;
+  rd.gchol = b.gchol;
+  a.bvec = b.bvec;
+  a.rpv = b.rpv;
+  a.bhat = b.bhat;
+  a.samp = b.samp;
+  a.nsamp = b.nsamp;
+  a.lev = b.lev;
+  a.xmask = b.xmask;
   a.key0 = (uint32_t)seed;
   a.key1 = (uint32_t)(seed >> 32);
   a.n_q = n_q;
@@ -1314,22 +1925,13 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   a.ok = b.ok;
   const auto t0 = std::chrono::steady_clock::now();
   MmStats st;
-  MM_OK(hipEventCreate(&st.ev[0]));
-  MM_OK(hipEventCreate(&st.ev[1]));
-  struct EvGuard {
-    MmStats& s;
-    ~EvGuard() {
-      for (hipEvent_t e : s.ev)
-        if (e) (void)hipEventDestroy(e);
-    }
-  } evg{st};
   size_t out = 0;
   if (with_point) {  // every row once, MM-1 replicate OB_MM_POINT_REP
     MmArgs pa = a;
     pa.n_rb = 1;
     pa.rep0 = OB_MM_POINT_REP;
     pa.counts = nullptr;
-    OB_TRY(run_batch(pa, K, s, rows, ok, st));
+    OB_TRY(run_batch(pa, K, s, rows, ok, st, rd));
     out = 1;
   }
   // resamples: OBRS-1 count images per segment, then batches of rb_cap slots
@@ -1347,7 +1949,7 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
       ba.m1 = p->d_m1;
       ba.nb_rep = nb_rep;
       ba.rep_pad = rep_pad;
-      OB_TRY(run_batch(ba, K, s, rows + (out + s0 + b0) * 3 * n_q, ok + out + s0 + b0, st));
+      OB_TRY(run_batch(ba, K, s, rows + (out + s0 + b0) * 3 * n_q, ok + out + s0 + b0, st, rd));
     }
   }
   uint32_t flag = 0;
@@ -1357,6 +1959,8 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   p->timing.mm_fit_rows = st.fit_rows;
   p->timing.mm_iterations = st.iterations;
   p->timing.mm_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  p->timing.mm_reduced = rd.on ? 1 : 0;
+  p->timing.mm_retried = (int64_t)st.retried;
   if (trace())
     fprintf(stderr, "[mm] call: %.1f ms, %.1f ms waiting in per-iteration syncs, assemble %.1f ms\n", p->timing.mm_ms,
             st.sync_ms, st.assemble_ms);

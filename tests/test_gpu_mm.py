@@ -150,3 +150,51 @@ def test_mm_identities_at_size(ob):
     assert np.allclose(r[..., 1] + r[..., 2], r[..., 0], rtol=0, atol=1e-9)
     # the point gap at the median approximates the difference of the groups' median outcomes
     assert abs(r[0, 2, 0] - (np.median(d["ya"]) - np.median(d["yb"]))) < 0.3
+
+
+@pytest.fixture
+def reduce_env(monkeypatch):
+    """OB_MM_REDUCE: 1 forces the row reduction (subsample, bands, reduced LPs, verification) at
+    any size, 0 turns it off; unset, it runs when both groups have >= 2^16 rows."""
+    def set_(v):
+        monkeypatch.setenv("OB_MM_REDUCE", v)
+    return set_
+
+
+@pytest.mark.parametrize("n,p,sims", [(3000, 2, 40), (6000, 5, 24), (20000, 15, 8)])
+def test_mm_row_reduction_matches_oracle(ob, O, reduce_env, n, p, sims):
+    """Forced row reduction against the oracle's HiGHS-exact fits: when every fixed row's sign
+    verifies, the reduced LP's optimum is the full LP's (Portnoy & Koenker 1997)."""
+    reduce_env("1")
+    d = mm_data(n, p, seed=n + p + 1)
+    panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"])
+    try:
+        rows, ok = panel.mm(SEED, sims, QS, 0, 3)
+        t = panel.timing()
+    finally:
+        panel.close()
+    assert t["mm_reduced"] == 1
+    want = oracle_rows(O, d, sims, QS, 3)
+    assert ok.all()
+    good, worst = close(rows, want, np.abs(want).max())
+    assert good, worst
+
+
+def test_mm_row_reduction_equals_full_solve(ob, reduce_env):
+    """At 150k rows (K = 16) the default path reduces; its rows equal the unreduced solve's (both
+    reach the same LP optima, to the IPM's 1e-12 gap)."""
+    d = mm_data(150_000, 15, seed=21)
+    panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"])
+    try:
+        reduce_env("")
+        r1, k1 = panel.mm(SEED, 128, QS, 0, 2)
+        t1 = panel.timing()
+        reduce_env("0")
+        r0, k0 = panel.mm(SEED, 128, QS, 0, 2)
+        t0 = panel.timing()
+    finally:
+        panel.close()
+    assert t1["mm_reduced"] == 1 and t0["mm_reduced"] == 0
+    assert k1.all() and k0.all()
+    assert np.allclose(r1, r0, rtol=0, atol=1e-8 * np.abs(r0).max()), np.abs(r1 - r0).max()
+    assert t1["mm_fit_rows"] < t0["mm_fit_rows"], (t1["mm_fit_rows"], t0["mm_fit_rows"])
