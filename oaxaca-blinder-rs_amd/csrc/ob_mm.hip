@@ -1160,11 +1160,13 @@ __global__ __launch_bounds__(256) void mm_band_kernel(const MmArgs a, int K) {
 // VERIFY:  at the reduced optimum beta, a fixed row whose residual has the wrong sign flags its fit
 //          for phase 3 (kRetry).
 template <int K, bool VERIFY>
-__global__ __launch_bounds__(256) void mm_classify_kernel(const MmArgs a) {
+__global__ __launch_bounds__(256, 2) void mm_classify_kernel(const MmArgs a) {
   constexpr int NXB = Xs<K>::NXB, S = Xs<K>::S, NVC = nv_cls(K), ND = VERIFY ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) double xs[kSub * S];
+  __shared__ __attribute__((aligned(16))) double xs[2][kSub * S];
   __shared__ uint32_t lst[kRc];
-  __shared__ uint32_t keep[kSub];
+  __shared__ uint32_t keep[2][kSub];
+  __shared__ double levs[2][kSub];  // the sub-tile's leverages and added-row bits, staged with xs
+  __shared__ uint32_t xbits[2][kSub];
   __shared__ uint32_t nkeep;
   const Blk b = blk_ctx(a, lst, true);
   const bool part = b.s < a.S;
@@ -1188,41 +1190,70 @@ __global__ __launch_bounds__(256) void mm_classify_kernel(const MmArgs a) {
   const size_t oi = li * (a.S_pad / 64) + b.fb;
   uint32_t* out = a.blist + oi * kRc;
   uint32_t* xm = a.xmask + oi * (kRc / 32);
-  const bool check = VERIFY && part && lo <= hi;  // fits of this round (the others have empty bands)
-  __syncthreads();  // lst
+  const bool mine = part && lo <= hi;  // a fit of this round (the others have empty bands)
+  const bool check = VERIFY && mine;
+  if (!__syncthreads_or(mine)) {  // no fit of the block takes part: an empty list
+    if (!VERIFY && threadIdx.x == 0) a.bnrows[oi] = 0u;
+    return;
+  }
   const uint32_t nsub = (b.n_ent + kSub - 1) / kSub;
+  double stg[Xs<K>::Stage], lv = 0.0;
+  uint32_t xb1 = 0u;
+  auto side_load = [&](uint32_t t) {  // threads < 64: row t * kSub + tid's leverage and added bit
+    const uint32_t e = t * kSub + threadIdx.x;
+    if (threadIdx.x < kSub && e < b.n_ent) {
+      lv = a.lev[li * kRc + e];
+      xb1 = (xm[e >> 5] >> (e & 31u)) & 1u;
+    }
+  };
+  auto side_store = [&](int buf) {
+    if (threadIdx.x < kSub) {
+      levs[buf][threadIdx.x] = lv;
+      xbits[buf][threadIdx.x] = xb1;
+      keep[buf][threadIdx.x] = 0u;
+    }
+  };
+  xs_load<K>(a, b, lst, 0, stg);  // lst: published by the barrier above
+  side_load(0);
+  xs_store<K>(xs[0], stg);
+  side_store(0);
+  __syncthreads();
   for (uint32_t t = 0; t < nsub; ++t) {
-    if (threadIdx.x < kSub) keep[threadIdx.x] = 0u;
-    double stg[Xs<K>::Stage];
-    xs_load<K>(a, b, lst, t, stg);
-    xs_store<K>(xs, stg);
-    __syncthreads();
-    uint32_t side = 0;
-    double rv[16];
+    const double* X = xs[t & 1];
+    uint32_t* kp = keep[t & 1];
+    xs_load<K>(a, b, lst, t + 1, stg);  // the next sub-tile's values, in flight during this one
+    side_load(t + 1);
+    const double* LV = levs[t & 1];
+    const uint32_t* XB = xbits[t & 1];
+    uint32_t side = 0, wrong = 0;  // wrong: bit j = step j's residual at beta has the other sign (VERIFY)
     mm_d4 dots[ND];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      if ((j & 3) == 0) group_dots<K, ND>(xs, j >> 2, b, fb, dots);
+      if ((j & 3) == 0) group_dots<K, ND>(X, j >> 2, b, fb, dots);
       const uint32_t e = t * kSub + 4 * j + b.rl;
       const bool valid = part && e < b.n_ent;
-      const double y = xs[(4 * j + b.rl) * S + Xs<K>::Y];
+      const double y = X[(4 * j + b.rl) * S + Xs<K>::Y];
       const double rh = y - dots[0][j & 3];
-      const double x = valid ? ext * fmax(a.lev[li * kRc + e] - sqk, 0.0) : 0.0;  // leverage widening
+      const double x = valid ? ext * fmax(LV[4 * j + b.rl] - sqk, 0.0) : 0.0;  // leverage widening
       const bool in = valid && rh >= lo - x && rh <= hi + x;
       side |= (in ? 1u : (rh > hi + x ? 2u : 0u)) << (2 * j);
       // rows added after an earlier verification are in the list too (a row flagged in this pass
       // is set after the barrier below, so within a sub-tile the bits read here are the old ones)
-      if (in || (e < b.n_ent && ((xm[e >> 5] >> (e & 31u)) & 1u))) keep[4 * j + b.rl] = 1u;
-      rv[j] = VERIFY ? y - dots[ND - 1][j & 3] : 0.0;
+      if (in || (e < b.n_ent && XB[4 * j + b.rl])) kp[4 * j + b.rl] = 1u;
+      if (VERIFY) {
+        const double rv = y - dots[ND - 1][j & 3], eps = 1e-9 * (1.0 + fabs(y));
+        const uint32_t sd = in ? 1u : (rh > hi + x ? 2u : 0u);
+        wrong |= (sd == 2u ? rv < -eps : (sd == 0u && rv > eps)) ? 1u << j : 0u;
+      }
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const uint32_t e = t * kSub + 4 * j + b.rl;
       const bool valid = part && e < b.n_ent;
-      const bool kept = keep[4 * j + b.rl] != 0u;
+      const bool kept = kp[4 * j + b.rl] != 0u;
       const uint32_t sd = (side >> (2 * j)) & 3u;
-      const double* xr = xs + (4 * j + b.rl) * S;
+      const double* xr = X + (4 * j + b.rl) * S;
       const double y = xr[Xs<K>::Y];
       if (!VERIFY) {
         const double c = valid ? (double)(lst[e] & 255u) : 0.0;
@@ -1234,22 +1265,21 @@ __global__ __launch_bounds__(256) void mm_classify_kernel(const MmArgs a) {
           A[xb] = __builtin_amdgcn_mfma_f64_16x16x4f64(ab, bx, A[xb], 0, 0, 0);
           T[xb] = __builtin_amdgcn_mfma_f64_16x16x4f64(c, bx, T[xb], 0, 0, 0);
         }
-      } else if (check && valid && !kept && sd != 1u) {
-        const double eps = 1e-9 * (1.0 + fabs(y));
-        if (sd == 2u ? rv[j] < -eps : rv[j] > eps) {  // the row joins the block's list next round
-          bad = true;
-          atomicOr(&xm[e >> 5], 1u << (e & 31u));
-        }
+      } else if (check && valid && !kept && ((wrong >> j) & 1u)) {  // the row joins the block's list next round
+        bad = true;
+        atomicOr(&xm[e >> 5], 1u << (e & 31u));
       }
     }
     if (!VERIFY && b.wave == 0) {  // the kept rows of this sub-tile, in row order
       const uint32_t e = t * kSub + b.lane;
-      const bool f = e < b.n_ent && keep[b.lane] != 0u;
+      const bool f = e < b.n_ent && kp[b.lane] != 0u;
       const unsigned long long m = __ballot(f);
       const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
       if (f) out[cnt + below] = lst[e];
       cnt += (uint32_t)__popcll(m);
     }
+    xs_store<K>(xs[(t + 1) & 1], stg);  // the other buffers were last read before the previous barrier
+    side_store((t + 1) & 1);
     __syncthreads();
   }
   if (!VERIFY) {

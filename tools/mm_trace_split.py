@@ -11,8 +11,8 @@ prev_end = None
 first = int(rows[0]["Start_Timestamp"])
 for r in rows:
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-    name = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("(anonymous namespace)::", "")
-    name = name.split("::")[-1]
+    name = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+    name = name.split("(")[0]
     key = (name, int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"])))
     tot[key][0] += 1
     tot[key][1] += (e - s) / 1e6
