@@ -50,11 +50,17 @@ namespace {
 constexpr double kEta = 0.99995;  // fraction of the distance to the boundary per step
 constexpr double kTol = 1e-12;    // relative duality gap at convergence
 constexpr uint32_t kDone = 1u, kFailed = 2u, kRetry = 4u;
-constexpr uint32_t kRc = 2048;  // rows (list entries) per chunk (a function of the panel only: determinism)
+// Chunk geometry (a function of the panel only: determinism). A chunk's nonzero-count rows form one
+// list (per fit block after the reduction); a block walks one list.
+constexpr uint32_t kRc = 2048;       // rows per chunk without the row reduction
+constexpr uint32_t kRcF = 8192;      // with it: the full and reduced lists (longer walks, 4x fewer partials)
+constexpr uint32_t kCap = 8192;      // list capacity bound (LDS copies of a list)
 constexpr uint32_t kSubStride = 8;   // phase 1 of the row reduction: every 8th row ...
-constexpr uint32_t kRc1 = kRc * kSubStride / 4;  // ... in chunks of 4096 rows (512 candidates: short walks)
+constexpr uint32_t kRc1 = 4096;      // ... in chunks of 4096 rows (512 candidates: short walks)
+static_assert(kRc <= kCap && kRcF <= kCap && kRc1 / kSubStride <= kCap, "lists fit the LDS copies");
 constexpr double kPhase1Tol = 1e-6;  // phase-1 relative gap (beta_hat only centres the bands)
 constexpr double kBandKappa = 4.0;   // band half-width in rank units: kappa sqrt(tau (1 - tau) K / m) + 0.01
+                                     // (OB_MM_KAPPA overrides it: a tuning knob; results do not depend on it)
 constexpr int kBandSamples = 4096;   // residuals per fit behind its band quantiles
 
 enum { FS_TAU, FS_GAP, FS_OBJ, FS_MU, FS_SIGMU, FS_AP, FS_AD, FS_NACT, FS_DELTA, FS_LO, FS_HI, FS_EXT, FS_OBJFIX, kFs };
@@ -98,21 +104,22 @@ struct MmArgs {
   unsigned long long* active_rows;   // live (fit, row) pairs of the next passes
   uint32_t* tprefix;                 // [slot][group][tiles + 1] (finish kernel scratch)
   uint32_t* lane_of;                 // [slot][group][simulation] -> fit lane (lanes in ascending tau)
-  uint32_t* rowlist;                 // [slot][chunk (A then B)][kRc] nonzero-count rows (mm_rows_kernel)
+  uint32_t* rowlist;                 // [slot][chunk (A then B)][cap] nonzero-count rows (mm_rows_kernel)
   uint32_t* nrows;                   // [slot][chunk] list lengths
-  uint32_t rc;                       // rows per chunk of this phase (kRc; kRc * kSubStride in phase 1)
+  uint32_t rc;                       // rows per chunk of this phase (kRc; kRcF / kRc1 with the reduction)
   uint32_t stride;                   // mm_rows_kernel: every stride-th row (phase 1) or all (1)
+  uint32_t cap;                      // list capacity: rc / stride entries (a multiple of 256)
   uint32_t block_lists;              // lists per (slot, chunk, fit block) (phase 2/3) instead of per chunk
   int rp;                            // X'x = b per fit (phase 2/3): primal residual in the solves
   double tol;                        // relative duality gap at convergence
-  uint32_t* blist;                   // mm_classify_kernel output: [slot][chunk][fit block][kRc]
+  uint32_t* blist;                   // mm_classify_kernel output: [slot][chunk][fit block][cap]
   uint32_t* bnrows;                  // [slot][chunk][fit block]
   double *bvec, *rpv, *bhat;         // [fit][K]: b, b - X'x of the iterate, phase-1 beta (band centres)
   uint32_t* samp;                    // [slot][group][2][kBandSamples]: sampled rows, counts
   uint32_t* nsamp;                   // [slot][group]
   double* gchol;                     // [slot][group][K * K + 1]: Cholesky factor of the phase-1 OLS Gram, sum c
-  double* lev;                       // [slot][chunk][kRc]: leverage sqrt(n x_i' G^-1 x_i) per full-list entry
-  uint32_t* xmask;                   // [slot][chunk][fit block][kRc / 32]: rows added to the block's list
+  double* lev;                       // [slot][chunk][cap]: leverage sqrt(n x_i' G^-1 x_i) per full-list entry
+  uint32_t* xmask;                   // [slot][chunk][fit block][cap / 32]: rows added to the block's list
                                      // after a wrong-signed verification (mm_verify)
   uint32_t key0, key1;
   int n_q;
@@ -159,23 +166,21 @@ constexpr int kRing = 4;    // wave steps of state in flight (affine / final)
 constexpr int kRingA = 4;   // the same for the assemble pass (its fragments sit in LDS to make room)
 constexpr int kStoreAt = 4; // step after which the next sub-tile's staged values are written
 typedef double mm_d4 __attribute__((ext_vector_type(4)));
-static_assert(kRc % 256 == 0 && kRc / 256 == 8, "mm_rows_kernel: 8 rows per thread");
 static_assert(16 % kRing == 0, "ring slots are static per unrolled step");
 
 // Nonzero-count rows of each (slot, chunk) in ascending order: (row - chunk start) << 8 | count.
-// A chunk spans a.rc rows, of which every a.stride-th is a candidate (kRc candidates per chunk).
+// A chunk spans a.rc rows, of which every a.stride-th is a candidate (a.cap candidates: a.cap / 256
+// consecutive ones per thread, counted, scanned, then written).
 __global__ __launch_bounds__(256) void mm_rows_kernel(const MmArgs a) {
   __shared__ uint32_t scan[256];
   const uint32_t gch = blockIdx.x, slot = blockIdx.z, nch = a.nch[0] + a.nch[1];
   const uint32_t g = gch >= a.nch[0] ? 1u : 0u;
   const uint32_t r0 = (gch - (g ? a.nch[0] : 0u)) * a.rc, nr = min(a.n[g] - r0, a.rc);
-  const uint32_t i0 = threadIdx.x * 8;
-  uint32_t c[8], k = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  const uint32_t per = a.cap / 256, i0 = threadIdx.x * per;
+  uint32_t k = 0;
+  for (uint32_t i = 0; i < per; ++i) {
     const uint32_t off = (i0 + i) * a.stride;
-    c[i] = off < nr ? row_count(a, slot, g, r0 + off) : 0u;
-    k += c[i] != 0u;
+    k += (off < nr && row_count(a, slot, g, r0 + off) != 0u) ? 1u : 0u;
   }
   scan[threadIdx.x] = k;
   __syncthreads();
@@ -186,10 +191,12 @@ __global__ __launch_bounds__(256) void mm_rows_kernel(const MmArgs a) {
     __syncthreads();
   }
   uint32_t o = scan[threadIdx.x] - k;
-  uint32_t* L = a.rowlist + ((size_t)slot * nch + gch) * kRc;
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-    if (c[i]) L[o++] = (((i0 + i) * a.stride) << 8) | c[i];
+  uint32_t* L = a.rowlist + ((size_t)slot * nch + gch) * a.cap;
+  for (uint32_t i = 0; i < per; ++i) {
+    const uint32_t off = (i0 + i) * a.stride;
+    const uint32_t c = off < nr ? row_count(a, slot, g, r0 + off) : 0u;
+    if (c) L[o++] = (off << 8) | c;
+  }
   if (threadIdx.x == 255) a.nrows[(size_t)slot * nch + gch] = scan[255];
 }
 
@@ -221,11 +228,11 @@ __device__ __forceinline__ Blk blk_ctx(const MmArgs& a, uint32_t* lst, bool all_
   b.X = a.cols[b.g];
   b.ld = a.ld[b.g];
   const size_t li = (size_t)b.slot * (a.nch[0] + a.nch[1]) + b.gch;
-  b.sb = (li * (a.S_pad / 64) + b.fb) * ((size_t)kRc * 64) + b.wave * 64 + b.fl;
+  b.sb = (li * (a.S_pad / 64) + b.fb) * ((size_t)a.cap * 64) + b.wave * 64 + b.fl;
   b.any = __syncthreads_or(b.live) != 0;
   const size_t lli = a.block_lists ? li * (a.S_pad / 64) + b.fb : li;  // this block's row list
   b.n_ent = b.any ? a.nrows[lli] : 0u;
-  const uint32_t* L = a.rowlist + lli * kRc;
+  const uint32_t* L = a.rowlist + lli * a.cap;
   for (uint32_t i = threadIdx.x; i < b.n_ent; i += 256) lst[i] = L[i];
   return b;
 }
@@ -386,7 +393,7 @@ __global__ __launch_bounds__(256, K <= 16 ? 2 : 1) void mm_assemble_mfma_kernel(
   constexpr int NCB = (NP + 15) / 16;
   constexpr int NXB = Xs<K>::NXB;  // X'Q r column blocks
   __shared__ __attribute__((aligned(16))) double xs[2][kSub * Xs<K>::S];
-  __shared__ uint32_t lst[kRc];
+  __shared__ uint32_t lst[kCap];
   const Blk b = blk_ctx(a, lst, mode == 0);
   if (!b.any) return;  // partials of dead fits are never reduced
   constexpr int NDOT = STEP ? 3 : 1;  // x_i . (bprev, dba, db) or x_i . beta
@@ -601,7 +608,7 @@ __global__ __launch_bounds__(256, K <= 16 ? 3 : 2) void mm_affine_kernel(const M
   constexpr int NV = 5 + 2 * K;
   constexpr int NXB = Xs<K>::NXB;
   __shared__ __attribute__((aligned(16))) double xs[2][kSub * Xs<K>::S];
-  __shared__ uint32_t lst[kRc];
+  __shared__ uint32_t lst[kCap];
   const Blk b = blk_ctx(a, lst, false);
   if (!b.any) return;  // partials of dead fits are never reduced
   double fb[2][(K + 3) / 4];
@@ -657,7 +664,7 @@ __global__ __launch_bounds__(256, K <= 16 ? 3 : 2) void mm_affine_kernel(const M
 template <int K>
 __global__ __launch_bounds__(256, 2) void mm_final_kernel(const MmArgs a) {
   __shared__ __attribute__((aligned(16))) double xs[2][kSub * Xs<K>::S];
-  __shared__ uint32_t lst[kRc];
+  __shared__ uint32_t lst[kCap];
   const Blk b = blk_ctx(a, lst, false);
   if (!b.any) return;  // partials of dead fits are never reduced
   double fb[3][(K + 3) / 4];
@@ -808,7 +815,7 @@ __global__ __launch_bounds__(1024) void mm_shift_kernel(const MmArgs a, int K) {
   const size_t F0 = fit_index(a, slot, g, 0);
   if (a.fstat[F0] & kFailed) return;  // no OLS start for this group: every fit failed already
   const size_t li0 = (size_t)slot * nch + c0;
-  // inclusive prefix of the chunk list lengths (ncg <= 1024 chunks of kRc rows: n_g < 2^21)
+  // inclusive prefix of the chunk list lengths (ncg <= 1024 chunks)
   for (uint32_t c = threadIdx.x; c < ncg; c += blockDim.x) pre[c + 1] = a.nrows[li0 + c];
   if (threadIdx.x == 0) pre[0] = 0;
   if (threadIdx.x < (unsigned)K) beta[threadIdx.x] = a.beta[F0 * K + threadIdx.x];
@@ -828,7 +835,7 @@ __global__ __launch_bounds__(1024) void mm_shift_kernel(const MmArgs a, int K) {
         if (pre[mid] <= e) lo = mid;
         else hi = mid;
       }
-      const uint32_t ent = a.rowlist[(li0 + lo) * kRc + (e - pre[lo])];
+      const uint32_t ent = a.rowlist[(li0 + lo) * a.cap + (e - pre[lo])];
       const uint32_t row = lo * a.rc + (ent >> 8);
       const double* X = a.cols[g];
       double xb = beta[0];
@@ -998,7 +1005,7 @@ __global__ __launch_bounds__(1024) void mm_sample_kernel(const MmArgs a) {
       if (pre[mid] <= e) lo = mid;
       else hi = mid;
     }
-    const uint32_t ent = a.rowlist[(li0 + lo) * kRc + (e - pre[lo])];
+    const uint32_t ent = a.rowlist[(li0 + lo) * a.cap + (e - pre[lo])];
     out[j] = lo * a.rc + (ent >> 8);
     out[kBandSamples + j] = ent & 255u;
   }
@@ -1020,7 +1027,7 @@ __global__ __launch_bounds__(256) void mm_lev_kernel(const MmArgs a, int K) {
   const uint32_t ne = a.nrows[li], r0 = (gch - (g ? a.nch[0] : 0u)) * a.rc;
   const double* X = a.cols[g];
   for (uint32_t e = threadIdx.x; e < ne; e += 256) {
-    const uint32_t row = r0 + (a.rowlist[li * kRc + e] >> 8);
+    const uint32_t row = r0 + (a.rowlist[li * a.cap + e] >> 8);
     double v[ob::kMmMaxK], q = 0.0;
     for (int i = 0; i < K; ++i) {  // L v = x (forward substitution), q = |v|^2
       double t = i ? X[(size_t)(i - 1) * a.ld[g] + row] : 1.0;
@@ -1028,7 +1035,7 @@ __global__ __launch_bounds__(256) void mm_lev_kernel(const MmArgs a, int K) {
       v[i] = t / L[i + i * K];
       q += v[i] * v[i];
     }
-    a.lev[li * kRc + e] = n > 0.0 ? sqrt(n * q) : sqrt((double)K);
+    a.lev[li * a.cap + e] = n > 0.0 ? sqrt(n * q) : sqrt((double)K);
   }
 }
 
@@ -1036,7 +1043,7 @@ __global__ __launch_bounds__(256) void mm_lev_kernel(const MmArgs a, int K) {
 // [lo, hi] = the count-weighted tau -/+ delta quantiles of the sampled residuals at beta_hat, with
 // delta = kappa sqrt(tau (1 - tau) K / m) + 0.01 (m = the phase-1 sample's rows). A fit whose
 // phase 1 failed keeps every row (band = the real line); padding fits keep none.
-__global__ __launch_bounds__(256) void mm_band_kernel(const MmArgs a, int K) {
+__global__ __launch_bounds__(256) void mm_band_kernel(const MmArgs a, int K, double kappa) {
   __shared__ double key[kBandSamples];
   __shared__ double wt[kBandSamples];
   __shared__ double beta[ob::kMmMaxK];
@@ -1066,7 +1073,7 @@ __global__ __launch_bounds__(256) void mm_band_kernel(const MmArgs a, int K) {
     a.bhat[F * K + t] = beta[t];
   }
   const double tau = f[FS_TAU];
-  const double delta = kBandKappa * sqrt(tau * (1.0 - tau) * K / fmax(f[FS_NACT], 1.0)) + 0.01;
+  const double delta = kappa * sqrt(tau * (1.0 - tau) * K / fmax(f[FS_NACT], 1.0)) + 0.01;
   if ((a.fstat[F] & kFailed) || (tau - delta <= 0.0 && tau + delta >= 1.0)) {
     if (t == 0) {
       f[FS_LO] = -INFINITY;
@@ -1148,7 +1155,7 @@ __global__ __launch_bounds__(256) void mm_band_kernel(const MmArgs a, int K) {
     f[FS_LO] = lo;
     f[FS_HI] = hi;
     // per unit of leverage above sqrt(K): kappa standard errors of x_i beta_hat
-    f[FS_EXT] = kBandKappa * sqrt(tau * (1.0 - tau) / fmax(f[FS_NACT], 1.0)) * slope;
+    f[FS_EXT] = kappa * sqrt(tau * (1.0 - tau) / fmax(f[FS_NACT], 1.0)) * slope;
   }
 }
 
@@ -1163,7 +1170,7 @@ template <int K, bool VERIFY>
 __global__ __launch_bounds__(256, 2) void mm_classify_kernel(const MmArgs a) {
   constexpr int NXB = Xs<K>::NXB, S = Xs<K>::S, NVC = nv_cls(K), ND = VERIFY ? 2 : 1;
   __shared__ __attribute__((aligned(16))) double xs[2][kSub * S];
-  __shared__ uint32_t lst[kRc];
+  __shared__ uint32_t lst[kCap];
   __shared__ uint32_t keep[2][kSub];
   __shared__ double levs[2][kSub];  // the sub-tile's leverages and added-row bits, staged with xs
   __shared__ uint32_t xbits[2][kSub];
@@ -1188,8 +1195,8 @@ __global__ __launch_bounds__(256, 2) void mm_classify_kernel(const MmArgs a) {
   bool bad = false;
   uint32_t cnt = 0;  // wave 0: entries of the block's list so far
   const size_t oi = li * (a.S_pad / 64) + b.fb;
-  uint32_t* out = a.blist + oi * kRc;
-  uint32_t* xm = a.xmask + oi * (kRc / 32);
+  uint32_t* out = a.blist + oi * a.cap;
+  uint32_t* xm = a.xmask + oi * (a.cap / 32);
   const bool mine = part && lo <= hi;  // a fit of this round (the others have empty bands)
   const bool check = VERIFY && mine;
   if (!__syncthreads_or(mine)) {  // no fit of the block takes part: an empty list
@@ -1202,7 +1209,7 @@ __global__ __launch_bounds__(256, 2) void mm_classify_kernel(const MmArgs a) {
   auto side_load = [&](uint32_t t) {  // threads < 64: row t * kSub + tid's leverage and added bit
     const uint32_t e = t * kSub + threadIdx.x;
     if (threadIdx.x < kSub && e < b.n_ent) {
-      lv = a.lev[li * kRc + e];
+      lv = a.lev[li * a.cap + e];
       xb1 = (xm[e >> 5] >> (e & 31u)) & 1u;
     }
   };
@@ -1760,8 +1767,9 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, MmS
   } else {
     hipLaunchKernelGGL(mm_rows_kernel, dim3(nch, 1, a.n_rb), dim3(256), 0, s, a);  // the full lists
     MM_OK(hipGetLastError());
-    MmArgs a1 = a;  // phase 1: every kSubStride-th row, chunks of kRc * kSubStride rows
+    MmArgs a1 = a;  // phase 1: every kSubStride-th row, chunks of kRc1 rows
     a1.rc = kRc1;
+    a1.cap = kRc1 / kSubStride;
     a1.stride = kSubStride;
     a1.nch[0] = rd.nch1[0];
     a1.nch[1] = rd.nch1[1];
@@ -1783,9 +1791,14 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, MmS
     al.gchol = rd.gchol;
     hipLaunchKernelGGL(mm_lev_kernel, dim3(nch, 1, a.n_rb), dim3(256), 0, s, al, K);
     MM_OK(hipGetLastError());
-    hipLaunchKernelGGL(mm_band_kernel, dim3((unsigned)n_fits), dim3(256), 0, s, a, K);
+    static const double kappa = [] {
+      const char* e = getenv("OB_MM_KAPPA");
+      const double v = e ? atof(e) : 0.0;
+      return v > 0.0 ? v : kBandKappa;
+    }();
+    hipLaunchKernelGGL(mm_band_kernel, dim3((unsigned)n_fits), dim3(256), 0, s, a, K, kappa);
     MM_OK(hipGetLastError());
-    MM_OK(hipMemsetAsync(a.xmask, 0, sizeof(uint32_t) * (size_t)a.n_rb * nch * (a.S_pad / 64) * (kRc / 32), s));
+    MM_OK(hipMemsetAsync(a.xmask, 0, sizeof(uint32_t) * (size_t)a.n_rb * nch * (a.S_pad / 64) * (a.cap / 32), s));
     // round 0: the bands; round 1: flagged fits, their bands plus the wrong-signed rows; round 2:
     // fits flagged again, on all rows (no verification: nothing is fixed)
     for (int round = 0; round < 3; ++round) {
@@ -1857,29 +1870,33 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   hipStream_t s = ctx->stream;
   const int S_pad = (sims + 63) / 64 * 64;
   const size_t rep_rows = (size_t)p->n[0] + p->n[1];
-  const uint32_t nch0 = (p->n[0] + kRc - 1) / kRc, nch1 = (p->n[1] + kRc - 1) / kRc;
-  if (nch0 > 1024 || nch1 > 1024)  // mm_shift_kernel's chunk prefix
+  if (p->n[0] > 1024u * kRc || p->n[1] > 1024u * kRc)  // mm_shift_kernel's chunk prefix (1024 chunks)
     return ob::fail(OB_E_UNSUPPORTED, "Machado-Mata groups take at most %u rows", 1024u * kRc);
-  // replicate slots per batch: IPM state (x, z, w: 3 f64 per fit and list entry, kRc entries per
-  // chunk) within 48 GB
-  const size_t state_rows = (size_t)(nch0 + nch1) * kRc;
-  const size_t state_per_rep = 3 * state_rows * S_pad * sizeof(double);
-  const uint64_t want = std::max<uint64_t>(n_reps, 1);
-  const uint32_t rb_cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({want, 256, (48ull << 30) / state_per_rep}));
-  const size_t fits = (size_t)rb_cap * 2 * S_pad;
-  const int nv_max = nv_asm(K);  // >= 5 + 2 K (affine) and nv_cls(K)
   // Row reduction: OB_MM_REDUCE=0 off, =1 on; by default on when both groups have >= 2^16 rows.
   Reduction rd;
   {
     const char* e = getenv("OB_MM_REDUCE");
     rd.on = e && *e ? (e[0] != '0') : (p->n[0] >= 65536u && p->n[1] >= 65536u);
   }
+  const uint32_t rcF = rd.on ? kRcF : kRc;  // the full lists' chunk rows (= their capacity)
+  const uint32_t nch0 = (p->n[0] + rcF - 1) / rcF, nch1 = (p->n[1] + rcF - 1) / rcF;
+  // replicate slots per batch: IPM state (x, z, w: 3 f64 per fit and list entry, rcF entries per
+  // chunk) within 48 GB
+  const size_t state_rows = (size_t)(nch0 + nch1) * rcF;
+  const size_t state_per_rep = 3 * state_rows * S_pad * sizeof(double);
+  const uint64_t want = std::max<uint64_t>(n_reps, 1);
+  const uint32_t rb_cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({want, 256, (48ull << 30) / state_per_rep}));
+  const size_t fits = (size_t)rb_cap * 2 * S_pad;
+  const int nv_max = nv_asm(K);  // >= 5 + 2 K (affine) and nv_cls(K)
   const uint32_t rc1 = kRc1;
   rd.nch1[0] = (p->n[0] + rc1 - 1) / rc1;
   rd.nch1[1] = (p->n[1] + rc1 - 1) / rc1;
   const size_t nfb = (size_t)S_pad / 64;
   const size_t lists_full = (size_t)rb_cap * (nch0 + nch1), lists_blk = rd.on ? lists_full * nfb : 0,
                lists_p1 = rd.on ? (size_t)rb_cap * (rd.nch1[0] + rd.nch1[1]) : 0;
+  const size_t cap1 = kRc1 / kSubStride;
+  const size_t list_words = (lists_full + lists_blk) * rcF + lists_p1 * cap1;
+  const size_t nch_max = std::max<size_t>(nch0 + nch1, rd.on ? rd.nch1[0] + rd.nch1[1] : 0);  // partials
   const size_t n_lists = lists_full + lists_blk + lists_p1;
   if (!p->mm_ws) {
     p->mm_ws = new Buffers();
@@ -1891,13 +1908,13 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   const size_t d8 = sizeof(double), u4 = sizeof(uint32_t);
   const size_t need[Buffers::kSlots] = {d8 * st_elems, d8 * st_elems, d8 * st_elems, d8 * fits * K,
                            d8 * fits * K, d8 * fits * K, d8 * fits * K, d8 * fits * K * K,
-                           d8 * fits * kFs, d8 * (size_t)rb_cap * (nch0 + nch1) * S_pad * nv_max,
+                           d8 * fits * kFs, d8 * (size_t)rb_cap * nch_max * S_pad * nv_max,
                            d8 * fits * nv_max, d8 * n_q, d8 * rb_cap * 3 * n_q, u4 * fits, u4,
                            sizeof(unsigned long long), u4 * rb_cap * 2 * (p->ntiles[0] + 1 + nt1 + 1), u4 * fits,
-                           u4 * n_lists * kRc, u4 * n_lists, rb_cap, d8 * fits * K, d8 * fits * K,
+                           u4 * list_words, u4 * n_lists, rb_cap, d8 * fits * K, d8 * fits * K,
                            d8 * fits * K, u4 * (size_t)rb_cap * 2 * 2 * kBandSamples, u4 * (size_t)rb_cap * 2,
-                           d8 * (size_t)rb_cap * 2 * (K * K + 1), d8 * lists_full * kRc,
-                           u4 * (lists_blk ? lists_blk : 1) * (kRc / 32)};
+                           d8 * (size_t)rb_cap * 2 * (K * K + 1), d8 * lists_full * rcF,
+                           u4 * (lists_blk ? lists_blk : 1) * (rcF / 32)};
   MM_OK(b.reserve(need));
   MM_OK(hipMemcpy(b.quant, quantiles, sizeof(double) * n_q, hipMemcpyHostToDevice));
 
@@ -1932,12 +1949,13 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   a.lane_of = b.lane_of;
   a.rowlist = b.rowlist;
   a.nrows = b.nrows;
-  a.rc = kRc;
+  a.rc = rcF;
   a.stride = 1;
+  a.cap = rcF;
   a.tol = kTol;
-  a.blist = b.rowlist + lists_full * kRc;
+  a.blist = b.rowlist + lists_full * rcF;
   a.bnrows = b.nrows + lists_full;
-  rd.list1 = b.rowlist + (lists_full + lists_blk) * kRc;
+  rd.list1 = b.rowlist + (lists_full + lists_blk) * rcF;
   rd.nrows1 = b.nrows + lists_full + lists_blk;
   rd.gchol = b.gchol;
   a.bvec = b.bvec;
