@@ -59,6 +59,8 @@ constexpr uint32_t kSubStride = 8;   // phase 1 of the row reduction: every 8th 
 constexpr uint32_t kRc1 = 4096;      // ... in chunks of 4096 rows (512 candidates: short walks)
 static_assert(kRc <= kCap && kRcF <= kCap && kRc1 / kSubStride <= kCap, "lists fit the LDS copies");
 constexpr double kPhase1Tol = 1e-6;  // phase-1 relative gap (beta_hat only centres the bands)
+constexpr int kFitStride = 16;       // phase 1 solves every 16th quantile (tau order) and the last ...
+constexpr int kFitStrideMin = 64;    // ... when a group has at least 64 simulations; the rest interpolate
 constexpr double kBandKappa = 4.0;   // band half-width in rank units: kappa sqrt(tau (1 - tau) K / m) + 0.01
                                      // (OB_MM_KAPPA overrides it: a tuning knob; results do not depend on it)
 constexpr int kBandSamples = 4096;   // residuals per fit behind its band quantiles
@@ -981,6 +983,46 @@ __global__ __launch_bounds__(256) void mm_step_kernel(const MmArgs a, int K, siz
 
 // ---- row reduction (phases 2 and 3) ----
 
+// Phase 1 solves S1 quantiles per (slot, group): sorted lanes 0, f, 2f, ... and S - 1 (f = 1: all).
+__host__ __device__ inline int sub_lane(int k, int S, int f) { return min(k * f, S - 1); }
+
+// Phase-1 fit k's tau = the full fit's at sub_lane(k) (thread per phase-1 fit).
+__global__ __launch_bounds__(256) void mm_subtau_kernel(const MmArgs a, const MmArgs a1, int f) {
+  const size_t F1 = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (F1 >= (size_t)a1.n_rb * 2 * a1.S_pad) return;
+  const size_t sg = F1 / a1.S_pad;
+  const int k = (int)(F1 % a1.S_pad);
+  if (k >= a1.S) return;
+  a1.fs[F1 * kFs + FS_TAU] = a.fs[(sg * a.S_pad + sub_lane(k, a.S, f)) * kFs + FS_TAU];
+}
+
+// Every full fit's phase-1 result: linear in tau between the two phase-1 fits around its lane
+// (a copy when f = 1). It only centres the fit's band, so interpolation error moves no result
+// (the fixed rows are verified). Padding fits are retired.
+__global__ __launch_bounds__(256) void mm_interp_kernel(const MmArgs a, const MmArgs a1, int K, int f) {
+  const size_t F = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (F >= (size_t)a.n_rb * 2 * a.S_pad) return;
+  const size_t sg = F / a.S_pad;
+  const int s = (int)(F % a.S_pad);
+  if (s >= a.S) {
+    a.fstat[F] = kDone | kFailed;
+    return;
+  }
+  const int k = a1.S > 1 ? min(s / f, a1.S - 2) : 0;
+  const size_t Fa = sg * a1.S_pad + k, Fb = a1.S > 1 ? Fa + 1 : Fa;
+  const double ta = a1.fs[Fa * kFs + FS_TAU], tb = a1.fs[Fb * kFs + FS_TAU], tau = a.fs[F * kFs + FS_TAU];
+  const double t = (f > 1 && tb > ta) ? fmin(fmax((tau - ta) / (tb - ta), 0.0), 1.0) : 0.0;
+  const bool failed = a1.fstat[Fa] != kDone || (t > 0.0 && a1.fstat[Fb] != kDone);
+  a.fstat[F] = failed ? (kDone | kFailed) : kDone;
+  for (int j = 0; j < K; ++j) {
+    const double ba = a1.beta[Fa * K + j], bb = a1.beta[Fb * K + j];
+    a.beta[F * K + j] = t > 0.0 ? (1.0 - t) * ba + t * bb : ba;
+  }
+  const double da = a1.fs[Fa * kFs + FS_DELTA], db = a1.fs[Fb * kFs + FS_DELTA];
+  a.fs[F * kFs + FS_DELTA] = t > 0.0 ? (1.0 - t) * da + t * db : da;
+  a.fs[F * kFs + FS_NACT] = a1.fs[Fa * kFs + FS_NACT];
+}
+
 // kBandSamples list entries of each (slot, group) at a fixed stride over the full nonzero-row lists:
 // the rows behind every fit's band quantiles (a function of the replicate alone).
 __global__ __launch_bounds__(1024) void mm_sample_kernel(const MmArgs a) {
@@ -1621,6 +1663,8 @@ struct Reduction {  // the row reduction's phase-1 geometry and list regions (mm
   uint32_t nch1[2] = {0, 0};
   uint32_t *list1 = nullptr, *nrows1 = nullptr;
   double* gchol = nullptr;
+  double *beta1 = nullptr, *bprev1 = nullptr, *dba1 = nullptr, *db1 = nullptr, *L1 = nullptr, *fs1 = nullptr;
+  uint32_t* fstat1 = nullptr;  // phase 1's fit arrays (past the full fits' in the same buffers)
 };
 
 hipError_t reduce_partials(const MmArgs& a, int nv, int n_min, int skip_dead, hipStream_t s) {
@@ -1631,7 +1675,9 @@ hipError_t reduce_partials(const MmArgs& a, int nv, int n_min, int skip_dead, hi
 
 // Row lists, the OLS start per (slot, group), the tau order and the shifted start (phase 1, or the
 // whole solve without the reduction); a.active_rows <- the live (fit, row) pairs of the first assemble.
-int start_fits(const MmArgs& a, int K, hipStream_t s) {
+// With the reduction, `full` holds every quantile: the order kernel sorts them there and phase 1 (a)
+// takes every f-th lane's tau (mm_subtau_kernel).
+int start_fits(const MmArgs& a, int K, hipStream_t s, const MmArgs* full = nullptr, int f = 1) {
   const uint32_t nch = a.nch[0] + a.nch[1];
   const size_t lds_solve = sizeof(double) * ((size_t)K * K + K);
   hipLaunchKernelGGL(mm_rows_kernel, dim3(nch, 1, a.n_rb), dim3(256), 0, s, a);
@@ -1642,12 +1688,18 @@ int start_fits(const MmArgs& a, int K, hipStream_t s) {
   MM_OK(reduce_partials(a, nv_asm(K), 0, 0, s));  // the OLS sums sit in fit 0 (the statuses are not set yet)
   hipLaunchKernelGGL(mm_start_kernel, dim3(a.n_rb * 2), dim3(64), lds_solve, s, a, K);
   MM_OK(hipGetLastError());
+  const MmArgs& ao = full ? *full : a;
   int m2 = 1;
-  while (m2 < a.S) m2 <<= 1;
+  while (m2 < ao.S) m2 <<= 1;
   const size_t lds_ord = (size_t)m2 * (sizeof(double) + sizeof(uint32_t));
   MM_OK(hipFuncSetAttribute((const void*)mm_order_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_ord));
-  hipLaunchKernelGGL(mm_order_kernel, dim3(a.n_rb * 2), dim3(256), lds_ord, s, a, m2);
+  hipLaunchKernelGGL(mm_order_kernel, dim3(ao.n_rb * 2), dim3(256), lds_ord, s, ao, m2);
   MM_OK(hipGetLastError());
+  if (full) {
+    hipLaunchKernelGGL(mm_subtau_kernel, dim3((unsigned)(((size_t)a.n_rb * 2 * a.S_pad + 255) / 256)), dim3(256), 0, s,
+                       *full, a, f);
+    MM_OK(hipGetLastError());
+  }
   hipLaunchKernelGGL(mm_shift_kernel, dim3(a.n_rb * 2), dim3(1024), 0, s, a, K);
   MM_OK(hipGetLastError());
   return OB_OK;
@@ -1777,9 +1829,27 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, MmS
     a1.nrows = rd.nrows1;
     a1.tol = kPhase1Tol;
     a1.gchol = rd.gchol;
+    // phase 1 solves S1 of the S quantiles (their own fit arrays); the others interpolate
+    static const int fstride = [] {  // OB_MM_FIT_STRIDE: tuning knob (results do not depend on it)
+      const char* e = getenv("OB_MM_FIT_STRIDE");
+      const int v = e ? atoi(e) : 0;
+      return v > 0 ? v : kFitStride;
+    }();
+    const int f = a.S >= kFitStrideMin ? fstride : 1;
+    a1.S = f > 1 ? (a.S - 1 + f - 1) / f + 1 : a.S;
+    a1.S_pad = (a1.S + 63) / 64 * 64;
+    a1.beta = rd.beta1;
+    a1.bprev = rd.bprev1;
+    a1.dba = rd.dba1;
+    a1.db = rd.db1;
+    a1.L = rd.L1;
+    a1.fs = rd.fs1;
+    a1.fstat = rd.fstat1;
     const auto tb = std::chrono::steady_clock::now();
-    OB_TRY(start_fits(a1, K, s));
+    OB_TRY(start_fits(a1, K, s, &a, f));
     OB_TRY(ipm(a1, K, 1, s, st));
+    hipLaunchKernelGGL(mm_interp_kernel, dim3((unsigned)((n_fits + 255) / 256)), dim3(256), 0, s, a, a1, K, f);
+    MM_OK(hipGetLastError());
     if (trace()) {
       MM_OK(hipStreamSynchronize(s));
       fprintf(stderr, "[mm] phase 1 done at %.1f ms\n",
@@ -1887,6 +1957,7 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   const uint64_t want = std::max<uint64_t>(n_reps, 1);
   const uint32_t rb_cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({want, 256, (48ull << 30) / state_per_rep}));
   const size_t fits = (size_t)rb_cap * 2 * S_pad;
+  const size_t fitsx = 2 * fits;  // fit arrays: the full fits, then phase 1's (at most as many)
   const int nv_max = nv_asm(K);  // >= 5 + 2 K (affine) and nv_cls(K)
   const uint32_t rc1 = kRc1;
   rd.nch1[0] = (p->n[0] + rc1 - 1) / rc1;
@@ -1906,10 +1977,10 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   const size_t st_elems = (size_t)rb_cap * state_rows * S_pad;
   const uint32_t nt1 = (p->n[1] + OB_TILE_ROWS - 1) / OB_TILE_ROWS;
   const size_t d8 = sizeof(double), u4 = sizeof(uint32_t);
-  const size_t need[Buffers::kSlots] = {d8 * st_elems, d8 * st_elems, d8 * st_elems, d8 * fits * K,
-                           d8 * fits * K, d8 * fits * K, d8 * fits * K, d8 * fits * K * K,
-                           d8 * fits * kFs, d8 * (size_t)rb_cap * nch_max * S_pad * nv_max,
-                           d8 * fits * nv_max, d8 * n_q, d8 * rb_cap * 3 * n_q, u4 * fits, u4,
+  const size_t need[Buffers::kSlots] = {d8 * st_elems, d8 * st_elems, d8 * st_elems, d8 * fitsx * K,
+                           d8 * fitsx * K, d8 * fitsx * K, d8 * fitsx * K, d8 * fitsx * K * K,
+                           d8 * fitsx * kFs, d8 * (size_t)rb_cap * nch_max * S_pad * nv_max,
+                           d8 * fits * nv_max, d8 * n_q, d8 * rb_cap * 3 * n_q, u4 * fitsx, u4,
                            sizeof(unsigned long long), u4 * rb_cap * 2 * (p->ntiles[0] + 1 + nt1 + 1), u4 * fits,
                            u4 * list_words, u4 * n_lists, rb_cap, d8 * fits * K, d8 * fits * K,
                            d8 * fits * K, u4 * (size_t)rb_cap * 2 * 2 * kBandSamples, u4 * (size_t)rb_cap * 2,
@@ -1958,6 +2029,13 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   rd.list1 = b.rowlist + (lists_full + lists_blk) * rcF;
   rd.nrows1 = b.nrows + lists_full + lists_blk;
   rd.gchol = b.gchol;
+  rd.beta1 = b.beta + fits * K;
+  rd.bprev1 = b.bprev + fits * K;
+  rd.dba1 = b.dba + fits * K;
+  rd.db1 = b.db + fits * K;
+  rd.L1 = b.L + fits * K * K;
+  rd.fs1 = b.fs + fits * kFs;
+  rd.fstat1 = b.fstat + fits;
   a.bvec = b.bvec;
   a.rpv = b.rpv;
   a.bhat = b.bhat;
