@@ -426,22 +426,43 @@ __device__ __forceinline__ void level2_draws(const GramArgs& a, const Work& w, u
 
 // A row drawn 256+ times wraps its byte and carries into the next one, which lowers the
 // replicate's byte sum below m: comparing sums with the level-1 counts is an exact check.
-// Four threads per replicate (consecutive lanes); threads my in [0, 256). With zero, each thread
-// then clears the 16 words it checked, recycling the image without another barrier.
-__device__ __forceinline__ void check_counts(const GramArgs& a, uint32_t* cnt, const uint32_t* mc, int my,
-                                             bool zero = false, bool i8 = false) {
+// Four threads per replicate (consecutive lanes); thread my in [0, 256) holds replicate my >> 2's
+// 16 words of sub-tile my & 3 in registers, stores them straight to the HBM image (the tile's
+// first ns sub-tiles), then clears them in LDS, recycling the image without another pass.
+// I8: the A-fragment units of ob_gram_i8.hip ([sub-tile][16-replicate block][lane][16 B], lane
+// = replicate 16 m + (l & 15) holding rows 16 (l >> 4) .. + 15), i.e. word group q of the thread
+// is unit sb * 256 + (r >> 4) * 64 + q * 16 + (r & 15). f64: replicate r's 16 words at r * 17 of
+// the sub-tile image, then its zero pad word.
+template <bool I8>
+__device__ __forceinline__ void check_store_counts(const GramArgs& a, uint32_t* cnt, const uint32_t* mc, int my,
+                                                   uint32_t tt, uint32_t rb, uint32_t ns) {
   const int r = my >> 2, part = my & 3;
   uint32_t* row = cnt + r * kCntStride + part * 16;
+  uint32_t v[16];
   uint32_t sum = 0, hib = 0;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    sum = __builtin_amdgcn_sad_u8(row[i], 0u, sum);
-    hib |= row[i] & 0x80808080u;
+    v[i] = row[i];
+    sum = __builtin_amdgcn_sad_u8(v[i], 0u, sum);
+    hib |= v[i] & 0x80808080u;
   }
-  if (i8 && hib && !(a.diag & 96)) atomicOr(a.flags, 2u);  // the i8 Gram reads counts as signed bytes: at most 127
-  if (zero)
+  if (I8 && hib && !(a.diag & 96)) atomicOr(a.flags, 2u);  // the i8 Gram reads counts as signed bytes: at most 127
+  if ((uint32_t)part < ns) {
+    if constexpr (I8) {
+      uint4* out = reinterpret_cast<uint4*>(const_cast<uint32_t*>(a.counts)) + ((size_t)tt * a.nb_rep + rb) * 1024 +
+                   part * 256 + (r >> 4) * 64 + (r & 15);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) row[i] = 0u;
+      for (int q = 0; q < 4; ++q) out[q * 16] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    } else {
+      uint32_t* out = const_cast<uint32_t*>(a.counts) + ((size_t)tt * a.nb_rep + rb) * 4 * kCimgWords +
+                      part * kCimgWords + r * kCimgStride;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) out[i] = v[i];
+      out[16] = 0u;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) row[i] = 0u;
   sum += __shfl_xor(sum, 1);
   sum += __shfl_xor(sum, 2);
   if (part == 0 && sum != mc[r] && !(a.diag & 96)) atomicOr(a.flags, 1u);
@@ -500,7 +521,7 @@ constexpr int kCntTilesPerBlock = 8;
 template <bool I8>
 __global__ __launch_bounds__(kBlock) void ob_count_kernel(const GramArgs a) {
   __shared__ uint32_t img[64 * kCntStride];
-  __shared__ uint32_t mc[64], cum[65];
+  __shared__ uint32_t mcb[2][64], cumb[2][65];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   Work w{};
   w.rb = blockIdx.y;
@@ -509,11 +530,17 @@ __global__ __launch_bounds__(kBlock) void ob_count_kernel(const GramArgs a) {
   const uint32_t tt1 = min(a.tiles_total, tt0 + kCntTilesPerBlock);
   // wave 0 loads tile tt+1's level-1 counts while the block draws tile tt
   uint32_t m_next = (wave == 0 && tt0 < tt1) ? level1_count(a, w.rep0, tt0, lane) : 0u;
+  // the image starts zeroed once; check_store_counts clears what it read (the pad words stay 0)
+  for (int i = tid; i < 64 * kCntStride; i += kBlock) img[i] = 0u;
+  // Two barriers per tile: the call prefix is double-buffered, so publishing tile tt + 1's
+  // (buffer (tt + 1) & 1) never races the checks of tile tt (buffer tt & 1), and the image
+  // clears of tile tt complete before the barrier that follows that publish.
   for (uint32_t tt = tt0; tt < tt1; ++tt) {
+    uint32_t* mc = mcb[tt & 1];
+    uint32_t* cum = cumb[tt & 1];
     w.g = tt >= a.tiles0 ? 1u : 0u;
     w.n = w.g ? a.n1 : a.n0;
     const uint32_t tile = tt - (w.g ? a.tiles0 : 0u);
-    for (int i = tid; i < 64 * kCntStride; i += kBlock) img[i] = 0u;
     if (wave == 0) {
       publish_counts(w, tile, m_next, mc, cum, lane);
       if (tt + 1 < tt1) m_next = level1_count(a, w.rep0, tt + 1, lane);
@@ -521,23 +548,8 @@ __global__ __launch_bounds__(kBlock) void ob_count_kernel(const GramArgs a) {
     __syncthreads();
     level2_draws(a, w, tile, img, mc, cum, 0, 1, wave, 4, lane);
     __syncthreads();
-    check_counts(a, img, mc, tid, false, I8);
     const uint32_t ns = (min(OB_TILE_ROWS, w.n - tile * OB_TILE_ROWS) + 63) >> 6;
-    if constexpr (I8) {
-      uint4* out = reinterpret_cast<uint4*>(const_cast<uint32_t*>(a.counts)) + ((size_t)tt * a.nb_rep + w.rb) * 1024;
-      for (uint32_t u = tid; u < ns * 256; u += kBlock) {
-        const uint32_t ln = u & 63u, mb = (u >> 6) & 3u, sb = u >> 8;
-        const uint32_t* src = img + (mb * 16 + (ln & 15u)) * kCntStride + sb * 16 + 4 * (ln >> 4);
-        out[u] = make_uint4(src[0], src[1], src[2], src[3]);
-      }
-    } else {
-      uint32_t* out = const_cast<uint32_t*>(a.counts) + ((size_t)tt * a.nb_rep + w.rb) * 4 * kCimgWords;
-      for (uint32_t i = tid; i < ns * kCimgWords; i += kBlock) {
-        const uint32_t s = i / kCimgWords, rem = i - s * kCimgWords, r = rem / kCimgStride, wd = rem - r * kCimgStride;
-        out[i] = wd < 16 ? img[r * kCntStride + s * 16 + wd] : 0u;
-      }
-    }
-    __syncthreads();
+    check_store_counts<I8>(a, img, mc, tid, tt, w.rb, ns);
   }
 }
 
