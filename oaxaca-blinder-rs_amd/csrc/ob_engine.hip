@@ -396,7 +396,7 @@ __device__ __forceinline__ void level2_draws(const GramArgs& a, const Work& w, u
       if (a.diag & 64)  // timing ablation (OB_GRAM_DIAG 64): no Philox, wrong draws
         u = ob_u32x4{pp * 0x9E3779B9u ^ r, pp * 0x85EBCA6Bu ^ c2, pp * 0xC2B2AE35u, pp ^ 0x27D4EB2Fu};
       else
-        u = ob_philox(pp, rep0 + r, c2, OB_TAG_L2, a.key0, a.key1);
+        u = ob_philox_x3(pp, rep0 + r, c2, OB_TAG_L2, a.key0, a.key1);
       uint32_t* row = cnt + r * kCntStride;
       if (full && (a.diag & 32)) {  // timing ablation (OB_GRAM_DIAG 32): no LDS atomics
         if ((u.x ^ u.y ^ u.z ^ u.w) == 0x5EED5EEDu) row[0] = 1u;
@@ -414,7 +414,7 @@ __device__ __forceinline__ void level2_draws(const GramArgs& a, const Work& w, u
     const int r = r_lo + lane;
     const uint32_t m = mc[r], nd = m & 15u;
     if (nd) {
-      const ob_u32x4 u = ob_philox(m >> 4, rep0 + r, c2, OB_TAG_L2, a.key0, a.key1);
+      const ob_u32x4 u = ob_philox_x3(m >> 4, rep0 + r, c2, OB_TAG_L2, a.key0, a.key1);
       const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
       uint32_t* row = cnt + r * kCntStride;
 #pragma unroll

@@ -59,6 +59,36 @@ OB_HD ob_u32x4 ob_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uin
   return o;
 }
 
+// The same function with each three-way xor as one v_bitop3_b32 (truth table 0x96) on gfx950,
+// where the compiler otherwise emits two v_xor_b32 per output word. The level-2 count kernel
+// draws with it (4.78 -> 4.48 ms at configs[1]); level 1 measured slower with it (3.38 -> 3.49 ms,
+// its unrolling changes), so it keeps ob_philox. Identical outputs by construction.
+OB_HD uint32_t ob_xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
+
+OB_HD ob_u32x4 ob_philox_x3(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t n0 = ob_xor3((uint32_t)(p1 >> 32), c1, k0);
+    const uint32_t n2 = ob_xor3((uint32_t)(p0 >> 32), c3, k1);
+    c1 = (uint32_t)p1;
+    c3 = (uint32_t)p0;
+    c0 = n0;
+    c2 = n2;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  ob_u32x4 o = {c0, c1, c2, c3};
+  return o;
+}
+
 // Fair bits [128 q, min(c, 128 q + 128)) of a level-1 node stream, counted: bit b of the stream
 // is bit (b & 31) of word ((b >> 5) & 3) of Philox({b >> 7, rep, c2, tag}).
 OB_HD uint32_t ob_l1_split_bits(uint32_t q, uint32_t c, uint32_t rep, uint32_t c2, uint32_t tag, uint32_t k0,
