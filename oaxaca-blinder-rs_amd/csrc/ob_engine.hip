@@ -363,6 +363,53 @@ __device__ __forceinline__ void add_draw(uint32_t* row, uint32_t lr) {
   atomicAdd(&row[lr >> 2], 1u << ((lr & 3u) * 8u));
 }
 
+// The four draws of one Philox word (byte b = a row of the tile): with a = w & 0xFCFCFCFC (byte b
+// = the row's word offset in bytes) and m = (w << 3) & 0x18181818 (byte b = its byte lane x 8), a
+// draw is one SDWA add (row offset + byte b of a) and one SDWA shift (1 << byte b of m) on gfx950,
+// where the compiler emits a shift-and-mask chain for each (5 VALU per draw -> 2 + 3/4). The
+// shifts read only byte b of their operand, so no mask per draw is needed.
+template <int B>
+__device__ __forceinline__ uint32_t sdwa_add_byte(uint32_t base, uint32_t a) {
+  uint32_t r;
+  if constexpr (B == 0)
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(base), "v"(a));
+  else if constexpr (B == 1)
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(base), "v"(a));
+  else if constexpr (B == 2)
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(base), "v"(a));
+  else
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(base), "v"(a));
+  return r;
+}
+
+template <int B>
+__device__ __forceinline__ uint32_t sdwa_shl_byte(uint32_t m, uint32_t one) {
+  uint32_t r;
+  if constexpr (B == 0)
+    asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:DWORD" : "=v"(r) : "v"(m), "v"(one));
+  else if constexpr (B == 1)
+    asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD" : "=v"(r) : "v"(m), "v"(one));
+  else if constexpr (B == 2)
+    asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_2 src1_sel:DWORD" : "=v"(r) : "v"(m), "v"(one));
+  else
+    asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_3 src1_sel:DWORD" : "=v"(r) : "v"(m), "v"(one));
+  return r;
+}
+
+template <int B>
+__device__ __forceinline__ void add_draw_byte(uint32_t* img, uint32_t row_off, uint32_t a, uint32_t m, uint32_t one) {
+  atomicAdd(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(img) + sdwa_add_byte<B>(row_off, a)),
+            sdwa_shl_byte<B>(m, one));
+}
+
+__device__ __forceinline__ void add_draws_word(uint32_t* img, uint32_t row_off, uint32_t w, uint32_t one) {
+  const uint32_t a = w & 0xFCFCFCFCu, m = (w << 3) & 0x18181818u;
+  add_draw_byte<0>(img, row_off, a, m, one);
+  add_draw_byte<1>(img, row_off, a, m, one);
+  add_draw_byte<2>(img, row_off, a, m, one);
+  add_draw_byte<3>(img, row_off, a, m, one);
+}
+
 __device__ __forceinline__ void level2_draws(const GramArgs& a, const Work& w, uint32_t tile, uint32_t* cnt,
                                              const uint32_t* mc, const uint32_t* cum, int k, int nparts, int wv,
                                              int nw, int lane) {
@@ -376,6 +423,7 @@ __device__ __forceinline__ void level2_draws(const GramArgs& a, const Work& w, u
   const uint32_t bnd = lane < nr ? cum[r_lo + 1 + lane] : 0xFFFFFFFFu;  // end of replicate r_lo + lane
   const uint32_t c2 = (tile << 1) | w.g;
   const uint32_t rep0 = a.first_rep + w.rep0;
+  const uint32_t one = 1u;  // the SDWA shifts' operand (a VGPR)
   int rr = r_lo;  // uniform: replicate of the window's first call
   for (uint32_t f0 = f_lo; f0 < f_hi; f0 += 64) {
     while (rr < r_hi - 1 && (uint32_t)__builtin_amdgcn_readlane(bnd, rr - r_lo) <= f0) ++rr;
@@ -403,7 +451,7 @@ __device__ __forceinline__ void level2_draws(const GramArgs& a, const Work& w, u
       } else if (full) {
         const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
-        for (int d = 0; d < 16; ++d) add_draw(row, (wd[d >> 2] >> (8 * (d & 3))) & 0xFFu);
+        for (int i = 0; i < 4; ++i) add_draws_word(cnt, (uint32_t)r * (kCntStride * 4), wd[i], one);
       } else {
         add_draw(row, ob_mulhi64(u.x, u.y, S));
         if (2 * pp + 1 < mc[r]) add_draw(row, ob_mulhi64(u.z, u.w, S));
