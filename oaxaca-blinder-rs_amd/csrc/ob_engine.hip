@@ -561,7 +561,10 @@ __device__ __forceinline__ void store_partials(const GramArgs& a, const Work& w,
 // Gram kernel fetches a sub-tile with a plain LDS-DMA copy. Counts are drawn once per replicate
 // batch, whatever the number of column groups.
 // ---------------------------------------------------------------------------------------------
-constexpr int kCntTilesPerBlock = 8;
+#ifndef OB_CNT_TILES
+#define OB_CNT_TILES 8  // tiles per count block (A/B builds: tools/build_alt.sh ... -DOB_CNT_TILES=n)
+#endif
+constexpr int kCntTilesPerBlock = OB_CNT_TILES;
 
 // I8: the image is written in the A-fragment order of ob_gram_i8.hip instead (v_mfma_i32_16x16x64_i8):
 // per (tile, batch) [sub-tile][16-replicate block m][lane][16 B], lane l = replicate 16 m + (l & 15),
