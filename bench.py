@@ -73,13 +73,17 @@ def stdout_to_stderr():
 
 
 def host_cores():
-    """Threads the CPU baselines use: the box's CPU share (OMP_NUM_THREADS, which the GPU box sets
-    to its per-GPU share), else every core this process may run on."""
-    env = os.environ.get("OMP_NUM_THREADS")
+    """Threads the CPU baselines use: every core this process may run on, as the reference's Rayon
+    global pool does (builder.rs:816-817)."""
+    return len(os.sched_getaffinity(0))
+
+
+def omp_share():
+    """The box's per-GPU CPU share (OMP_NUM_THREADS as the GPU box sets it), reported beside."""
     try:
-        return max(1, int(env)) if env else len(os.sched_getaffinity(0))
+        return int(os.environ.get("OMP_NUM_THREADS", "0")) or None
     except ValueError:
-        return len(os.sched_getaffinity(0))
+        return None
 
 
 def cpu_model():
@@ -94,7 +98,8 @@ def cpu_model():
 
 
 def host_info(threads):
-    return {"cores": threads, "cpu_model": cpu_model(), "host_cpus_visible": len(os.sched_getaffinity(0))}
+    return {"cores": threads, "cpu_model": cpu_model(), "host_cpus_visible": len(os.sched_getaffinity(0)),
+            "omp_num_threads_share": omp_share()}
 
 
 def cpu_baseline(d, preds, weighted, ref, target_s, threads):
@@ -377,6 +382,36 @@ def load_traffic(rows, preds, reps, gram_path=1):
     return None
 
 
+def end_to_end(ob, ctx, d, ya, yb, n, ref, stat_cols, dev):
+    """One configs[1] run() from a fresh panel, as the reference's published figures are whole runs
+    (README.md:316-317): host -> HBM upload and the Gram panel (ob_panel_create), the digit images
+    and exception rows (prep, first boot of the panel), n replicates, and the aggregation of every
+    reported component on the host. Host clock around all of it; prep_ms by HIP events."""
+    import torch
+
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    panel = ob.Panel(d["xa"], ya, d["xb"], yb, d["wa"], d["wb"], ctx=ctx)
+    t_create = time.perf_counter() - t0
+    panel.set_gather_columns(list(range(len(stat_cols))))
+    rows = torch.empty((n, panel.row_len), dtype=torch.float64, device=dev)
+    ok = torch.empty(n, dtype=torch.uint8, device=dev)
+    panel.boot_sharded_device(0x0B5EED, 0, n, rows.data_ptr(), ok.data_ptr(), ref,
+                              stream=torch.cuda.current_stream(dev).cuda_stream)
+    panel.sync()
+    tm = panel.timing()
+    hr = rows[:, : len(stat_cols)].cpu().numpy()
+    ob.aggregate(np.ascontiguousarray(hr), ok.cpu().numpy(), stat_cols)
+    total_s = time.perf_counter() - t0
+    panel.close()
+    return {"replicates": n, "ms": total_s * 1e3, "replicates_per_s": n / total_s,
+            "panel_create_ms": t_create * 1e3, "prep_ms": tm["prep_ms"],
+            "boot_ms": tm["level1_ms"] + tm["counts_ms"] + tm["gram_ms"] + tm["reduce_ms"] + tm["solve_ms"],
+            "oz_exceptions": tm["oz_exceptions"], "oz_bits": tm["oz_bits"],
+            "what": "fresh ob_panel_create (H2D + Gram panel) + digit images/exception rows + one boot of n "
+                    "replicates + host aggregation, host clock"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -391,7 +426,8 @@ def main():
     ap.add_argument("--ref", type=int, default=0, help="ReferenceCoefficients (0 = GroupA)")
     ap.add_argument("--unweighted", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="0 disables the CPU baseline leg")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0: the box's CPU share (host_cores())")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every core this process may use (host_cores())")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end configs[1] run from a fresh panel")
     ap.add_argument("--taus", type=str, default="",
                     help="configs[3]: comma-separated RIF quantiles sharing one bootstrap (e.g. 0.1,0.5,0.9); "
                          "reports replicate-quantiles/s instead of the headline metric")
@@ -458,6 +494,7 @@ def main():
     kd = panel.k + panel.n_base
     ns = 6 + 2 * kd  # every reported component (+ total_gap): the only columns the aggregation reads
     stat_cols = np.arange(ns, dtype=np.int32)
+    panel.set_gather_columns(list(range(ns)))  # the RCCL all-gather moves only these 48 of 153 f64 (K = 21)
     seed = 0x0B5EED
     # Two row buffers: step i's replicates run on the GPU while rank 0 aggregates step i - 1's on
     # the host (builder.rs:841-930 after the loop of :816-839); the component columns come back
@@ -528,6 +565,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, gram_launch_ms = float(t[0]), float(t[1])
 
+    e2e = None
+    if not args.no_e2e and not taus and world == 1:
+        e2e = end_to_end(ob, ctx, d, ya, yb, total, args.ref, stat_cols, dev)
+
     if rank == 0:
         value = total * args.steps / elapsed
         k = args.preds + 1
@@ -548,7 +589,7 @@ def main():
                     "avg_launch_ms": gram_launch_ms, "i8_ops_per_replicate": ops_rep,
                     "i8_ops_issued_per_replicate": ops_issued,
                     "f64_equivalent_tflops": achieved, "f64_flops_per_replicate": flops_rep,
-                    "f64_equivalent_frac_of_f64_mfma_peak": achieved / F64_MFMA_PEAK_TFLOPS}
+                    "f64_equivalent_x_of_f64_mfma_peak": achieved / F64_MFMA_PEAK_TFLOPS}
         else:
             roof = {"bound": "mfma", "achieved": achieved, "peak": F64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": achieved / F64_MFMA_PEAK_TFLOPS, "traffic": traffic,
@@ -577,10 +618,13 @@ def main():
                        "parallelism": f"replicates sharded x{world}, engine RCCL all-gather (ob_boot_run_sharded_device)"},
             "roofline": roof,
             "gram_path": "i8 MFMA (v_mfma_i32_16x16x64_i8), exact 7 x 8-bit digit slices (f64-equivalent)" if gram_path == 2 else "f64 MFMA",
+            # what a per-replicate row gather would have to stream: a rate, not a
+            # roofline fraction -- the Gram reads each panel byte once per 256-replicate tile instead
             "gather_equivalent": {"algorithmic_bytes_per_replicate": bytes_rep,
                                   "GBps": bytes_rep * value / world / 1e9,
-                                  "frac_of_hbm_peak": bytes_rep * value / world / 1e9 / HBM_PEAK_GBPS},
+                                  "x_of_hbm_peak": bytes_rep * value / world / 1e9 / HBM_PEAK_GBPS},
             "breakdown_ms_per_step_rank0": {k_: v / args.steps for k_, v in sums.items()},
+            "end_to_end": e2e,
         }
         if world == 1 and args.cpu_seconds > 0 and not taus:
             out["cpu_baseline"] = cpu_baseline(d, args.preds, weighted, args.ref, args.cpu_seconds, args.cpu_threads)

@@ -166,6 +166,11 @@ typedef struct {
   double heck_sums_ms;       /* Heckman panels: ob_heck_sums_kernel (IMR sums) time */
   int32_t mm_reduced;        /* ob_mm_run: 1 if the row reduction ran (subsample, bands, reduced LPs) */
   int64_t mm_retried;        /* ob_mm_run: fits the reduction solved again on all rows (phase 3) */
+  double prep_ms;            /* i8 Gram: building the panel's digit images + exception rows (HIP events;
+                                nonzero only on the boot run that built them, the first of a panel) */
+  int32_t oz_exceptions;     /* i8 Gram: exception rows, summed in f64 beside the integer Gram */
+  int32_t oz_bits;           /* i8 Gram: a row is an exception when some |v_c| >= 2^oz_bits x its chunk's
+                                scale for column c (geometric mean over nonzero rows), or not finite */
 } ob_timing;
 int ob_panel_last_timing(const ob_panel* panel, ob_timing* out);
 /* Synchronize the stream used by the last *_device call and collect its timings. */
@@ -206,6 +211,19 @@ int ob_boot_run_sharded_device(ob_panel* panel, uint64_t seed, uint64_t first_re
 int ob_boot_run_multi(ob_panel* const* panels, int n_panels, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
                       int ref_mode, double* rows, uint8_t* ok);
 
+/* The row columns the sharded entry points move over RCCL (ascending offsets into a row; n = 0 or
+   every column: whole rows, the default). Aggregation reads only the component columns (two-fold,
+   three-fold, total gap, detailed: [0, 6 + 2 Kd), plus the selection terms of a Heckman row), so a
+   caller that only aggregates gathers those: 48 of 153 f64 per replicate at K = 21. Delivered rows
+   then hold the other columns for this rank's own replicates only (NaN for the other ranks'). */
+int ob_panel_set_gather_columns(ob_panel* panel, const int32_t* cols, int32_t n);
+/* Test hook: a sharded run of `world` ranks simulated on this panel's one GPU -- each rank's shard
+   computed and packed in turn and copied to where ncclAllGather would place it -- then delivered to
+   host rows/ok as rank self_rank would receive them (the layout arithmetic of ob_shard_layout.h and
+   the pack / unpack kernels of the real path, without the collective). */
+int ob_debug_shard_sim(ob_panel* panel, int world, int self_rank, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
+                       int ref_mode, double* rows, uint8_t* ok);
+
 /* ---- test hook: the OBRS-1 resample counts themselves (bitwise parity, builder.rs:822-827) ----
  * For replicates [first_rep, first_rep + n_reps) of `group` (0 = A, 1 = B): level1 receives
  * n_reps x ceil(n_g / 256) tile counts and row_counts n_reps x n_g per-row draw counts, exactly
@@ -216,6 +234,10 @@ int ob_debug_counts(ob_panel* panel, uint64_t seed, uint64_t first_rep, uint32_t
    e_pad per group) of replicates [first_rep, first_rep + n_reps <= 16384), gram: n_reps x 2 x e_pad,
    computed by path 1 (f64 MFMA) or 2 (exact integer-sliced i8 MFMA); 0 = the default choice. */
 int ob_debug_gram(ob_panel* panel, int path, uint64_t seed, uint64_t first_rep, uint32_t n_reps, double* gram);
+/* Test hook: the i8 Gram's exception rows once the panel's digit images exist:
+   *bits = the threshold B, *n_exc = the number of exception rows, rows[0 .. min(cap, n_exc)) =
+   (group << 31 | row) ascending. */
+int ob_debug_gram_exceptions(ob_panel* panel, int32_t* bits, int32_t* n_exc, uint32_t* rows, int32_t cap);
 
 /* ---- inference (host) --------------------------------------------------------------------- */
 /* inference.rs:4-34: out = {std_err, p_value, ci_lower, ci_upper}; n = 0 gives NaNs. */
@@ -285,7 +307,9 @@ uint64_t ob_prepared_seed(const ob_prepared* prep);
 ob_panel* ob_prepared_panel(ob_prepared* prep);
 int ob_prepared_boot(ob_prepared* prep, uint64_t first_rep, uint64_t n_reps, double* rows, uint8_t* ok);
 /* ob_boot_run_sharded over the prepared panel (its seed and reference coefficients): with a rank
-   context (ob_ctx_create_rank) each rank runs its shard and every rank receives all rows. */
+   context (ob_ctx_create_rank) each rank runs its shard and every rank receives all rows. Only the
+   columns ob_prepared_finish aggregates travel (ob_panel_set_gather_columns): the coefficient and
+   mean columns of the other ranks' replicates arrive as NaN. */
 int ob_prepared_boot_sharded(ob_prepared* prep, uint64_t first_rep, uint64_t n_reps, double* rows, uint8_t* ok);
 int ob_prepared_boot_device(ob_prepared* prep, uint64_t first_rep, uint64_t n_reps, double* d_rows,
                             uint8_t* d_ok, void* hip_stream);
@@ -358,6 +382,13 @@ void ob_matrices_free(ob_matrices* m);
 int ob_mm_run(ob_panel* panel, uint64_t seed, int32_t simulations, const double* quantiles,
               int32_t n_quantiles, uint64_t first_rep, uint64_t n_reps, int32_t with_point, double* rows,
               uint8_t* ok);
+/* Test hook: make chosen quantile-regression fits count as failed, as Clarabel's non-Solved statuses
+   do in the reference (quantile_regression.rs:120-128), to pin the pass's failure semantics
+   (quantile_decomposition.rs:221-259): each group drops its failed fits independently, the
+   survivors pair by index, and a pass with fewer than simulations / 2 successes in a group fails.
+   mask: 2 x sims bytes [group][simulation]; fit (g, s) of pass rep fails when bit (rep & 7) of
+   mask[g * sims + s] is set (the point pass has rep = 2^32 - 1, bit 7). sims = 0 clears it. */
+int ob_debug_mm_fail(ob_panel* panel, const uint8_t* mask, int32_t sims);
 
 typedef struct {
   const char* outcome;

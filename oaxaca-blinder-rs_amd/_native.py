@@ -23,7 +23,7 @@ OB_TABLE_TWO_FOLD, OB_TABLE_DETAILED_EXPLAINED, OB_TABLE_DETAILED_UNEXPLAINED = 
 OB_TABLE_DETAILED_SELECTION, OB_TABLE_THREE_FOLD = 3, 4
 OB_VEC_RESIDUALS, OB_VEC_XA_MEAN, OB_VEC_XB_MEAN, OB_VEC_BETA_STAR = 0, 1, 2, 3
 
-# Every exported entry point of include/oaxaca_boot.h (tests/test_capi_exports.py checks both ways).
+# Every exported entry point of include/oaxaca_boot.h (tests/test_capi_host.py checks both ways).
 EXPORTED = (
     "ob_last_error", "ob_version", "ob_device_count", "ob_ctx_create", "ob_ctx_destroy",
     "ob_panel_create", "ob_panel_destroy", "ob_panel_row_len", "ob_panel_k", "ob_panel_n_base", "ob_panel_n_y",
@@ -40,6 +40,7 @@ EXPORTED = (
     "ob_qd_results_n_failed", "ob_qd_results_free",
     "ob_get_unique_id", "ob_ctx_create_rank", "ob_ctx_rank", "ob_boot_run_sharded", "ob_boot_run_sharded_device",
     "ob_boot_run_multi", "ob_debug_counts", "ob_prepared_boot_sharded", "ob_debug_gram",
+    "ob_debug_gram_exceptions", "ob_panel_set_gather_columns", "ob_debug_shard_sim", "ob_debug_mm_fail",
 )
 
 
@@ -75,7 +76,8 @@ class ob_timing(C.Structure):
                 ("mm_assemble_ms", C.c_double), ("mm_fit_rows", C.c_double), ("mm_iterations", C.c_int32),
                 ("mm_ms", C.c_double), ("gather_ms", C.c_double), ("gram_path", C.c_int32),
                 ("probit_ms", C.c_double), ("probit_launches", C.c_int32), ("heck_sums_ms", C.c_double),
-                ("mm_reduced", C.c_int32), ("mm_retried", C.c_int64)]
+                ("mm_reduced", C.c_int32), ("mm_retried", C.c_int64), ("prep_ms", C.c_double),
+                ("oz_exceptions", C.c_int32), ("oz_bits", C.c_int32)]
 
 
 class ob_unique_id(C.Structure):
@@ -185,6 +187,11 @@ _SIGS = {
     "ob_boot_run_sharded_device": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, _P, _P, _P]),
     "ob_boot_run_multi": (C.c_int, [C.POINTER(_P), C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, _D, _U8]),
     "ob_debug_gram": (C.c_int, [_P, C.c_int, C.c_uint64, C.c_uint64, C.c_uint32, _D]),
+    "ob_debug_mm_fail": (C.c_int, [_P, _U8, C.c_int32]),
+    "ob_panel_set_gather_columns": (C.c_int, [_P, C.POINTER(C.c_int32), C.c_int32]),
+    "ob_debug_shard_sim": (C.c_int, [_P, C.c_int, C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, C.c_int, _D, _U8]),
+    "ob_debug_gram_exceptions": (C.c_int, [_P, C.POINTER(C.c_int32), C.POINTER(C.c_int32),
+                                           C.POINTER(C.c_uint32), C.c_int32]),
     "ob_prepared_boot_sharded": (C.c_int, [_P, C.c_uint64, C.c_uint64, _D, _U8]),
     "ob_debug_counts": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_int, C.POINTER(C.c_uint32), _U8]),
 }

@@ -862,6 +862,13 @@ int ob_prepared_boot(ob_prepared* p, uint64_t first_rep, uint64_t n_reps, double
 
 int ob_prepared_boot_sharded(ob_prepared* p, uint64_t first_rep, uint64_t n_reps, double* rows, uint8_t* ok) {
   if (!p) return ob::fail(OB_E_INVALID, "null pointer");
+  // the RCCL all-gather moves only the columns finish() aggregates: two-fold, three-fold, total
+  // gap, detailed [0, 6 + 2 Kd) and a Heckman row's selection terms after its 5K' tail
+  const int kd = p->k + p->n_base, sel0 = 6 + 2 * kd + 5 * p->k;
+  std::vector<int32_t> cols;
+  for (int c = 0; c < 6 + 2 * kd; ++c) cols.push_back(c);
+  for (size_t i = 0; i < p->selection_names.size(); ++i) cols.push_back(sel0 + (int)i);
+  OB_TRY(ob_panel_set_gather_columns(p->panel, cols.data(), (int32_t)cols.size()));
   return ob_boot_run_sharded(p->panel, p->seed, first_rep, n_reps, p->ref, rows, ok);
 }
 

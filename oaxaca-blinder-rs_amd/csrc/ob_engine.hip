@@ -1379,7 +1379,14 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   OB_TRY(ensure_buf(&p->d_counts, p->cap_counts, (size_t)tiles * pl.nb_rep * 4 * kCimgWords));
   OB_TRY(ensure_buf(&p->d_partial, p->cap_partial, need_partial * p->e_pad));
   OB_TRY(ensure_buf(&p->d_gram, p->cap_gram, (size_t)2 * pl.rep_pad * p->e_pad));
-  OB_TRY(ensure_buf(&p->d_chunks, p->cap_chunks, std::max(pl.chunks.size(), pl_tail.chunks.size())));
+  if (!p->chunks_ready) {  // the chunk table depends on the panel only: uploaded once, never rewritten
+    p->chunks = pl.chunks;
+    OB_TRY(ensure_buf(&p->d_chunks, p->cap_chunks, p->chunks.size()));
+    HIP_OK(hipMemcpyAsync(p->d_chunks, p->chunks.data(), sizeof(uint32_t) * p->chunks.size(), hipMemcpyHostToDevice, s));
+    p->chunks_ready = true;
+  }
+  if (pl.chunks != p->chunks || pl_tail.chunks != p->chunks)
+    return ob::fail(OB_E_INVALID, "internal: the chunk table changed with the replicate count");
   if (p->heckman) OB_TRY(ensure_heck(p, pl));
   // Gram path: the exact integer-sliced i8 GEMM (ob_gram_i8.hip) unless forced to f64 MFMA
   // (OB_GRAM_PATH=f64) or the digit images do not fit. Heckman's kernels read either image layout.
@@ -1389,20 +1396,18 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     force = ev && !strcmp(ev, "f64") ? 1 : (ev && !strcmp(ev, "i8") ? 2 : 0);
   }
   bool use_i8 = force != 1;
+  std::memset(&p->timing, 0, sizeof(p->timing));
   if (use_i8) {
-    OB_TRY(ob::oz_prepare(p, pl.chunks));
+    OB_TRY(ob::oz_prepare(p, s));
     use_i8 = p->oz_state == 1;
     if (!use_i8 && force == 2) return ob::fail(OB_E_UNSUPPORTED, "the i8 Gram's digit images do not fit in HBM");
   }
-  HIP_OK(hipMemcpyAsync(p->d_chunks, pl.chunks.data(), sizeof(uint32_t) * pl.chunks.size(), hipMemcpyHostToDevice, s));
-  HIP_OK(hipStreamSynchronize(s));  // the host vector dies with this call
   HIP_OK(hipMemsetAsync(p->d_flags, 0, sizeof(uint32_t), s));
 
   const size_t lds_l1 = sizeof(uint32_t) * std::max(l1_lds_words(p->ntiles[0]), l1_lds_words(p->ntiles[1]));
   HIP_OK(hipFuncSetAttribute((const void*)ob_level1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_l1));
   HIP_OK(hipFuncSetAttribute((const void*)ob_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)solve_lds_bytes(p)));
-  std::memset(&p->timing, 0, sizeof(p->timing));
   p->timing.chunks = nch;
   p->timing.blocks = use_i8 ? (int32_t)((uint32_t)nch * ((pl.nb_rep + 3) / 4) * (uint32_t)p->oz_n_ct)
                             : (int32_t)(pl.nb_rep * pl.n_cg * (uint32_t)nch);
@@ -1418,12 +1423,6 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   for (uint64_t s0 = 0; s0 < n_reps; s0 += seg) {
     const uint32_t ns = (uint32_t)std::min<uint64_t>(seg, n_reps - s0);
     const Plan& plx = (ns == seg) ? pl : pl_tail;
-    if (plx.chunks != pl.chunks) {
-      HIP_OK(hipStreamSynchronize(s));
-      HIP_OK(hipMemcpyAsync(p->d_chunks, plx.chunks.data(), sizeof(uint32_t) * plx.chunks.size(),
-                            hipMemcpyHostToDevice, s));
-      HIP_OK(hipStreamSynchronize(s));
-    }
     const int nchx = plx.n_chunks();
     const uint32_t frep = (uint32_t)(first_rep + s0);
     hipEvent_t* ev = p->seg_events.data() + kSegEvents * (size_t)p->pending_segments;
@@ -1461,6 +1460,7 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
                        (const double*)p->d_partial, (const uint32_t*)p->d_chunks, nchx, plx.rep_pad, p->e_pad, ns,
                        p->d_gram);
     HIP_OK(hipGetLastError());
+    if (use_i8) OB_TRY(ob::oz_exceptions(p, p->d_counts, plx.nb_rep, ns, p->d_gram, s));
     if (timed) HIP_OK(hipEventRecord(ev[4], s));
     if (p->heckman) {  // probit iterations + IMR sums + two-step solve (synchronizes the stream)
       ob_heck_seg hs = heck_seg(p, plx, p->d_chunks, p->d_gram, ref_mode);
@@ -1524,6 +1524,7 @@ int engine_collect(ob_panel* p) {
     p->timing.gather_ms = t;
     p->gather_timed = false;
   }
+  if (p->timing.gram_path == 2) OB_TRY(ob::oz_collect(p));
   uint32_t flag = 0;
   HIP_OK(hipMemcpy(&flag, p->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost));
   if (flag & 1u) return ob::fail(OB_E_OVERFLOW, "a resampled row was drawn more than 255 times in one replicate");
@@ -1748,15 +1749,9 @@ void ob_panel_destroy(ob_panel* p) {
   (void)hipFree(p->d_hactive);
   (void)hipFree(p->d_rows_tmp);
   (void)hipFree(p->d_ok_tmp);
-  (void)hipFree(p->d_shard_rows);
-  (void)hipFree(p->d_shard_ok);
-  (void)hipFree(p->d_gather_rows);
-  (void)hipFree(p->d_gather_ok);
-  for (hipEvent_t e : p->gather_ev)
-    if (e) (void)hipEventDestroy(e);
-  (void)hipFree(p->d_oz_b[0]);
-  (void)hipFree(p->d_oz_b[1]);
-  (void)hipFree(p->d_oz_pexp);
+  ob::shard_free(p);
+  ob::oz_free(p);
+  (void)hipFree(p->d_mm_fail);
   for (hipEvent_t e : p->seg_events) (void)hipEventDestroy(e);
   if (p->mm_ws_free) p->mm_ws_free(p->mm_ws);
   delete p;

@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "ob_common.hpp"
+#include "ob_shard_layout.h"
 
 // Level-2 count images in HBM (ob_count_kernel): [tile (A then B)][replicate batch][sub-tile]
 // [kCimgWords]; replicate r's counts for the sub-tile's 64 rows are the 16 words at r * 17 (+1 pad
@@ -71,12 +72,24 @@ struct ob_panel {
   size_t cap_m1 = 0, cap_partial = 0, cap_gram = 0, cap_chunks = 0, cap_counts = 0;
   void* mm_ws = nullptr;  // Machado-Mata workspace (ob_mm.hip), freed by mm_ws_free
   void (*mm_ws_free)(void*) = nullptr;
-  // sharded runs (ob_shard.cpp): this rank's rows, the all-gathered rows, the gather's events
+  uint8_t* d_mm_fail = nullptr;  // ob_debug_mm_fail: forced fit failures [2][mm_fail_sims]
+  int mm_fail_sims = 0;
+  // sharded runs (ob_shard.cpp, buffer layouts in ob_shard_layout.h): this rank's rows, the packed
+  // send block, the all-gathered block, host-delivery staging, the gathered columns, the events
   double* d_shard_rows = nullptr;
   uint8_t* d_shard_ok = nullptr;
+  double* d_send = nullptr;
+  uint8_t* d_send_ok = nullptr;
   double* d_gather_rows = nullptr;
   uint8_t* d_gather_ok = nullptr;
-  size_t cap_shard = 0, cap_gather = 0, cap_shard_ok = 0, cap_gather_ok = 0;
+  double* d_deliver_rows = nullptr;
+  uint8_t* d_deliver_ok = nullptr;
+  double* d_own_rows = nullptr;  // ob_debug_shard_sim: the simulated rank's own shard rows
+  size_t cap_shard = 0, cap_gather = 0, cap_shard_ok = 0, cap_gather_ok = 0, cap_send = 0, cap_send_ok = 0;
+  size_t cap_deliver = 0, cap_deliver_ok = 0, cap_own = 0;
+  std::vector<int32_t> gather_cols;   // gathered row columns, ascending (empty: every column)
+  int32_t* d_gather_map = nullptr;    // [row_len] slot of each column or -1, then [nc] the columns
+  bool gather_map_ready = false;
   hipEvent_t gather_ev[2] = {nullptr, nullptr};
   bool gather_timed = false;
   // integer-sliced Gram (ob_gram_i8.hip): digit images per group, pair exponents per chunk
@@ -85,6 +98,23 @@ struct ob_panel {
   int oz_n_ct = 0;
   void* d_oz_b[2] = {nullptr, nullptr};
   int32_t* d_oz_pexp = nullptr;
+  // exception rows (ob_gram_i8.hip): rows whose magnitude dwarfs their chunk's
+  // typical one (or that are not finite) are left out of the digit images and summed in f64
+  int8_t* d_oz_dev[2] = {nullptr, nullptr};  // per row: max over columns of (exponent - chunk scale)
+  int32_t* d_oz_tile_chunk[2] = {nullptr, nullptr};
+  int64_t* d_oz_acc = nullptr;   // [chunk][k1][2]: exponent sums and nonzero counts
+  int32_t* d_oz_meta = nullptr;  // oz_meta layout (ob_gram_i8.hip)
+  uint32_t* d_oz_exc = nullptr;  // [kOzExcCap] (g << 31 | row), sorted
+  double* d_oz_excp = nullptr;   // [kOzExcCap][e_pad] their f64 pair products
+  std::vector<int32_t> oz_tile_chunk[2];  // host copies (the async uploads read them)
+  hipEvent_t oz_ev[2] = {nullptr, nullptr};
+  bool oz_timed = false;  // the last boot run built the digit images (timing.prep_ms)
+  int oz_nexc = -1;       // exception rows (-1: not read back yet), their threshold bits
+  int oz_bits = 0;
+  bool oz_overflow = false;
+  // the panel's chunk table (a function of the panel only), uploaded once into d_chunks
+  std::vector<uint32_t> chunks;
+  bool chunks_ready = false;
   std::vector<hipEvent_t> seg_events;  // 6 per segment of the last boot run
   ob_timing timing = {};
   bool timing_pending = false;
@@ -100,7 +130,19 @@ int engine_collect(ob_panel* p);
 int engine_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_reps, hipStream_t s,
                   uint32_t* nb_rep, uint32_t* rep_pad);
 // ob_gram_i8.hip
-int oz_prepare(ob_panel* p, const std::vector<uint32_t>& chunks);
+int oz_prepare(ob_panel* p, hipStream_t s);
 int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t* counts, uint32_t nb_rep,
             uint32_t rep_pad, uint32_t n_reps, double* partial, hipStream_t s);
+// adds the exception rows' f64 terms to the reduced Grams [rep][2][e_pad] of a segment
+int oz_exceptions(ob_panel* p, const uint32_t* counts, uint32_t nb_rep, uint32_t n_reps, double* gram, hipStream_t s);
+// after the stream is synchronized: exception count / bits into p->timing, overflow -> error
+int oz_collect(ob_panel* p);
+void oz_free(ob_panel* p);
+// ob_shard.cpp
+void shard_free(ob_panel* p);
+// ob_shard_kernels.hip (layouts: ob_shard_layout.h)
+int shard_pack(const double* rows, const uint8_t* ok, const ob_shard_range& s, int rl, int nc, const int32_t* cols,
+               int n_y, double* send, uint8_t* send_ok, hipStream_t st);
+int shard_unpack(const double* recv, const uint8_t* recv_ok, const ob_shard_range& s, int world, uint64_t n_reps,
+                 int rl, int nc, const int32_t* cmap, int n_y, const double* own, double* rows, uint8_t* ok, hipStream_t st);
 }  // namespace ob

@@ -84,74 +84,311 @@ __device__ __forceinline__ void oz_pair_cols(int pair, int k1, int* a, int* b) {
   *b = aa + rem;
 }
 
-// Per (chunk, pair): the exponent E with 2^(E-1) <= max |P| < 2^E over the chunk's rows (0 if all
-// zero or a padding pair). Same product expression as oz_digits_kernel.
-__global__ __launch_bounds__(256) void oz_pairexp_kernel(const double* cols0, const double* cols1, int64_t ld0,
-                                                         int64_t ld1, uint32_t n0, uint32_t n1, int nxy, int weighted,
-                                                         const uint32_t* chunks, int k1, int e, int n_pairs_pad,
-                                                         int32_t* pexp) {
-  __shared__ double red[256];
-  const int chunk = blockIdx.x, pair = blockIdx.y, tid = threadIdx.x;
-  if (pair >= e) {
-    if (tid == 0) pexp[chunk * n_pairs_pad + pair] = 0;
-    return;
-  }
-  int ca, cb;
-  oz_pair_cols(pair, k1, &ca, &cb);
-  const uint32_t g = chunks[3 * chunk];
-  const double* cols = g ? cols1 : cols0;
-  const int64_t ld = g ? ld1 : ld0;
-  const uint32_t n = g ? n1 : n0;
-  const size_t r0 = (size_t)chunks[3 * chunk + 1] * OB_TILE_ROWS;
-  const size_t r1 = std::min<size_t>((size_t)chunks[3 * chunk + 2] * OB_TILE_ROWS, n);
-  double m = 0.0;
-  for (size_t r = r0 + tid; r < r1; r += 256)
-    m = fmax(m, fabs(oz_v(cols, ld, nxy, weighted, r, ca) * oz_v(cols, ld, nxy, weighted, r, cb)));
-  red[tid] = m;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (tid < o) red[tid] = fmax(red[tid], red[tid + o]);
-    __syncthreads();
-  }
-  if (tid == 0) {
-    int ex = 0;
-    if (red[0] > 0.0) (void)frexp(red[0], &ex);  // red[0] = f 2^ex, f in [0.5, 1)
-    pexp[chunk * n_pairs_pad + pair] = ex;
+// ---------------------------------------------------------------------------------------------
+// Panel preparation (once per panel, on the boot stream; no host synchronization).
+//
+// Exception rows. A fixed-point exponent per (chunk, pair) rounds every product of the chunk to
+// 2^(E-55): a row whose magnitude dwarfs the chunk's (a top-coded 99,999,999, a sentinel, a
+// heavy-tail draw) would set E for all the others and cost every replicate that does not draw it
+// up to (max / typical)^2 2^-55 of relative accuracy. So, per (chunk, column c), the scale s_c is
+// the rounded mean binary exponent of the column's nonzero finite |v_c| (the log of its geometric
+// mean: one outlier in 15k rows moves it by 27 / 15k), and a row is an exception when some
+// |v_c| >= 2^(s_c + B), or some v_c is not finite. Exception rows get zero digits and enter every
+// replicate's Gram as c_ri P_i in f64 (oz_exc_kernel, zero counts skipped -- the gathered rows of
+// the reference, builder.rs:822-829, never touch an undrawn row, NaN or not). For the others
+// |v_c| < 2^(s_c + B) <= 2^(B + 1) rms(v_c) (rms >= geometric mean), so the rounding of any Gram
+// entry stays below 2^(2B - 53) sqrt(G_aa G_bb) in the worst case (every rounding the same sign;
+// ~ sqrt(n) smaller in practice): 2^-37 at B = 8. B starts at kOzBitsMin and rises only if more
+// than kOzExcCap rows would be exceptions; more than kOzExcCap non-finite rows is an error.
+// ---------------------------------------------------------------------------------------------
+constexpr int kOzExcCap = 4096;  // exception rows per panel (both groups)
+constexpr int kOzBitsMin = 8;
+constexpr int kOzMaxK1 = 128;
+constexpr int kExpBias = 4096;  // pair exponents while being reduced: ex + kExpBias, 0 = all zero
+// d_oz_meta (int32): [0] B, [1] exceptions X (<= cap), [2] group-A exceptions, [3] overflow,
+// [4] append cursor, [kMetaHist + d + 128] rows of deviation d (d in [-128, 127], 127 = non-finite)
+constexpr int kMetaHist = 8;
+constexpr int kMetaWords = kMetaHist + 256;
+
+// Per (chunk, column): sum of the binary exponents (frexp) of the nonzero finite v_c and their
+// count. Grid: the group's tiles (a tile lies in one chunk), one row per thread.
+__global__ __launch_bounds__(256) void oz_scale_kernel(const double* cols, int64_t ld, uint32_t n, int nxy,
+                                                       int weighted, int k1, const int32_t* tile_chunk,
+                                                       unsigned long long* acc) {
+  const uint32_t tile = blockIdx.x, row = tile * 256u + threadIdx.x;
+  const int chunk = tile_chunk[tile], lane = threadIdx.x & 63;
+  for (int c = 0; c < k1; ++c) {
+    const double v = row < n ? oz_v(cols, ld, nxy, weighted, row, c) : 0.0;
+    int ex = 0, nz = 0;
+    if (v != 0.0 && isfinite(v)) {
+      (void)frexp(v, &ex);
+      nz = 1;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      ex += __shfl_xor(ex, o);
+      nz += __shfl_xor(nz, o);
+    }
+    if (lane == 0 && nz) {
+      atomicAdd(&acc[((size_t)chunk * k1 + c) * 2], (unsigned long long)(long long)ex);
+      atomicAdd(&acc[((size_t)chunk * k1 + c) * 2 + 1], (unsigned long long)nz);
+    }
   }
 }
 
-// B digits of one group: grid (sub-tile, column tile), 256 threads = (slice group, pair block, lane).
-__global__ __launch_bounds__(256) void oz_digits_kernel(const double* cols, int64_t ld, uint32_t n, int nxy,
-                                                        int weighted, int k1, int e, int n_ct, int n_pairs_pad,
-                                                        const int32_t* tile_chunk, const int32_t* pexp,
-                                                        ob_v4i* B) {
-  const uint32_t sub = blockIdx.x;
-  const int ct = blockIdx.y, t = threadIdx.x, lane = t & 63, nb = (t >> 6) & 1, grp = t >> 7;
-  const int pair = ct * kPairsPerTile + 16 * nb + (lane & 15);
-  int a = 0, b = 0;
-  const bool live = pair < e;
-  if (live) oz_pair_cols(pair, k1, &a, &b);
-  const int E = live ? pexp[tile_chunk[sub >> 2] * n_pairs_pad + pair] : 0;
-  int8_t dig[16][kS];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const size_t row = (size_t)sub * 64 + 16 * (lane >> 4) + j;
-    double P = 0.0;
-    if (live && row < n) P = oz_v(cols, ld, nxy, weighted, row, a) * oz_v(cols, ld, nxy, weighted, row, b);
-    long long m = (long long)rint(ldexp(P, kFracBits - E));  // |m| <= 2^54: exact
-#pragma unroll
-    for (int sl = kS - 1; sl >= 0; --sl) {  // balanced digits, least significant first
-      const int8_t d = (int8_t)(m & 0xff);
-      dig[j][sl] = d;
-      m = (m - d) >> 8;
+// Per row: d = max over columns of (exponent of v_c - s_c), clamped to [-128, 126]; 127 if some v_c
+// is not finite; -128 for all-zero and padding rows. Histogram into meta.
+__global__ __launch_bounds__(256) void oz_dev_kernel(const double* cols, int64_t ld, uint32_t n, int nxy, int weighted,
+                                                     int k1, const int32_t* tile_chunk, const long long* acc,
+                                                     int8_t* dev, int32_t* meta) {
+  __shared__ int sc[kOzMaxK1];
+  __shared__ uint32_t hist[256];
+  const int tid = threadIdx.x;
+  const uint32_t tile = blockIdx.x, row = tile * 256u + tid;
+  const int chunk = tile_chunk[tile];
+  hist[tid] = 0u;
+  for (int c = tid; c < k1; c += 256) {
+    const long long s = acc[((size_t)chunk * k1 + c) * 2], m = acc[((size_t)chunk * k1 + c) * 2 + 1];
+    sc[c] = m ? (int)floor((double)s / (double)m + 0.5) : 0;
+  }
+  __syncthreads();
+  int d = -128;
+  if (row < n) {
+    for (int c = 0; c < k1; ++c) {
+      const double v = oz_v(cols, ld, nxy, weighted, row, c);
+      if (v == 0.0) continue;
+      if (!isfinite(v)) {
+        d = 127;
+        break;
+      }
+      int ex = 0;
+      (void)frexp(v, &ex);
+      d = max(d, min(ex - sc[c], 126));
     }
   }
-  const int sl0 = grp ? kSlo : 0, sl1 = grp ? kS : kSlo;
-  for (int sl = sl0; sl < sl1; ++sl) {
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
+  dev[row] = (int8_t)d;  // the grid covers the padded rows ld = 256 x tiles exactly
+  atomicAdd(&hist[d + 128], 1u);
+  __syncthreads();
+  if (hist[tid]) atomicAdd(reinterpret_cast<uint32_t*>(meta) + kMetaHist + tid, hist[tid]);
+}
+
+// B = the smallest bits >= kOzBitsMin that leaves at most kOzExcCap exception rows.
+__global__ void oz_choose_kernel(int32_t* meta) {
+  if (threadIdx.x != 0) return;
+  const uint32_t* h = reinterpret_cast<const uint32_t*>(meta) + kMetaHist;
+  int b = kOzBitsMin;
+  unsigned long long x = 0;
+  for (;; ++b) {
+    x = 0;
+    for (int d = b + 1; d <= 127; ++d) x += h[d + 128];
+    if (x <= (unsigned long long)kOzExcCap || b >= 126) break;
+  }
+  meta[0] = b;
+  meta[1] = (int32_t)min(x, (unsigned long long)kOzExcCap);
+  meta[3] = x > (unsigned long long)kOzExcCap ? 1 : 0;
+  meta[4] = 0;
+}
+
+__global__ __launch_bounds__(256) void oz_collect_kernel(const int8_t* dev, uint32_t n, uint32_t g, int32_t* meta,
+                                                         uint32_t* exc) {
+  const uint32_t row = blockIdx.x * 256u + threadIdx.x;
+  if (row >= n || dev[row] <= meta[0]) return;
+  const int slot = atomicAdd(&meta[4], 1);
+  if (slot < kOzExcCap) exc[slot] = (g << 31) | row;
+}
+
+// One block: bitonic sort of the exception list (padding 0xFFFFFFFF sorts last), so the f64 sums
+// run in a fixed order (group A rows ascending, then group B's); meta[2] = group A's count.
+__global__ __launch_bounds__(1024) void oz_sort_kernel(uint32_t* exc, int32_t* meta) {
+  __shared__ uint32_t s[kOzExcCap];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < kOzExcCap; i += 1024) s[i] = exc[i];
+  __syncthreads();
+  for (int k = 2; k <= kOzExcCap; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < kOzExcCap; i += 1024) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const uint32_t a = s[i], b = s[ixj];
+          if ((a > b) == ((i & k) == 0)) {
+            s[i] = b;
+            s[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  for (int i = tid; i < kOzExcCap; i += 1024) {
+    exc[i] = s[i];
+    const bool here = s[i] < 0x80000000u, next = i + 1 < kOzExcCap && s[i + 1] < 0x80000000u;
+    if (here && !next) meta[2] = i + 1;
+  }
+  if (tid == 0 && s[0] >= 0x80000000u) meta[2] = 0;
+}
+
+// f64 pair products of the exception rows: excp[x][e] = v_a v_b (NaN / inf kept).
+__global__ __launch_bounds__(256) void oz_excp_kernel(const double* cols0, const double* cols1, int64_t ld0,
+                                                      int64_t ld1, int nxy, int weighted, int k1, int e, int e_pad,
+                                                      const uint32_t* exc, const int32_t* meta, double* excp) {
+  const int x = blockIdx.x;
+  if (x >= meta[1]) return;
+  const uint32_t ent = exc[x], g = ent >> 31, row = ent & 0x7FFFFFFFu;
+  const double* cols = g ? cols1 : cols0;
+  const int64_t ld = g ? ld1 : ld0;
+  for (int q = threadIdx.x; q < e_pad; q += 256) {
+    double P = 0.0;
+    if (q < e) {
+      int a, b;
+      oz_pair_cols(q, k1, &a, &b);
+      P = oz_v(cols, ld, nxy, weighted, row, a) * oz_v(cols, ld, nxy, weighted, row, b);
+    }
+    excp[(size_t)x * e_pad + q] = P;
+  }
+}
+
+// Stage the 64 rows [row0, row0 + 64) of every v column into vs[r * k1p + c], exception and
+// padding rows as zeros. Coalesced: 64 consecutive rows of one column per wave instruction.
+__device__ __forceinline__ void oz_stage(double* vs, int k1p, const double* cols, int64_t ld, uint32_t n, int nxy,
+                                         int weighted, int k1, const int8_t* dev, int bits, size_t row0) {
+  for (int i = threadIdx.x; i < 64 * k1; i += 256) {
+    const int r = i & 63, c = i >> 6;
+    const size_t row = row0 + r;
+    vs[r * k1p + c] = (row < n && dev[row] <= bits) ? oz_v(cols, ld, nxy, weighted, row, c) : 0.0;
+  }
+}
+
+// Per (chunk, pair): the largest |P| over the chunk's regular rows, as the raw exponent
+// ex + kExpBias (atomicMax; 2^(ex-1) <= max |P| < 2^ex). Grid: the group's tiles.
+__global__ __launch_bounds__(256) void oz_pexp_kernel(const double* cols, int64_t ld, uint32_t n, int nxy,
+                                                      int weighted, int k1, int e, int npp, const int32_t* tile_chunk,
+                                                      const int8_t* dev, const int32_t* meta, int32_t* raw) {
+  extern __shared__ __attribute__((aligned(16))) double ozs[];
+  const int k1p = k1 | 1, tid = threadIdx.x;
+  double* vs = ozs;               // [64][k1p]
+  double* mx = ozs + 64 * k1p;    // [e]
+  uint8_t* pa = reinterpret_cast<uint8_t*>(mx + e);
+  uint8_t* pb = pa + e;
+  const uint32_t tile = blockIdx.x;
+  const int chunk = tile_chunk[tile], bits = meta[0];
+  for (int q = tid; q < e; q += 256) {
+    int a, b;
+    oz_pair_cols(q, k1, &a, &b);
+    pa[q] = (uint8_t)a;
+    pb[q] = (uint8_t)b;
+    mx[q] = 0.0;
+  }
+  for (int sub = 0; sub < 4; ++sub) {
+    __syncthreads();
+    oz_stage(vs, k1p, cols, ld, n, nxy, weighted, k1, dev, bits, (size_t)tile * 256 + sub * 64);
+    __syncthreads();
+    for (int q = tid; q < e; q += 256) {
+      const int a = pa[q], b = pb[q];
+      double m = mx[q];
+#pragma unroll 8
+      for (int r = 0; r < 64; ++r) m = fmax(m, fabs(vs[r * k1p + a] * vs[r * k1p + b]));
+      mx[q] = m;
+    }
+  }
+  for (int q = tid; q < e; q += 256)
+    if (mx[q] > 0.0) {
+      int ex = 0;
+      (void)frexp(mx[q], &ex);
+      atomicMax(&raw[(size_t)chunk * npp + q], ex + kExpBias);
+    }
+}
+
+__global__ __launch_bounds__(256) void oz_pexp_finish_kernel(int32_t* pexp, int count) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < count) pexp[i] = pexp[i] ? pexp[i] - kExpBias : 0;
+}
+
+// B digits of one 64-row sub-tile for every column tile: grid = the group's sub-tiles. Unit u =
+// (column tile, pair block, lane): lane l holds pair 16 nb + (l & 15), rows 16 (l >> 4) + j -- the B
+// fragment -- and writes one 16-byte word per slice (consecutive units: consecutive 16 B).
+__global__ __launch_bounds__(256) void oz_digits_kernel(const double* cols, int64_t ld, uint32_t n, int nxy,
+                                                        int weighted, int k1, int e, int n_ct, int n_pairs_pad,
+                                                        const int32_t* tile_chunk, const int8_t* dev,
+                                                        const int32_t* meta, const int32_t* pexp, ob_v4i* B) {
+  extern __shared__ __attribute__((aligned(16))) double ozs[];
+  const int k1p = k1 | 1;
+  const uint32_t sub = blockIdx.x;
+  const int chunk = tile_chunk[sub >> 2];
+  oz_stage(ozs, k1p, cols, ld, n, nxy, weighted, k1, dev, meta[0], (size_t)sub * 64);
+  __syncthreads();
+  for (int u = threadIdx.x; u < n_ct * 128; u += 256) {
+    const int ct = u >> 7, nb = (u >> 6) & 1, lane = u & 63;
+    const int pair = ct * kPairsPerTile + 16 * nb + (lane & 15);
+    int a = 0, b = 0;
+    const bool live = pair < e;
+    if (live) oz_pair_cols(pair, k1, &a, &b);
+    const int E = live ? pexp[(size_t)chunk * n_pairs_pad + pair] : 0;
+    const double* v0 = ozs + 16 * (lane >> 4) * k1p;
+    long long m[16];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) w[j >> 2] |= (uint32_t)(uint8_t)dig[j][sl] << (8 * (j & 3));
-    B[(((size_t)sub * n_ct + ct) * kS + sl) * 2 * 64 + nb * 64 + lane] = (ob_v4i){(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+    for (int j = 0; j < 16; ++j) {
+      const double P = live ? v0[j * k1p + a] * v0[j * k1p + b] : 0.0;
+      m[j] = (long long)rint(ldexp(P, kFracBits - E));  // |m| <= 2^54: exact
+    }
+    ob_v4i* dst = B + ((size_t)sub * n_ct + ct) * kS * 128 + nb * 64 + lane;
+#pragma unroll
+    for (int sl = kS - 1; sl >= 0; --sl) {  // balanced digits, least significant first
+      uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int8_t d = (int8_t)(m[j] & 0xff);
+        w[j >> 2] |= (uint32_t)(uint8_t)d << (8 * (j & 3));
+        m[j] = (m[j] - d) >> 8;
+      }
+      dst[sl * 128] = (ob_v4i){(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+    }
+  }
+}
+
+// The exception rows' terms of a segment: gram[rep][g][e] += sum_x c(rep, x) P_x[e] over the
+// group's exception rows in list order, zero counts skipped. Grid: (64-replicate batch, group).
+// c(rep, row) is byte (j & 15) of A-fragment unit ((tile * nb_rep + batch) * 4 + sub-tile) * 256 +
+// (r >> 4) * 64 + (j >> 4) * 16 + (r & 15) (ob_count_kernel<true>; j = row & 63, r = rep & 63).
+__global__ __launch_bounds__(256) void oz_exc_kernel(const uint8_t* counts, uint32_t nb_rep, uint32_t tiles0,
+                                                     const uint32_t* exc, const double* excp, const int32_t* meta,
+                                                     int e, int e_pad, uint32_t n_reps, double* gram) {
+  __shared__ uint8_t cnt[64][64];  // [exception][replicate]
+  __shared__ double pv[64][64];    // [exception][pair]
+  const uint32_t rb = blockIdx.x, g = blockIdx.y;
+  const int nx_all = meta[1], na = meta[2];
+  const int x0 = g ? na : 0, x1 = g ? nx_all : na;
+  if (x0 >= x1) return;
+  const int tid = threadIdx.x, el = tid & 63, rq = tid >> 6;
+  for (int eb = 0; eb < e; eb += 64) {
+    double acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0;
+    for (int xb = x0; xb < x1; xb += 64) {
+      const int nx = min(64, x1 - xb);
+      __syncthreads();
+      for (int i = tid; i < 64 * nx; i += 256) {
+        const int j = i >> 6, r = i & 63;
+        const uint32_t row = exc[xb + j] & 0x7FFFFFFFu, jr = row & 63u;
+        const size_t unit = (((size_t)(g ? tiles0 : 0u) + (row >> 8)) * nb_rep + rb) * 1024 + ((row >> 6) & 3u) * 256 +
+                            (r >> 4) * 64 + (jr >> 4) * 16 + (r & 15);
+        cnt[j][r] = counts[unit * 16 + (jr & 15u)];
+        pv[j][r] = eb + r < e ? excp[(size_t)(xb + j) * e_pad + eb + r] : 0.0;
+      }
+      __syncthreads();
+      for (int j = 0; j < nx; ++j) {
+        const double pj = pv[j][el];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const uint32_t c = cnt[j][rq * 16 + i];
+          if (c) acc[i] += (double)c * pj;
+        }
+      }
+    }
+    if (eb + el < e)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t rep = rb * 64u + (uint32_t)(rq * 16 + i);
+        if (rep < n_reps) gram[((size_t)rep * 2 + g) * e_pad + eb + el] += acc[i];
+      }
   }
 }
 
@@ -398,16 +635,18 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
 
 namespace ob {
 
-// Build (once per panel) the digit images and exponents for the panel's chunking. Returns OB_OK
-// with p->oz_state = 1, or OB_OK with p->oz_state = -1 when the digit images would not fit (the
-// caller keeps the f64 MFMA Gram).
-int oz_prepare(ob_panel* p, const std::vector<uint32_t>& chunks) {
+// Build (once per panel, on stream s) the digit images, the pair exponents and the exception
+// rows for the panel's chunking (p->chunks, already in p->d_chunks). Returns OB_OK with
+// p->oz_state = 1, or OB_OK with p->oz_state = -1 when the digit images would not fit (the
+// caller keeps the f64 MFMA Gram). Enqueue only: nothing here waits for the device.
+int oz_prepare(ob_panel* p, hipStream_t s) {
   if (p->oz_state != 0) return OB_OK;
   // exact int32 slice sums need 128 x (a chunk's draws) < 2^31: a group's draws bound a chunk's
-  if (p->n[0] >= (1u << 24) || p->n[1] >= (1u << 24)) {
+  if (p->n[0] >= (1u << 24) || p->n[1] >= (1u << 24) || p->k1 > kOzMaxK1 || !p->chunks_ready) {
     p->oz_state = -1;
     return OB_OK;
   }
+  const std::vector<uint32_t>& chunks = p->chunks;
   const int n_chunks = (int)(chunks.size() / 3);
   const int n_ct = (p->e + kPairsPerTile - 1) / kPairsPerTile;
   const int npp = n_ct * kPairsPerTile;
@@ -420,54 +659,144 @@ int oz_prepare(ob_panel* p, const std::vector<uint32_t>& chunks) {
     p->oz_state = -1;
     return OB_OK;
   }
-  for (int g = 0; g < 2; ++g)
-    OZ_HIP(hipMalloc(&p->d_oz_b[g], std::max<size_t>((size_t)(p->ld[g] >> 6) * n_ct * kSubUnits * 16, 16)));
-  OZ_HIP(hipMalloc(&p->d_oz_pexp, sizeof(int32_t) * (size_t)n_chunks * npp));
-  int32_t* d_tc = nullptr;
-  uint32_t* d_chunks = nullptr;
-  int rc = OB_OK;
-  do {
-#define OZ_TRY(expr)                                                                                     \
-  {                                                                                                      \
-    hipError_t e_ = (expr);                                                                              \
-    if (e_ != hipSuccess) {                                                                              \
-      rc = ob::fail(OB_E_HIP, "HIP error %s at %s:%d", hipGetErrorString(e_), __FILE__, __LINE__);      \
-      break;                                                                                             \
-    }                                                                                                    \
+  for (int g = 0; g < 2; ++g) {
+    if (!p->d_oz_b[g])
+      OZ_HIP(hipMalloc(&p->d_oz_b[g], std::max<size_t>((size_t)(p->ld[g] >> 6) * n_ct * kSubUnits * 16, 16)));
+    if (!p->d_oz_dev[g]) OZ_HIP(hipMalloc(&p->d_oz_dev[g], std::max<size_t>((size_t)p->ld[g], 1)));
+    if (!p->d_oz_tile_chunk[g]) OZ_HIP(hipMalloc(&p->d_oz_tile_chunk[g], sizeof(int32_t) * std::max(p->ntiles[g], 1u)));
+    p->oz_tile_chunk[g].assign(std::max(p->ntiles[g], 1u), 0);
   }
-    OZ_TRY(hipMalloc(&d_chunks, sizeof(uint32_t) * chunks.size()));
-    OZ_TRY(hipMemcpy(d_chunks, chunks.data(), sizeof(uint32_t) * chunks.size(), hipMemcpyHostToDevice));
-    const int nxy = p->p + p->n_y;
-    hipLaunchKernelGGL(oz_pairexp_kernel, dim3(n_chunks, npp), dim3(256), 0, 0, (const double*)p->d_cols[0],
-                       (const double*)p->d_cols[1], p->ld[0], p->ld[1], p->n[0], p->n[1], nxy, p->weighted,
-                       (const uint32_t*)d_chunks, p->k1, p->e, npp, p->d_oz_pexp);
-    OZ_TRY(hipGetLastError());
-    for (int g = 0; g < 2 && rc == OB_OK; ++g) {
-      const uint32_t nsub = (uint32_t)(p->ld[g] >> 6);
-      if (nsub == 0) continue;
-      std::vector<int32_t> tc(p->ntiles[g] ? p->ntiles[g] : 1, 0);
-      for (int c = 0; c < n_chunks; ++c)
-        if (chunks[3 * c] == (uint32_t)g)
-          for (uint32_t t = chunks[3 * c + 1]; t < chunks[3 * c + 2]; ++t) tc[t] = c;
-      OZ_TRY(hipMalloc(&d_tc, sizeof(int32_t) * tc.size()));
-      OZ_TRY(hipMemcpy(d_tc, tc.data(), sizeof(int32_t) * tc.size(), hipMemcpyHostToDevice));
-      hipLaunchKernelGGL(oz_digits_kernel, dim3(nsub, n_ct), dim3(256), 0, 0, (const double*)p->d_cols[g], p->ld[g],
-                         p->n[g], nxy, p->weighted, p->k1, p->e, n_ct, npp, (const int32_t*)d_tc,
-                         (const int32_t*)p->d_oz_pexp, reinterpret_cast<ob_v4i*>(p->d_oz_b[g]));
-      OZ_TRY(hipGetLastError());
-      OZ_TRY(hipDeviceSynchronize());
-      (void)hipFree(d_tc);
-      d_tc = nullptr;
+  if (!p->d_oz_pexp) OZ_HIP(hipMalloc(&p->d_oz_pexp, sizeof(int32_t) * (size_t)n_chunks * npp));
+  if (!p->d_oz_acc) OZ_HIP(hipMalloc(&p->d_oz_acc, sizeof(int64_t) * 2 * (size_t)n_chunks * p->k1));
+  if (!p->d_oz_meta) OZ_HIP(hipMalloc(&p->d_oz_meta, sizeof(int32_t) * kMetaWords));
+  if (!p->d_oz_exc) OZ_HIP(hipMalloc(&p->d_oz_exc, sizeof(uint32_t) * kOzExcCap));
+  if (!p->d_oz_excp) OZ_HIP(hipMalloc(&p->d_oz_excp, sizeof(double) * kOzExcCap * (size_t)p->e_pad));
+  for (int i = 0; i < 2; ++i)
+    if (!p->oz_ev[i]) OZ_HIP(hipEventCreate(&p->oz_ev[i]));
+  for (int c = 0; c < n_chunks; ++c)
+    for (uint32_t t = chunks[3 * c + 1]; t < chunks[3 * c + 2]; ++t) p->oz_tile_chunk[chunks[3 * c]][t] = c;
+
+  OZ_HIP(hipEventRecord(p->oz_ev[0], s));
+  for (int g = 0; g < 2; ++g)
+    OZ_HIP(hipMemcpyAsync(p->d_oz_tile_chunk[g], p->oz_tile_chunk[g].data(), sizeof(int32_t) * p->oz_tile_chunk[g].size(),
+                          hipMemcpyHostToDevice, s));
+  OZ_HIP(hipMemsetAsync(p->d_oz_acc, 0, sizeof(int64_t) * 2 * (size_t)n_chunks * p->k1, s));
+  OZ_HIP(hipMemsetAsync(p->d_oz_meta, 0, sizeof(int32_t) * kMetaWords, s));
+  OZ_HIP(hipMemsetAsync(p->d_oz_pexp, 0, sizeof(int32_t) * (size_t)n_chunks * npp, s));
+  OZ_HIP(hipMemsetAsync(p->d_oz_exc, 0xFF, sizeof(uint32_t) * kOzExcCap, s));
+  const int nxy = p->p + p->n_y;
+  const double* cols[2] = {p->d_cols[0], p->d_cols[1]};
+  for (int g = 0; g < 2; ++g)
+    if (p->ntiles[g]) {
+      hipLaunchKernelGGL(oz_scale_kernel, dim3(p->ntiles[g]), dim3(256), 0, s, cols[g], p->ld[g], p->n[g], nxy,
+                         p->weighted, p->k1, (const int32_t*)p->d_oz_tile_chunk[g],
+                         reinterpret_cast<unsigned long long*>(p->d_oz_acc));
+      OZ_HIP(hipGetLastError());
     }
-    if (rc == OB_OK) OZ_TRY(hipDeviceSynchronize());
-#undef OZ_TRY
-  } while (0);
-  (void)hipFree(d_tc);
-  (void)hipFree(d_chunks);
-  if (rc != OB_OK) return rc;
+  for (int g = 0; g < 2; ++g)
+    if (p->ntiles[g]) {
+      hipLaunchKernelGGL(oz_dev_kernel, dim3(p->ntiles[g]), dim3(256), 0, s, cols[g], p->ld[g], p->n[g], nxy,
+                         p->weighted, p->k1, (const int32_t*)p->d_oz_tile_chunk[g], (const long long*)p->d_oz_acc,
+                         p->d_oz_dev[g], p->d_oz_meta);
+      OZ_HIP(hipGetLastError());
+    }
+  hipLaunchKernelGGL(oz_choose_kernel, dim3(1), dim3(64), 0, s, p->d_oz_meta);
+  OZ_HIP(hipGetLastError());
+  for (int g = 0; g < 2; ++g)
+    if (p->ntiles[g]) {
+      hipLaunchKernelGGL(oz_collect_kernel, dim3(p->ntiles[g]), dim3(256), 0, s, (const int8_t*)p->d_oz_dev[g], p->n[g],
+                         (uint32_t)g, p->d_oz_meta, p->d_oz_exc);
+      OZ_HIP(hipGetLastError());
+    }
+  hipLaunchKernelGGL(oz_sort_kernel, dim3(1), dim3(1024), 0, s, p->d_oz_exc, p->d_oz_meta);
+  OZ_HIP(hipGetLastError());
+  hipLaunchKernelGGL(oz_excp_kernel, dim3(kOzExcCap), dim3(256), 0, s, cols[0], cols[1], p->ld[0], p->ld[1], nxy,
+                     p->weighted, p->k1, p->e, p->e_pad, (const uint32_t*)p->d_oz_exc, (const int32_t*)p->d_oz_meta,
+                     p->d_oz_excp);
+  OZ_HIP(hipGetLastError());
+  const int k1p = p->k1 | 1;
+  const size_t lds_pexp = sizeof(double) * ((size_t)64 * k1p + p->e) + 2 * (size_t)p->e;
+  const size_t lds_dig = sizeof(double) * (size_t)64 * k1p;
+  OZ_HIP(hipFuncSetAttribute((const void*)oz_pexp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_pexp));
+  OZ_HIP(hipFuncSetAttribute((const void*)oz_digits_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dig));
+  for (int g = 0; g < 2; ++g)
+    if (p->ntiles[g]) {
+      hipLaunchKernelGGL(oz_pexp_kernel, dim3(p->ntiles[g]), dim3(256), lds_pexp, s, cols[g], p->ld[g], p->n[g], nxy,
+                         p->weighted, p->k1, p->e, npp, (const int32_t*)p->d_oz_tile_chunk[g],
+                         (const int8_t*)p->d_oz_dev[g], (const int32_t*)p->d_oz_meta, p->d_oz_pexp);
+      OZ_HIP(hipGetLastError());
+    }
+  const int npe = n_chunks * npp;
+  hipLaunchKernelGGL(oz_pexp_finish_kernel, dim3((npe + 255) / 256), dim3(256), 0, s, p->d_oz_pexp, npe);
+  OZ_HIP(hipGetLastError());
+  for (int g = 0; g < 2; ++g) {
+    const uint32_t nsub = (uint32_t)(p->ld[g] >> 6);
+    if (p->ntiles[g] == 0 || nsub == 0) continue;
+    hipLaunchKernelGGL(oz_digits_kernel, dim3(nsub), dim3(256), lds_dig, s, cols[g], p->ld[g], p->n[g], nxy,
+                       p->weighted, p->k1, p->e, n_ct, npp, (const int32_t*)p->d_oz_tile_chunk[g],
+                       (const int8_t*)p->d_oz_dev[g], (const int32_t*)p->d_oz_meta, (const int32_t*)p->d_oz_pexp,
+                       reinterpret_cast<ob_v4i*>(p->d_oz_b[g]));
+    OZ_HIP(hipGetLastError());
+  }
+  OZ_HIP(hipEventRecord(p->oz_ev[1], s));
+  p->oz_timed = true;
+  p->oz_nexc = -1;
   p->oz_n_ct = n_ct;
   p->oz_state = 1;
   return OB_OK;
+}
+
+// The exception rows' f64 terms of one segment (after ob_reduce_kernel). Skipped once a synchronized
+// run has shown the panel has none.
+int oz_exceptions(ob_panel* p, const uint32_t* counts, uint32_t nb_rep, uint32_t n_reps, double* gram, hipStream_t s) {
+  if (p->oz_state != 1 || p->oz_nexc == 0 || n_reps == 0) return OB_OK;
+  hipLaunchKernelGGL(oz_exc_kernel, dim3(nb_rep, 2), dim3(256), 0, s, reinterpret_cast<const uint8_t*>(counts), nb_rep,
+                     p->ntiles[0], (const uint32_t*)p->d_oz_exc, (const double*)p->d_oz_excp,
+                     (const int32_t*)p->d_oz_meta, p->e, p->e_pad, n_reps, gram);
+  OZ_HIP(hipGetLastError());
+  return OB_OK;
+}
+
+// After the boot stream is synchronized: the preparation's time and exception statistics into
+// p->timing; more non-finite rows than the exception list holds is an error (their rows would
+// be missing from every Gram).
+int oz_collect(ob_panel* p) {
+  if (p->oz_state != 1) return OB_OK;
+  if (p->oz_timed) {
+    float t = 0.f;
+    OZ_HIP(hipEventElapsedTime(&t, p->oz_ev[0], p->oz_ev[1]));
+    p->timing.prep_ms = t;
+    p->oz_timed = false;
+  }
+  if (p->oz_nexc < 0) {
+    int32_t meta[4] = {0, 0, 0, 0};
+    OZ_HIP(hipMemcpy(meta, p->d_oz_meta, sizeof(meta), hipMemcpyDeviceToHost));
+    p->oz_bits = meta[0];
+    p->oz_nexc = meta[1];
+    p->oz_overflow = meta[3] != 0;
+  }
+  p->timing.oz_bits = p->oz_bits;
+  p->timing.oz_exceptions = p->oz_nexc;
+  if (p->oz_overflow)
+    return ob::fail(OB_E_UNSUPPORTED, "more than %d rows hold non-finite values (NaN or inf); the i8 Gram keeps at most "
+                                      "that many exception rows (OB_GRAM_PATH=f64 runs the f64 MFMA Gram)",
+                    kOzExcCap);
+  return OB_OK;
+}
+
+void oz_free(ob_panel* p) {
+  for (int g = 0; g < 2; ++g) {
+    (void)hipFree(p->d_oz_b[g]);
+    (void)hipFree(p->d_oz_dev[g]);
+    (void)hipFree(p->d_oz_tile_chunk[g]);
+  }
+  (void)hipFree(p->d_oz_pexp);
+  (void)hipFree(p->d_oz_acc);
+  (void)hipFree(p->d_oz_meta);
+  (void)hipFree(p->d_oz_exc);
+  (void)hipFree(p->d_oz_excp);
+  for (hipEvent_t e : p->oz_ev)
+    if (e) (void)hipEventDestroy(e);
 }
 
 // One segment's Gram partials: d_chunks holds the panel's chunk table, counts the I8 images of
@@ -513,3 +842,22 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
 }
 
 }  // namespace ob
+
+extern "C" {
+
+// Test hook (include/oaxaca_boot.h): the exception rows of the panel's i8 Gram, once built.
+int ob_debug_gram_exceptions(ob_panel* p, int32_t* bits, int32_t* n_exc, uint32_t* rows, int32_t cap) {
+  if (!p || !bits || !n_exc) return ob::fail(OB_E_INVALID, "null pointer");
+  if (p->oz_state != 1) return ob::fail(OB_E_INVALID, "the panel's i8 Gram is not built (run a boot on the i8 path first)");
+  OZ_HIP(hipSetDevice(p->ctx->device));
+  OZ_HIP(hipDeviceSynchronize());
+  int32_t meta[4] = {0, 0, 0, 0};
+  OZ_HIP(hipMemcpy(meta, p->d_oz_meta, sizeof(meta), hipMemcpyDeviceToHost));
+  *bits = meta[0];
+  *n_exc = meta[1];
+  if (rows && cap > 0 && meta[1] > 0)
+    OZ_HIP(hipMemcpy(rows, p->d_oz_exc, sizeof(uint32_t) * (size_t)std::min(cap, meta[1]), hipMemcpyDeviceToHost));
+  return meta[3] ? ob::fail(OB_E_UNSUPPORTED, "more than %d non-finite rows", kOzExcCap) : OB_OK;
+}
+
+}  // extern "C"

@@ -128,6 +128,10 @@ struct MmArgs {
   const double* quantiles;
   double* rows;  // [slot][3 n_q]
   uint8_t* ok;
+  // ob_debug_mm_fail (tests only): fit (g, s) of pass `rep` counts as failed when bit (rep & 7) of
+  // fail_mask[g * fail_sims + s] is set -- the reference's dropped Clarabel fits, on demand
+  const uint8_t* fail_mask;
+  int fail_sims;
 };
 
 __device__ __forceinline__ size_t fit_index(const MmArgs& a, uint32_t slot, uint32_t g, int s) {
@@ -1470,7 +1474,8 @@ __global__ __launch_bounds__(256) void mm_finish_kernel(const MmArgs a, int K, i
     const uint32_t* lanes = a.lane_of + ((size_t)slot * 2 + g) * a.S_pad;
     for (int s = 0; s < a.S; ++s) {
       const uint32_t j = lanes[s];
-      if (a.fstat[fit_index(a, slot, g, (int)j)] == kDone) idx[k++] = (uint16_t)j;
+      const bool forced = a.fail_mask && s < a.fail_sims && ((a.fail_mask[g * a.fail_sims + s] >> (rep & 7u)) & 1u);
+      if (a.fstat[fit_index(a, slot, g, (int)j)] == kDone && !forced) idx[k++] = (uint16_t)j;
     }
     cnt[g] = k;
   }
@@ -2049,6 +2054,8 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   a.quantiles = b.quant;
   a.rows = b.rows;
   a.ok = b.ok;
+  a.fail_mask = p->d_mm_fail;
+  a.fail_sims = p->mm_fail_sims;
   const auto t0 = std::chrono::steady_clock::now();
   MmStats st;
   size_t out = 0;
@@ -2102,4 +2109,17 @@ extern "C" int ob_mm_run(ob_panel* panel, uint64_t seed, int32_t simulations, co
   if (!panel || !quantiles || !rows || !ok) return ob::fail(OB_E_INVALID, "null pointer");
   return ob::mm_run(panel, seed, simulations, quantiles, n_quantiles, first_rep, n_reps, with_point != 0, rows, ok,
                     nullptr);
+}
+
+extern "C" int ob_debug_mm_fail(ob_panel* p, const uint8_t* mask, int32_t sims) {
+  if (!p || sims < 0 || (sims && !mask)) return ob::fail(OB_E_INVALID, "bad arguments");
+  MM_OK(hipSetDevice(p->ctx->device));
+  (void)hipFree(p->d_mm_fail);
+  p->d_mm_fail = nullptr;
+  p->mm_fail_sims = 0;
+  if (sims == 0) return OB_OK;
+  MM_OK(hipMalloc(&p->d_mm_fail, 2 * (size_t)sims));
+  MM_OK(hipMemcpy(p->d_mm_fail, mask, 2 * (size_t)sims, hipMemcpyHostToDevice));
+  p->mm_fail_sims = sims;
+  return OB_OK;
 }

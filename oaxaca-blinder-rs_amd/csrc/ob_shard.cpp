@@ -22,6 +22,7 @@
 
 #include "ob_common.hpp"
 #include "ob_engine.hpp"
+#include "ob_shard_layout.h"
 
 static_assert(sizeof(ob_unique_id) == sizeof(ncclUniqueId), "ob_unique_id mirrors ncclUniqueId");
 
@@ -96,22 +97,15 @@ void comm_free(void* c) {
   if (destroy) (void)destroy((ncclComm_t)c);
 }
 
-struct Shard {
-  uint64_t per, first, count;
-};
+using Shard = ob_shard_range;
 
 Shard shard_of(uint64_t first_rep, uint64_t n_reps, int rank, int world) {
-  Shard s;
-  s.per = (n_reps + (uint64_t)world - 1) / (uint64_t)world;
-  const uint64_t lo = std::min<uint64_t>((uint64_t)rank * s.per, n_reps);
-  s.first = first_rep + lo;
-  s.count = std::min<uint64_t>(n_reps, lo + s.per) - lo;
-  return s;
+  return ob_shard_of(first_rep, n_reps, rank, world);
 }
 
 template <typename T>
 int ensure_dev(T** buf, size_t* cap, size_t elems) {
-  if (*cap >= elems) return OB_OK;
+  if (*cap >= elems && *buf) return OB_OK;
   (void)hipFree(*buf);
   *buf = nullptr;
   *cap = 0;
@@ -120,20 +114,40 @@ int ensure_dev(T** buf, size_t* cap, size_t elems) {
   return OB_OK;
 }
 
-// Enqueue this rank's shard into the panel's shard buffers ([t][count][row_len] blocks inside an
-// n_y x per x row_len allocation), then the all-gather of each outcome's per-row block into
-// [t][world x per][row_len]. The gathered blocks are in replicate order (rank r holds ids
-// [r per, (r+1) per)); the padding past n_reps is ignored. Collective calls are enqueued by
-// `gather` so that several devices' calls can share one ncclGroupStart/End.
+int n_gather_cols(const ob_panel* p) { return p->gather_cols.empty() ? p->row_len : (int)p->gather_cols.size(); }
+
+// The gathered-column map on the device: [row_len] slot of each row column (-1: not gathered),
+// then the nc gathered columns. Uploaded when the column set changes (a blocking copy).
+int ensure_gather_map(ob_panel* p) {
+  if (p->gather_map_ready) return OB_OK;
+  const int rl = p->row_len, nc = n_gather_cols(p);
+  std::vector<int32_t> m((size_t)rl + nc, -1);
+  for (int q = 0; q < nc; ++q) {
+    const int c = p->gather_cols.empty() ? q : p->gather_cols[q];
+    m[c] = q;
+    m[(size_t)rl + q] = c;
+  }
+  if (!p->d_gather_map) SH_HIP(hipMalloc(&p->d_gather_map, sizeof(int32_t) * (size_t)(2 * rl)));
+  SH_HIP(hipMemcpy(p->d_gather_map, m.data(), sizeof(int32_t) * m.size(), hipMemcpyHostToDevice));
+  p->gather_map_ready = true;
+  return OB_OK;
+}
+
+
+// Enqueue this rank's shard into the panel's shard buffers, then pack the gathered columns into
+// the send block and record the gather's start event.
 int shard_compute(ob_panel* p, uint64_t seed, const Shard& sh, int world, int ref_mode, hipStream_t s) {
   const size_t rl = (size_t)p->row_len, ny = (size_t)p->n_y;
+  const int nc = n_gather_cols(p);
   SH_HIP(hipSetDevice(p->ctx->device));
+  OB_TRY(ensure_gather_map(p));
   const size_t slots = ny * std::max<uint64_t>(sh.per, 1);
   OB_TRY(ensure_dev(&p->d_shard_rows, &p->cap_shard, slots * rl));
   OB_TRY(ensure_dev(&p->d_shard_ok, &p->cap_shard_ok, slots));
-  OB_TRY(ensure_dev(&p->d_gather_rows, &p->cap_gather, slots * (size_t)world * rl));
+  OB_TRY(ensure_dev(&p->d_send, &p->cap_send, slots * (size_t)nc));
+  OB_TRY(ensure_dev(&p->d_send_ok, &p->cap_send_ok, slots));
+  OB_TRY(ensure_dev(&p->d_gather_rows, &p->cap_gather, slots * (size_t)world * nc));
   OB_TRY(ensure_dev(&p->d_gather_ok, &p->cap_gather_ok, slots * (size_t)world));
-  SH_HIP(hipMemsetAsync(p->d_shard_ok, 0, slots, s));
   if (sh.count) {
     OB_TRY(ob::engine_boot(p, seed, sh.first, sh.count, ref_mode, p->d_shard_rows, p->d_shard_ok, s));
   } else {  // an empty shard (n_reps < world): nothing to time but the gather
@@ -145,35 +159,50 @@ int shard_compute(ob_panel* p, uint64_t seed, const Shard& sh, int world, int re
     SH_HIP(hipEventCreate(&p->gather_ev[1]));
   }
   SH_HIP(hipEventRecord(p->gather_ev[0], s));
+  OB_TRY(ob::shard_pack(p->d_shard_rows, p->d_shard_ok, sh, (int)rl, nc, p->d_gather_map + rl, (int)ny, p->d_send,
+                        p->d_send_ok, s));
   return OB_OK;
 }
 
+// One all-gather per outcome of the packed rows and of the ok bytes: rank r's block lands at
+// ob_recv_block_off(r).
 int shard_gather(const Rccl* r, ob_panel* p, ncclComm_t comm, const Shard& sh, int world, hipStream_t s) {
-  const size_t rl = (size_t)p->row_len;
-  for (int t = 0; t < p->n_y; ++t) {  // engine_boot wrote outcome t's rows at t * count
-    SH_NCCL(r, r->all_gather(p->d_shard_rows + (size_t)t * sh.count * rl,
-                             p->d_gather_rows + (size_t)t * world * sh.per * rl, sh.per * rl, ncclFloat64, comm, s),
+  const int nc = n_gather_cols(p);
+  for (int t = 0; t < p->n_y; ++t) {
+    SH_NCCL(r, r->all_gather(p->d_send + ob_send_off(sh, t, 0, nc, 0), p->d_gather_rows + ob_recv_block_off(sh, world, t, 0, nc),
+                             ob_send_elems(sh, nc), ncclFloat64, comm, s),
             "ncclAllGather(rows)");
-    SH_NCCL(r, r->all_gather(p->d_shard_ok + (size_t)t * sh.count, p->d_gather_ok + (size_t)t * world * sh.per,
+    SH_NCCL(r, r->all_gather(p->d_send_ok + ob_send_ok_off(sh, t, 0), p->d_gather_ok + ob_recv_block_off(sh, world, t, 0, 1),
                              sh.per, ncclUint8, comm, s),
             "ncclAllGather(ok)");
   }
   return OB_OK;
 }
 
-// Gathered blocks -> the caller's [t][n_reps] layout (device or host), then the gather's end event.
-int shard_deliver(ob_panel* p, const Shard& sh, int world, uint64_t n_reps, double* rows, uint8_t* ok,
-                  hipMemcpyKind kind, hipStream_t s) {
-  const size_t rl = (size_t)p->row_len;
+// Gathered blocks -> the caller's [t][n_reps] layout (device rows directly; host rows through the
+// panel's staging buffers), then the gather's end event. own: this rank's shard rows (for the
+// columns outside the gathered set), or the simulated rank's (ob_debug_shard_sim).
+int shard_deliver(ob_panel* p, const Shard& sh, int world, uint64_t n_reps, double* rows, uint8_t* ok, bool host,
+                  const double* own, hipStream_t s) {
+  const size_t rl = (size_t)p->row_len, ny = (size_t)p->n_y;
   SH_HIP(hipSetDevice(p->ctx->device));
   SH_HIP(hipEventRecord(p->gather_ev[1], s));
   p->gather_timed = true;
   p->timing_pending = true;  // ob_panel_sync waits on s and reads the gather's events
   p->last_stream = s;
-  for (int t = 0; t < p->n_y; ++t) {
-    SH_HIP(hipMemcpyAsync(rows + (size_t)t * n_reps * rl, p->d_gather_rows + (size_t)t * world * sh.per * rl,
-                          sizeof(double) * n_reps * rl, kind, s));
-    SH_HIP(hipMemcpyAsync(ok + (size_t)t * n_reps, p->d_gather_ok + (size_t)t * world * sh.per, n_reps, kind, s));
+  double* drows = rows;
+  uint8_t* dok = ok;
+  if (host) {
+    OB_TRY(ensure_dev(&p->d_deliver_rows, &p->cap_deliver, ny * n_reps * rl));
+    OB_TRY(ensure_dev(&p->d_deliver_ok, &p->cap_deliver_ok, ny * n_reps));
+    drows = p->d_deliver_rows;
+    dok = p->d_deliver_ok;
+  }
+  OB_TRY(ob::shard_unpack(p->d_gather_rows, p->d_gather_ok, sh, world, n_reps, (int)rl, n_gather_cols(p),
+                          p->d_gather_map, (int)ny, own, drows, dok, s));
+  if (host) {
+    SH_HIP(hipMemcpyAsync(rows, drows, sizeof(double) * ny * n_reps * rl, hipMemcpyDeviceToHost, s));
+    SH_HIP(hipMemcpyAsync(ok, dok, ny * n_reps, hipMemcpyDeviceToHost, s));
   }
   return OB_OK;
 }
@@ -199,7 +228,7 @@ int sharded_device(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_re
   const Shard sh = shard_of(first_rep, n_reps, c->rank, c->world);
   OB_TRY(shard_compute(p, seed, sh, c->world, ref_mode, s));
   OB_TRY(shard_gather(r, p, (ncclComm_t)c->comm, sh, c->world, s));
-  return shard_deliver(p, sh, c->world, n_reps, d_rows, d_ok, hipMemcpyDeviceToDevice, s);
+  return shard_deliver(p, sh, c->world, n_reps, d_rows, d_ok, false, p->d_shard_rows, s);
 }
 
 struct Clique {
@@ -273,7 +302,7 @@ int ob_boot_run_sharded(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t
   const Shard sh = shard_of(first_rep, n_reps, c->rank, c->world);
   OB_TRY(shard_compute(p, seed, sh, c->world, ref_mode, c->stream));
   OB_TRY(shard_gather(r, p, (ncclComm_t)c->comm, sh, c->world, c->stream));
-  OB_TRY(shard_deliver(p, sh, c->world, n_reps, rows, ok, hipMemcpyDeviceToHost, c->stream));
+  OB_TRY(shard_deliver(p, sh, c->world, n_reps, rows, ok, true, p->d_shard_rows, c->stream));
   return ob_panel_sync(p);
 }
 
@@ -289,6 +318,8 @@ int ob_boot_run_multi(ob_panel* const* panels, int n_panels, uint64_t seed, uint
     if (pi->row_len != p0->row_len || pi->n_y != p0->n_y || pi->n[0] != p0->n[0] || pi->n[1] != p0->n[1] ||
         pi->p != p0->p)
       return ob::fail(OB_E_INVALID, "panel %d does not hold the same design as panel 0", i);
+    if (pi->gather_cols != p0->gather_cols)
+      return ob::fail(OB_E_INVALID, "panel %d gathers other columns than panel 0", i);
     devs[i] = pi->ctx->device;
     for (int j = 0; j < i; ++j)
       if (devs[j] == devs[i]) return ob::fail(OB_E_INVALID, "panels %d and %d share device %d", j, i, devs[i]);
@@ -321,9 +352,73 @@ int ob_boot_run_multi(ob_panel* const* panels, int n_panels, uint64_t seed, uint
   SH_NCCL(r, r->group_end(), "ncclGroupEnd");
   OB_TRY(rc);
   ob_panel* p0 = panels[0];
-  OB_TRY(shard_deliver(p0, sh[0], n_panels, n_reps, rows, ok, hipMemcpyDeviceToHost, p0->ctx->stream));
+  OB_TRY(shard_deliver(p0, sh[0], n_panels, n_reps, rows, ok, true, p0->d_shard_rows, p0->ctx->stream));
   for (int i = 0; i < n_panels; ++i) OB_TRY(ob_panel_sync(panels[i]));
   return OB_OK;
 }
 
+int ob_panel_set_gather_columns(ob_panel* p, const int32_t* cols, int32_t n) {
+  if (!p || (n > 0 && !cols) || n < 0) return ob::fail(OB_E_INVALID, "bad arguments");
+  std::vector<int32_t> v(cols, cols + n);
+  for (int32_t i = 0; i < n; ++i)
+    if (v[i] < 0 || v[i] >= p->row_len || (i && v[i] <= v[i - 1]))
+      return ob::fail(OB_E_INVALID, "gather columns must be ascending row offsets in [0, %d)", p->row_len);
+  if ((int)v.size() == p->row_len) v.clear();  // every column
+  if (v != p->gather_cols) {
+    p->gather_cols = std::move(v);
+    p->gather_map_ready = false;
+  }
+  return OB_OK;
+}
+
+int ob_debug_shard_sim(ob_panel* p, int world, int self_rank, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
+                       int ref_mode, double* rows, uint8_t* ok) {
+  if (!p || world < 1 || self_rank < 0 || self_rank >= world || (n_reps && (!rows || !ok)))
+    return ob::fail(OB_E_INVALID, "bad arguments");
+  OB_TRY(check_panel(p, ref_mode));
+  if (n_reps == 0) return OB_OK;
+  hipStream_t s = p->ctx->stream;
+  const size_t rl = (size_t)p->row_len, ny = (size_t)p->n_y;
+  const int nc = n_gather_cols(p);
+  Shard self{};
+  for (int r = 0; r < world; ++r) {
+    const Shard sh = shard_of(first_rep, n_reps, r, world);
+    OB_TRY(shard_compute(p, seed, sh, world, ref_mode, s));
+    OB_TRY(ob::engine_collect(p));  // this rank's shard has finished (its ok / overflow checks)
+    for (int t = 0; t < p->n_y; ++t) {  // the all-gather's placement of rank r's blocks
+      SH_HIP(hipMemcpyAsync(p->d_gather_rows + ob_recv_block_off(sh, world, t, r, nc), p->d_send + ob_send_off(sh, t, 0, nc, 0),
+                            sizeof(double) * ob_send_elems(sh, nc), hipMemcpyDeviceToDevice, s));
+      SH_HIP(hipMemcpyAsync(p->d_gather_ok + ob_recv_block_off(sh, world, t, r, 1), p->d_send_ok + ob_send_ok_off(sh, t, 0),
+                            sh.per, hipMemcpyDeviceToDevice, s));
+    }
+    if (r == self_rank) {
+      self = sh;
+      OB_TRY(ensure_dev(&p->d_own_rows, &p->cap_own, std::max<size_t>(ny * sh.count * rl, 1)));
+      if (sh.count)
+        SH_HIP(hipMemcpyAsync(p->d_own_rows, p->d_shard_rows, sizeof(double) * ny * sh.count * rl, hipMemcpyDeviceToDevice, s));
+    }
+  }
+  OB_TRY(shard_deliver(p, self, world, n_reps, rows, ok, true, p->d_own_rows, s));
+  return ob_panel_sync(p);
+}
+
 }  // extern "C"
+
+namespace ob {
+
+void shard_free(ob_panel* p) {
+  (void)hipFree(p->d_shard_rows);
+  (void)hipFree(p->d_shard_ok);
+  (void)hipFree(p->d_send);
+  (void)hipFree(p->d_send_ok);
+  (void)hipFree(p->d_gather_rows);
+  (void)hipFree(p->d_gather_ok);
+  (void)hipFree(p->d_deliver_rows);
+  (void)hipFree(p->d_deliver_ok);
+  (void)hipFree(p->d_own_rows);
+  (void)hipFree(p->d_gather_map);
+  for (hipEvent_t e : p->gather_ev)
+    if (e) (void)hipEventDestroy(e);
+}
+
+}  // namespace ob

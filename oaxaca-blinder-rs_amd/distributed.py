@@ -75,19 +75,28 @@ def gather_rows(prepared, n_reps: int, group=None, device=None):
     return all_rows[:n_reps].cpu().numpy(), all_ok[:n_reps].cpu().numpy()
 
 
+_engine_ctx: dict = {}
+
+
 def engine_context(device: int, group=None):
     """This rank's engine context on an RCCL communicator spanning the group's ranks: rank 0's
-    ncclUniqueId travels by broadcast_object_list; the engine owns the communicator."""
+    ncclUniqueId travels by broadcast_object_list; the engine owns the communicator. One context
+    per (group, device, rank, world), reused by later fits: a communicator holds device buffers
+    and proxy threads, so a fresh one per fit would accumulate them."""
     import torch.distributed as dist
 
     from . import _native as N
 
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
-    uid = [N.unique_id() if rank == 0 else None]
-    if world > 1:
-        dist.broadcast_object_list(uid, src=0, group=group)
-    return N.rank_context(device, rank, world, uid[0])
+    key = (id(group) if group is not None else None, int(device), rank, world)
+    ctx = _engine_ctx.get(key)
+    if ctx is None:
+        uid = [N.unique_id() if rank == 0 else None]
+        if world > 1:
+            dist.broadcast_object_list(uid, src=0, group=group)
+        ctx = _engine_ctx[key] = N.rank_context(device, rank, world, uid[0])
+    return ctx
 
 
 def fit_sharded(builder, group=None, device=None, engine=False):

@@ -114,6 +114,11 @@ class Panel:
                                   n_reps, int(bool(with_point)), _dp(rows), ok.ctypes.data_as(C.POINTER(C.c_uint8))))
         return rows, ok
 
+    def debug_mm_fail(self, mask=None):
+        """ob_debug_mm_fail: mask[g][s] bit (rep & 7) forces fit (g, s) of pass rep to fail."""
+        m = np.ascontiguousarray(np.zeros((2, 0)) if mask is None else mask, dtype=np.uint8)
+        N.check(N.lib().ob_debug_mm_fail(self._h, m.ctypes.data_as(C.POINTER(C.c_uint8)), m.shape[1]))
+
     def boot_device(self, seed: int, first_rep: int, n_reps: int, rows_ptr: int, ok_ptr: int,
                     ref=ReferenceCoefficients.GroupA, stream: int | None = None):
         N.check(N.lib().ob_boot_run_device(self._h, seed & ((1 << 64) - 1), first_rep, n_reps, int(ref),
@@ -153,6 +158,35 @@ class Panel:
         g = np.empty((n_reps, 2, e_pad))
         N.check(N.lib().ob_debug_gram(self._h, int(path), seed & ((1 << 64) - 1), first_rep, n_reps, _dp(g)))
         return g
+
+    def set_gather_columns(self, cols=None):
+        """Row columns the sharded entry points gather (ob_panel_set_gather_columns); None = all."""
+        c = np.ascontiguousarray([] if cols is None else cols, dtype=np.int32)
+        N.check(N.lib().ob_panel_set_gather_columns(self._h, _ip(c), len(c)))
+
+    def component_columns(self):
+        """The row columns the aggregation reads: two-fold, three-fold, total gap, detailed."""
+        return list(range(6 + 2 * (self.k + self.n_base)))
+
+    def debug_shard_sim(self, world: int, self_rank: int, seed: int, first_rep: int, n_reps: int,
+                        ref=ReferenceCoefficients.GroupA):
+        """ob_debug_shard_sim: a `world`-rank sharded run simulated on this GPU, as rank
+        `self_rank` receives it."""
+        rows = np.empty((self.n_y, n_reps, self.row_len))
+        ok = np.zeros((self.n_y, n_reps), dtype=np.uint8)
+        if n_reps:
+            N.check(N.lib().ob_debug_shard_sim(self._h, world, self_rank, seed & ((1 << 64) - 1), first_rep, n_reps,
+                                               int(ref), _dp(rows), ok.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return (rows[0], ok[0]) if self.n_y == 1 else (rows, ok)
+
+    def debug_gram_exceptions(self):
+        """The i8 Gram's exception rows (ob_debug_gram_exceptions): (bits, [(group, row), ...])."""
+        bits, n = C.c_int32(0), C.c_int32(0)
+        buf = np.zeros(4096, dtype=np.uint32)
+        N.check(N.lib().ob_debug_gram_exceptions(self._h, C.byref(bits), C.byref(n),
+                                                 buf.ctypes.data_as(C.POINTER(C.c_uint32)), len(buf)))
+        ent = buf[: n.value]
+        return bits.value, [(int(e >> 31), int(e & 0x7FFFFFFF)) for e in ent]
 
     def sync(self):
         N.check(N.lib().ob_panel_sync(self._h))

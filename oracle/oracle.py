@@ -632,12 +632,18 @@ def empirical_quantile(v, q):  # quantile_decomposition.rs:164-171
     return float(v[min(int(len(v) * q), len(v) - 1)])
 
 
-def mm_single_pass(xa, ya, ca, xb, yb, cb, seed, rep, sims, quantiles):
+def mm_single_pass(xa, ya, ca, xb, yb, cb, seed, rep, sims, quantiles, fail_mask=None):
     """run_single_pass (quantile_decomposition.rs:173-279) on count-weighted groups; returns the
-    row [gap, characteristics, coefficients] per target quantile."""
+    row [gap, characteristics, coefficients] per target quantile. fail_mask[g][s] bit (rep & 7)
+    drops fit (g, s) as a failed solve_qr (Err, :221-229) -- the engine's ob_debug_mm_fail."""
     taus = [mm_tau(seed, rep, s) for s in range(sims)]
-    ba = [b for b in (qr_exact(xa, ya, ca, t) for t in taus) if b is not None]
-    bb = [b for b in (qr_exact(xb, yb, cb, t) for t in taus) if b is not None]
+
+    def dropped(g, s):
+        return fail_mask is not None and s < len(fail_mask[g]) and (int(fail_mask[g][s]) >> (rep & 7)) & 1
+
+    # filter_map keeps the successful fits in simulation order, independently per group
+    ba = [b for s, b in enumerate(qr_exact(xa, ya, ca, t) for t in taus) if b is not None and not dropped(0, s)]
+    bb = [b for s, b in enumerate(qr_exact(xb, yb, cb, t) for t in taus) if b is not None and not dropped(1, s)]
     if len(ba) < sims // 2 or len(bb) < sims // 2:
         raise OracleError("NalgebraError", "Failed to estimate a sufficient number of quantile regressions.")
     num = min(len(ba), len(bb))

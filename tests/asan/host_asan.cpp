@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../include/oaxaca_boot.h"
+#include "../../oaxaca-blinder-rs_amd/csrc/ob_shard_layout.h"
 
 static int failures = 0;
 #define CHECK(c)                                                        \
@@ -132,11 +133,79 @@ static void no_gpu() {
   CHECK(rc == OB_E_HIP && ctx == nullptr);
 }
 
+// ob_shard_layout.h through a simulated all-gather: every rank computes its shard of fake rows
+// (a pure function of (outcome, replicate, column), like the engine's), packs the gathered
+// columns into an exactly-sized send block (ASan catches any offset past it), the blocks land
+// where ncclAllGather puts them, and each rank's delivery must give every replicate's gathered
+// columns, its own replicates' other columns, and NaN for the rest.
+static double fake(int t, uint64_t rep, int c) { return t * 1e6 + (double)rep * 16.0 + c; }
+
+static void shard_layout() {
+  const int rl = 7, ny = 3;
+  const std::vector<std::vector<int>> col_sets = {{0, 1, 2, 3, 4, 5, 6}, {0, 2, 5}};
+  const int worlds[] = {1, 2, 3, 8};
+  const uint64_t ns[] = {1, 2, 5, 37, 64, 1001};
+  for (const auto& cols : col_sets)
+    for (int world : worlds)
+      for (uint64_t n : ns) {
+        const uint64_t first = 11;
+        const int nc = (int)cols.size();
+        const ob_shard_range s0 = ob_shard_of(first, n, 0, world);
+        std::vector<double> recv(ob_recv_block_off(s0, world, ny, 0, nc));
+        std::vector<uint8_t> recv_ok(ob_recv_block_off(s0, world, ny, 0, 1));
+        uint64_t covered = 0;
+        for (int r = 0; r < world; ++r) {
+          const ob_shard_range s = ob_shard_of(first, n, r, world);
+          CHECK(s.per == s0.per && s.count <= s.per && s.lo == covered && s.first == first + s.lo);
+          covered += s.count;
+          std::vector<double> rows((size_t)ny * s.count * rl);
+          std::vector<uint8_t> ok((size_t)ny * s.count);
+          for (int t = 0; t < ny; ++t)
+            for (uint64_t i = 0; i < s.count; ++i) {
+              for (int c = 0; c < rl; ++c) rows.at(ob_shard_row_off(s, t, i, rl, c)) = fake(t, s.first + i, c);
+              ok.at(ob_shard_ok_off(s, t, i)) = (uint8_t)(1 + ((s.first + i) & 1));
+            }
+          std::vector<double> send((size_t)ny * ob_send_elems(s, nc));
+          std::vector<uint8_t> send_ok((size_t)ny * s.per);
+          for (int t = 0; t < ny; ++t)
+            for (uint64_t i = 0; i < s.per; ++i) {
+              for (int q = 0; q < nc; ++q)
+                send.at(ob_send_off(s, t, i, nc, q)) = i < s.count ? rows.at(ob_shard_row_off(s, t, i, rl, cols[q])) : 0.0;
+              send_ok.at(ob_send_ok_off(s, t, i)) = i < s.count ? ok.at(ob_shard_ok_off(s, t, i)) : 0;
+            }
+          for (int t = 0; t < ny; ++t) {  // ncclAllGather per outcome: rank r's block of t
+            std::memcpy(&recv.at(ob_recv_block_off(s, world, t, r, nc)), &send.at(ob_send_off(s, t, 0, nc, 0)),
+                        sizeof(double) * ob_send_elems(s, nc));
+            std::memcpy(&recv_ok.at(ob_recv_block_off(s, world, t, r, 1)), &send_ok.at(ob_send_ok_off(s, t, 0)), s.per);
+          }
+        }
+        CHECK(covered == n);
+        for (int me = 0; me < world; ++me) {
+          const ob_shard_range s = ob_shard_of(first, n, me, world);
+          for (int t = 0; t < ny; ++t)
+            for (uint64_t j = 0; j < n; ++j) {
+              CHECK(recv_ok.at(ob_recv_ok_off(s, world, t, j)) == (uint8_t)(1 + ((first + j) & 1)));
+              for (int c = 0; c < rl; ++c) {
+                int q = -1;
+                for (int k = 0; k < nc; ++k)
+                  if (cols[k] == c) q = k;
+                const bool own = j >= s.lo && j < s.lo + s.count;
+                const double want = fake(t, first + j, c);
+                if (q >= 0) CHECK(recv.at(ob_recv_off(s, world, t, j, nc, q)) == want);
+                else if (own) CHECK(ob_shard_row_off(s, t, j - s.lo, rl, c) < (size_t)ny * s.count * rl);
+                CHECK(ob_deliver_off(n, t, j, rl, c) < (size_t)ny * n * rl);
+              }
+            }
+        }
+      }
+}
+
 int main(int argc, char** argv) {
   const char* dir = argc > 1 ? argv[1] : "/tmp";
   csv_and_frames(dir);
   inference();
   no_gpu();
+  shard_layout();
   std::printf("host_asan: %s (%d failed checks)\n", failures ? "FAIL" : "ok", failures);
   return failures ? 1 : 0;
 }

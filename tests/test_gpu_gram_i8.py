@@ -1,10 +1,14 @@
 """The exact integer-sliced Gram (ob_gram_i8.hip) against the f64 MFMA Gram (ob_gram_kernel).
 
 Both compute G_r = sum_i c_ri v_i v_i^T (v = sqrt(w) [1, x, y], ols.rs:68-78) for the same
-OBRS-1 counts. The i8 path's only approximation is the 56-bit fixed-point split of each pair
-product relative to its chunk's power of two (2^-57 of the chunk's largest |P| per row), so the
-two Grams must agree to 1e-12 of the natural scale sqrt(G_aa G_bb) of every entry; and the rows
-the engine returns (default path: i8) must equal the f64 path's rows to 1e-9 relative.
+OBRS-1 counts. The i8 path's only approximation is the 54-bit fixed-point split of each pair
+product relative to its chunk's power of two (rounding <= 2^-55 of the chunk's largest regular
+|P| per row); rows whose magnitude dwarfs their chunk's ("exception rows": some |v_c| >= 2^B x
+the chunk's geometric-mean scale of column c, or non-finite) are summed in f64 instead
+(DESIGN.md §5.0). So the two Grams must agree to 1e-12 of the natural scale sqrt(G_aa G_bb) of
+every entry -- also for replicates that miss a 1e8x sentinel row -- and the rows the engine
+returns (default path: i8) must equal the f64 path's rows to 1e-9 relative and the oracle's
+(builder.rs:816-839 over gathered rows) to 1e-6.
 """
 import os
 
@@ -81,3 +85,174 @@ def test_i8_rows_equal_f64_rows(ob, O):
             assert np.all(np.abs(r8 - r64) <= 1e-9 * np.maximum(np.abs(r64), gap)), ref
     finally:
         panel.close()
+
+
+# ---- exception rows: sentinels, heavy tails, non-finite values ---------------------------------
+def _chunks(na, nb):
+    """ob_engine.hip make_plan: ~64 balanced chunks of whole 256-row tiles per panel."""
+    out = []
+    ta, tb = -(-na // 256), -(-nb // 256)
+    tt = ta + tb
+    for g, tg in ((0, ta), (1, tb)):
+        if tg == 0:
+            continue
+        want = max(1, (64 * tg + tt // 2) // max(tt, 1))
+        nc = min(tg, max(want, -(-tg // 4096)))
+        out += [(g, tg * c // nc, tg * (c + 1) // nc) for c in range(nc)]
+    return out
+
+
+def _exception_rule(xa, ya, wa, xb, yb, wb, bits_min=8, cap=4096):
+    """numpy restatement of oz_scale/oz_dev/oz_choose/oz_collect (ob_gram_i8.hip): per (chunk,
+    column) s_c = floor(mean frexp exponent of the nonzero finite v_c + 0.5); per row d = max_c
+    min(ex - s_c, 126) (127 if some v_c is not finite); B = the smallest bits >= 8 leaving <= 4096
+    rows with d > B. Returns (B, sorted [(group, row)])."""
+    def vmat(x, y, w):
+        one = np.ones((x.shape[0], 1))
+        v = np.hstack([one, x, y.reshape(len(y), -1)])
+        return v * np.sqrt(w)[:, None] if w is not None else v
+    vs = [vmat(xa, ya, wa), vmat(xb, yb, wb)]
+    devs = [np.full(v.shape[0], -128, dtype=np.int64) for v in vs]
+    for g, t0, t1 in _chunks(len(ya), len(yb)):
+        v = vs[g][t0 * 256: t1 * 256]
+        with np.errstate(invalid="ignore"):
+            ex = np.frexp(np.where(np.isfinite(v), v, 0.0))[1].astype(np.int64)
+        nz = (v != 0) & np.isfinite(v)
+        s = np.where(nz.any(0), np.floor(np.where(nz, ex, 0).sum(0) / np.maximum(nz.sum(0), 1) + 0.5), 0)
+        dev = np.where(nz, np.minimum(ex - s.astype(np.int64), 126), -128).max(1)
+        dev = np.where((~np.isfinite(v)).any(1), 127, np.maximum(dev, -128))
+        devs[g][t0 * 256: t1 * 256] = dev
+    allv = np.concatenate(devs)
+    b = bits_min
+    while (allv > b).sum() > cap and b < 126:
+        b += 1
+    return b, [(g, int(r)) for g in (0, 1) for r in np.nonzero(devs[g] > b)[0]]
+
+
+def _sentinel_panel(O, n, p, seed):
+    d = O.synthetic_panel(n, p, True, seed=seed)
+    rng = np.random.default_rng(seed)
+    xa, xb, ya, yb = d["xa"].copy(), d["xb"].copy(), d["ya"].copy(), d["yb"].copy()
+    wa = np.exp(rng.normal(0.0, 1.0, len(ya)))  # log-normal survey weights
+    wb = np.exp(rng.normal(0.0, 1.0, len(yb)))
+    med = float(np.median(np.abs(xa[:, 1])))
+    for r, f in ((1000, 1e6), (1001, 1e7), (1002, 1e8)):  # three sentinels in one chunk of A
+        xa[r, 1] = f * med
+    xb[4000, 2] = 99_999_999.0  # a top-coded covariate in B
+    yb[9000] = 1e9              # and an outcome sentinel
+    return xa, ya, wa, xb, yb, wb
+
+
+def test_exception_rows_follow_the_rule(ob, O):
+    """The engine's exception list is exactly the numpy restatement of its rule."""
+    xa, ya, wa, xb, yb, wb = _sentinel_panel(O, 120_000, 6, 3)
+    panel = ob.Panel(xa, ya, xb, yb, wa, wb)
+    try:
+        panel.debug_gram(SEED, 0, 64, path=2)
+        bits, rows = panel.debug_gram_exceptions()
+        b_ref, rows_ref = _exception_rule(xa, ya, wa, xb, yb, wb)
+        assert bits == b_ref == 8 and rows == rows_ref, (bits, rows[:10], rows_ref[:10])
+        assert {(0, 1000), (0, 1001), (0, 1002), (1, 4000), (1, 9000)} <= set(rows)
+        assert panel.timing()["oz_exceptions"] == len(rows)
+    finally:
+        panel.close()
+
+
+def test_sentinels_gram_exact_for_replicates_missing_them(ob, O):
+    """Sentinel rows 1e6-1e8 x the median in one chunk, log-normal weights: the i8 Gram equals
+    the f64 Gram to 1e-12 of sqrt(G_aa G_bb) on every replicate -- including the ~37 % that do
+    not draw a given sentinel, where a chunk-wide exponent would lose up to 1e-5."""
+    xa, ya, wa, xb, yb, wb = _sentinel_panel(O, 200_000, 8, 5)
+    panel = ob.Panel(xa, ya, xb, yb, wa, wb)
+    try:
+        reps = 256
+        g64 = panel.debug_gram(SEED, 0, reps, path=1)
+        g8 = panel.debug_gram(SEED, 0, reps, path=2)
+        assert panel.timing()["gram_path"] == 2 and panel.timing()["oz_exceptions"] >= 5
+        worst = _check_gram(g8, g64, 8 + 2)
+        assert worst < 1e-12
+        na = len(ya)
+        drew = np.array([np.isin([1000, 1001, 1002], O.resample_indices(SEED, r, 0, na)) for r in range(reps)])
+        assert (~drew[:, 2]).sum() > 50 and (~drew.any(1)).sum() > 0  # replicates missing the 1e8 row, and all three
+    finally:
+        panel.close()
+
+
+@pytest.mark.parametrize("ref", [0, 2])
+def test_sentinels_rows_and_stats_match_oracle(ob, O, ref):
+    """Rows and SE / CI / p of every reported component vs the oracle's gathered-row algorithm
+    (builder.rs:816-839, ols.rs:68-89) over 256 replicates, 1e-6 mixed tolerance."""
+    xa, ya, wa, xb, yb, wb = _sentinel_panel(O, 200_000, 8, 5)
+    panel = ob.Panel(xa, ya, xb, yb, wa, wb)
+    try:
+        rows, ok = panel.boot(SEED, 0, 256, ref)
+        assert panel.timing()["gram_path"] == 2
+    finally:
+        panel.close()
+    cfg = O.PassConfig(9, 8, O.REF_FROM_ENUM[ref], True)
+    orows, ook = O.boot_ref(cfg, O.with_intercept(xa), ya, wa, O.with_intercept(xb), yb, wb, SEED, 0, 256,
+                            full=False)
+    assert np.array_equal(ok, ook)
+    gap = abs(float(np.nanmedian(orows[:, 5])))
+    m = ook.astype(bool)
+    scale = np.maximum(np.abs(orows[m]), gap)
+    assert np.all(np.abs(rows[m] - orows[m]) <= 1e-6 * scale)
+    st = ob.aggregate(rows, ok, np.arange(6 + 2 * 9, dtype=np.int32))
+    for j in range(6 + 2 * 9):
+        se, pv, (lo, hi) = O.bootstrap_stats(orows[m, j])
+        for got, want in ((st[j, 0], se), (st[j, 2], lo), (st[j, 3], hi)):
+            assert abs(got - want) <= 1e-6 * max(abs(want), gap), (j, got, want)
+        assert st[j, 1] == pv
+
+
+def test_heavy_tailed_covariate_matches_oracle(ob, O):
+    """A Pareto(1.2) income-like covariate (many rows far above the geometric mean: B rises only if
+    more than 4096 would be exceptions) and log-normal weights: rows vs the oracle at 1e-6."""
+    d = O.synthetic_panel(150_000, 5, True, seed=9)
+    rng = np.random.default_rng(9)
+    xa, xb = d["xa"].copy(), d["xb"].copy()
+    xa[:, 3] = rng.pareto(1.2, len(xa)) * 1e4 + 1e3
+    xb[:, 3] = rng.pareto(1.2, len(xb)) * 1e4 + 1e3
+    wa, wb = np.exp(rng.normal(0, 1.5, len(xa))), np.exp(rng.normal(0, 1.5, len(xb)))
+    panel = ob.Panel(xa, d["ya"], xb, d["yb"], wa, wb)
+    try:
+        rows, ok = panel.boot(SEED, 0, 128, 0)
+        bits, exc = panel.debug_gram_exceptions()
+        assert (bits, exc) == _exception_rule(xa, d["ya"], wa, xb, d["yb"], wb)
+    finally:
+        panel.close()
+    cfg = O.PassConfig(6, 5, 0, True)
+    orows, ook = O.boot_ref(cfg, O.with_intercept(xa), d["ya"], wa, O.with_intercept(xb), d["yb"], wb, SEED, 0, 128,
+                            full=False)
+    assert np.array_equal(ok, ook) and ok.all()
+    gap = abs(float(np.median(orows[:, 5])))
+    assert np.all(np.abs(rows - orows) <= 1e-6 * np.maximum(np.abs(orows), gap))
+
+
+def test_nonfinite_rows_touch_only_replicates_that_draw_them(ob, O):
+    """NaN in a predictor of one row of A and inf in the outcome of one row of B (strtod lets both
+    through the CSV reader): exception rows, so a replicate that does not draw them is finite and
+    equal to the oracle's gathered-row result, and one that does gets the reference's NaN / failed
+    Cholesky (ok = 0 iff a pivot is NaN, ob_oracle.c orc_cholesky)."""
+    d = O.synthetic_panel(20_000, 4, True, seed=12)
+    xa, yb = d["xa"].copy(), d["yb"].copy()
+    xa[777, 2] = np.nan
+    yb[4321] = np.inf
+    panel = ob.Panel(xa, d["ya"], d["xb"], yb, d["wa"], d["wb"])
+    try:
+        rows, ok = panel.boot(SEED, 0, 200, 0)
+        bits, exc = panel.debug_gram_exceptions()
+        assert (0, 777) in exc and (1, 4321) in exc
+    finally:
+        panel.close()
+    cfg = O.PassConfig(5, 4, 0, True)
+    orows, ook = O.boot_ref(cfg, O.with_intercept(xa), d["ya"], d["wa"], O.with_intercept(d["xb"]), yb, d["wb"],
+                            SEED, 0, 200, full=False)
+    assert np.array_equal(ok, ook)
+    drew_a = np.array([777 in set(O.resample_indices(SEED, r, 0, len(xa))) for r in range(200)])
+    assert drew_a.any() and (~drew_a).any()
+    assert not ok[drew_a].any()  # a NaN pivot fails the Cholesky, as in the reference
+    fin = np.isfinite(orows)
+    assert np.array_equal(fin, np.isfinite(rows))
+    gap = abs(float(np.nanmedian(orows[:, 5])))
+    assert np.all(np.abs(rows[fin] - orows[fin]) <= 1e-6 * np.maximum(np.abs(orows[fin]), gap))

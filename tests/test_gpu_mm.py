@@ -26,16 +26,36 @@ def mm_data(n, p, seed):
     return out
 
 
-def oracle_rows(O, d, sims, qs, reps):
+def oracle_rows(O, d, sims, qs, reps, fail_mask=None):
+    """Point pass then replicates 0..reps-1; a pass the reference would fail (:231-236) is a NaN row
+    with ok = 0, as the engine reports it."""
     xa, xb = O.with_intercept(d["xa"]), O.with_intercept(d["xb"])
     na, nb = len(d["ya"]), len(d["yb"])
-    rows = [O.mm_single_pass(xa, d["ya"], np.ones(na, np.int64), xb, d["yb"], np.ones(nb, np.int64), SEED,
-                             O.MM_POINT_REP, sims, qs)]
+    counts = [(np.ones(na, np.int64), np.ones(nb, np.int64), O.MM_POINT_REP)]
     for r in range(reps):
-        ca = np.bincount(O.resample_indices(SEED, r, 0, na), minlength=na)
-        cb = np.bincount(O.resample_indices(SEED, r, 1, nb), minlength=nb)
-        rows.append(O.mm_single_pass(xa, d["ya"], ca, xb, d["yb"], cb, SEED, r, sims, qs))
-    return np.array(rows)
+        counts.append((np.bincount(O.resample_indices(SEED, r, 0, na), minlength=na),
+                       np.bincount(O.resample_indices(SEED, r, 1, nb), minlength=nb), r))
+    rows, ok = [], []
+    for ca, cb, rep in counts:
+        try:
+            rows.append(O.mm_single_pass(xa, d["ya"], ca, xb, d["yb"], cb, SEED, rep, sims, qs, fail_mask))
+            ok.append(1)
+        except O.OracleError:
+            rows.append(np.full(3 * len(qs), np.nan))
+            ok.append(0)
+    return (np.array(rows), np.array(ok, np.uint8)) if fail_mask is not None else np.array(rows)
+
+
+def close_mm(rows, want, n_q):
+    """Mixed per-quantity tolerance: |d| <= 1e-6 max(|want|, |gap of that pass at that quantile|)
+    for the gap, characteristics and coefficients effects of every pass and quantile."""
+    r = np.asarray(rows, float).reshape(len(rows), n_q, 3)
+    w = np.asarray(want, float).reshape(len(want), n_q, 3)
+    scale = np.maximum(np.abs(w), np.abs(w[..., :1]))
+    err = np.abs(r - w)
+    nan_ok = np.isnan(r) & np.isnan(w)
+    bad = ~(err <= RTOL * scale) & ~nan_ok
+    return not bad.any(), float(np.nanmax(np.where(nan_ok, 0.0, err / np.maximum(scale, 1e-300))))
 
 
 @pytest.mark.parametrize("n,p,sims", [(600, 1, 30), (1500, 3, 40), (3000, 5, 24), (5000, 15, 12),
@@ -49,7 +69,7 @@ def test_mm_rows_match_oracle(ob, O, n, p, sims):
         panel.close()
     want = oracle_rows(O, d, sims, QS, 3)
     assert ok.all()
-    good, worst = close(rows, want, np.abs(want).max())
+    good, worst = close_mm(rows, want, len(QS))
     assert good, worst
 
 
@@ -176,7 +196,7 @@ def test_mm_row_reduction_matches_oracle(ob, O, reduce_env, n, p, sims):
     assert t["mm_reduced"] == 1
     want = oracle_rows(O, d, sims, QS, 3)
     assert ok.all()
-    good, worst = close(rows, want, np.abs(want).max())
+    good, worst = close_mm(rows, want, len(QS))
     assert good, worst
 
 
@@ -198,3 +218,53 @@ def test_mm_row_reduction_equals_full_solve(ob, reduce_env):
     assert k1.all() and k0.all()
     assert np.allclose(r1, r0, rtol=0, atol=1e-8 * np.abs(r0).max()), np.abs(r1 - r0).max()
     assert t1["mm_fit_rows"] < t0["mm_fit_rows"], (t1["mm_fit_rows"], t0["mm_fit_rows"])
+
+
+def test_mm_failed_fits_pair_by_index_and_sims_half_rule(ob, O):
+    """The reference drops a failed solve_qr per group independently (filter_map, :221-229), pairs
+    the survivors by index (:238-258) and fails a pass with fewer than simulations / 2 survivors
+    in a group (:231-236). Forced failures (ob_debug_mm_fail), the oracle applying the same rules:
+    * every pass: A loses simulations 2, 5, 11 (A's betas shift against B's);
+    * replicate 1: B also loses simulation 7;
+    * replicate 2: A loses 8 more (11 of 20 fail, 9 survivors < 10): the pass fails;
+    * replicate 3: A loses 7 more (exactly 10 = sims / 2 survivors): the pass holds."""
+    d = mm_data(1500, 3, seed=5)
+    sims = 20
+    mask = np.zeros((2, sims), np.uint8)
+    mask[0, [2, 5, 11]] = 0xFF
+    mask[1, 7] |= 1 << 1
+    mask[0, 12:20] |= 1 << 2
+    mask[0, 12:19] |= 1 << 3
+    panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"])
+    try:
+        panel.debug_mm_fail(mask)
+        rows, ok = panel.mm(SEED, sims, QS, 0, 4)
+        panel.debug_mm_fail(None)
+        clean, _ = panel.mm(SEED, sims, QS, 0, 4)
+    finally:
+        panel.close()
+    want, wok = oracle_rows(O, d, sims, QS, 4, fail_mask=mask)
+    assert list(ok) == list(wok) == [1, 1, 1, 0, 1]
+    good, worst = close_mm(rows, want, len(QS))
+    assert good, worst
+    assert np.isnan(rows[3]).all()
+    assert not np.allclose(rows[1], clean[1])  # the shifted pairing changes the pass
+
+
+def test_mm_point_pass_failure(ob, O, N):
+    """More than half of group B's point-pass fits failing fails the point pass (ok = 0, NaN row),
+    which QuantileDecompositionBuilder::run reports as NalgebraError (:231-236, ob_builder.cpp)."""
+    d = mm_data(1200, 2, seed=6)
+    sims = 16
+    mask = np.zeros((2, sims), np.uint8)
+    mask[1, :9] = 1 << 7  # the point pass (rep 2^32 - 1): 9 of 16 fail, 7 < 8 survive
+    panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"])
+    try:
+        panel.debug_mm_fail(mask)
+        rows, ok = panel.mm(SEED, sims, QS, 0, 2)
+    finally:
+        panel.close()
+    want, wok = oracle_rows(O, d, sims, QS, 2, fail_mask=mask)
+    assert list(ok) == list(wok) == [0, 1, 1]
+    good, worst = close_mm(rows, want, len(QS))
+    assert good, worst

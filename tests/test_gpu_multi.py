@@ -151,6 +151,87 @@ def test_boot_multi_one_device(ob, O, N):
     assert e.value.code == N.OB_E_INVALID
 
 
+@pytest.mark.parametrize("n_y", [1, 3])
+def test_shard_sim_world_gt1_bitwise(ob, O, n_y):
+    """ob_shard.cpp's world > 1 arithmetic (ob_shard_layout.h: short and empty tail shards, padded
+    per-rank blocks, outcome-major n_y blocks sent at t * per and received at t * W * per) run on
+    one GPU with the all-gather's placement simulated: every rank's delivered rows equal
+    ob_boot_run bit for bit, for W in {2, 3, 8}, n % W != 0 and n < W."""
+    d = O.synthetic_panel(5000, 4, True, seed=21)
+    ya, yb = d["ya"], d["yb"]
+    if n_y == 3:
+        ya = np.column_stack([ya, ob.rif(ya, 0.1), ob.rif(ya, 0.9)])
+        yb = np.column_stack([yb, ob.rif(yb, 0.1), ob.rif(yb, 0.9)])
+    panel = ob.Panel(d["xa"], ya, d["xb"], yb, d["wa"], d["wb"], device=0)
+    try:
+        for world, first, n in ((2, 3, 37), (3, 0, 10), (8, 11, 5), (8, 0, 1001), (3, 7, 2)):
+            a_rows, a_ok = panel.boot(SEED, first, n, 2)
+            for me in sorted({0, world - 1, world // 2}):
+                rows, ok = panel.debug_shard_sim(world, me, SEED, first, n, 2)
+                assert np.array_equal(ok, a_ok) and np.array_equal(rows, a_rows), (world, n, me)
+    finally:
+        panel.close()
+
+
+def test_shard_sim_component_gather(ob, O):
+    """With the gather narrowed to the aggregation's columns (48 of 153 at K = 21 in the bench):
+    those columns equal ob_boot_run for every replicate; the others hold this rank's own
+    replicates and NaN for the rest; aggregation over the delivered rows is unchanged."""
+    d = O.synthetic_panel(6000, 6, True, seed=22)
+    panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"], d["wa"], d["wb"], device=0)
+    try:
+        cols = panel.component_columns()
+        assert len(cols) == 6 + 2 * 7
+        n, world = 203, 4
+        a_rows, a_ok = panel.boot(SEED, 0, n, 0)
+        panel.set_gather_columns(cols)
+        per = -(-n // world)
+        for me in (0, 3):
+            rows, ok = panel.debug_shard_sim(world, me, SEED, 0, n, 0)
+            assert np.array_equal(ok, a_ok) and np.array_equal(rows[:, cols], a_rows[:, cols])
+            rest = [c for c in range(panel.row_len) if c not in cols]
+            mine = np.zeros(n, bool)
+            mine[me * per: min(n, (me + 1) * per)] = True
+            assert np.array_equal(rows[mine][:, rest], a_rows[mine][:, rest])
+            assert np.isnan(rows[~mine][:, rest]).all()
+            c32 = np.asarray(cols, dtype=np.int32)
+            assert np.array_equal(ob.aggregate(rows, ok, c32), ob.aggregate(a_rows, a_ok, c32))
+        panel.set_gather_columns(None)
+        rows, ok = panel.debug_shard_sim(world, 1, SEED, 0, n, 0)
+        assert np.array_equal(rows, a_rows)
+    finally:
+        panel.close()
+
+
+def test_boot_device_returns_before_the_work_finishes(ob, O):
+    """ob_boot_run_device only enqueues (no host synchronization once the panel's chunk table and
+    digit images exist): right after the call the caller's stream still has the work pending."""
+    import time
+
+    import torch
+
+    d = O.synthetic_panel(1_000_000, 20, True)
+    panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"], d["wa"], d["wb"], device=0)
+    try:
+        n = 10_000
+        rows = torch.empty((n, panel.row_len), dtype=torch.float64, device="cuda:0")
+        ok = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+        stream = torch.cuda.current_stream(0)
+        panel.boot_device(SEED, 0, n, rows.data_ptr(), ok.data_ptr(), 0, stream=stream.cuda_stream)
+        panel.sync()  # first call: builds the digit images
+        t0 = time.perf_counter()
+        panel.boot_device(SEED, n, n, rows.data_ptr(), ok.data_ptr(), 0, stream=stream.cuda_stream)
+        t_call = time.perf_counter() - t0
+        pending = not stream.query()
+        panel.sync()
+        t_all = time.perf_counter() - t0
+        assert pending and t_call < 0.5 * t_all, (t_call, t_all)
+        r_host, ok_host = panel.boot(SEED, n, 64, 0)
+        assert np.array_equal(rows[:64].cpu().numpy(), r_host)
+    finally:
+        panel.close()
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
