@@ -36,7 +36,8 @@ extern "C" {
 #define OB_E_HIP 7           /* HIP runtime failure / no GPU: the engine never falls back to the CPU */
 #define OB_E_INVALID 8       /* bad argument */
 #define OB_E_UNSUPPORTED 9   /* outside the engine's scope (Heckman selection, sizes over limits) */
-#define OB_E_OVERFLOW 10     /* a resample count exceeded 255 in one row (probability < 1e-500) */
+#define OB_E_OVERFLOW 10     /* a resample count exceeded the Gram's range in one row: 127 on the default i8
+                                path (probability ~1e-215 per row and replicate), 255 on the f64 path */
 #define OB_E_RCCL 11         /* RCCL missing or a collective failed (multi-GPU entry points) */
 
 const char* ob_last_error(void);

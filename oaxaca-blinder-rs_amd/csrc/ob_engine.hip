@@ -23,6 +23,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <vector>
 
 #include "ob_device.hpp"
@@ -111,12 +113,21 @@ __host__ __device__ inline uint32_t l1_lds_words(uint32_t ntiles) {
 
 __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t n1, uint32_t tiles0,
                                                            uint32_t first_rep, uint32_t stride,
-                                                           uint32_t key0, uint32_t key1, uint32_t* m1) {
+                                                           uint32_t key0, uint32_t key1, uint32_t* m1,
+                                                           const ob_ky_tables ky_g) {
   extern __shared__ __attribute__((aligned(16))) uint32_t l1s[];
   __shared__ uint32_t s_rej, s_tail, s_acc;
+  constexpr int kKy = OB_KY_MAX_LOG - OB_KY_MIN_LOG + 1;
+  __shared__ uint32_t ky_hot[kKy][OB_KY_HOT + 1];  // the Knuth-Yao tables' first columns
   const uint32_t g = blockIdx.y, rl = blockIdx.x, rep = first_rep + rl, tid = threadIdx.x;
   const uint32_t n = g ? n1 : n0;
   if (n == 0) return;
+  for (uint32_t i = tid; i < kKy * (OB_KY_HOT + 1); i += kBlock) {
+    const uint32_t t = i / (OB_KY_HOT + 1), c = i % (OB_KY_HOT + 1);
+    ky_hot[t][c] = ky_g.off[t][ky_g.i0[t] + c];
+  }
+  ob_ky_tables ky = ky_g;
+  for (int t = 0; t < kKy; ++t) ky.hot[t] = ky_hot[t];
   const uint32_t T = (n + OB_TILE_ROWS - 1) >> OB_TILE_SHIFT, D = l1_depth(T), J = l1_top_levels(T);
   const uint32_t tail = n - (T - 1) * OB_TILE_ROWS;
   const bool small = l1_small(T), partial = tail < OB_TILE_ROWS;
@@ -149,7 +160,7 @@ __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t
     auto level = [&](uint32_t l, uint32_t ll, uint32_t kb, uint32_t nodes, const uint32_t* cur, uint32_t* nxt) {
       const uint32_t span = 1u << (D - l - 1);  // tiles per child
       const uint32_t nnext = (T + span - 1) / span;
-      const uint32_t tag = OB_TAG_L1T + (round << 5) + l;
+      const uint32_t tag = OB_TAG_L1K + (round << 5) + l;
       if (ll < 8) {  // nodes <= 2^ll: 256 >> ll threads per node; never the large last level
         const uint32_t sh = 8 - ll, k = tid >> sh, j = tid & ((1u << sh) - 1);
         if (j == 0 && k < nodes) nxt[2 * k] = 0;
@@ -157,8 +168,9 @@ __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t
         if (k < nodes) {
           const uint32_t c = cur[k];
           uint32_t left = 0;
-          for (uint32_t q = j; 128 * q < c; q += 1u << sh)
-            left += ob_l1_split_bits(q, c, rep, ((kb + k) << 1) | g, tag, key0, key1);
+          const uint32_t ns = c ? ob_l1_streams(c) : 0u;
+          for (uint32_t q = j; q < ns; q += 1u << sh)
+            left += ob_l1_split_stream(q, c, rep, ((kb + k) << 1) | g, tag, key0, key1, ky);
           if (left) atomicAdd(&nxt[2 * k], left);
         }
         __syncthreads();
@@ -173,7 +185,8 @@ __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t
         for (uint32_t k = tid; k < nodes; k += kBlock) {
           const uint32_t c = cur[k], kg = kb + k;
           uint32_t left = 0;
-          for (uint32_t q = 0; 128 * q < c; ++q) left += ob_l1_split_bits(q, c, rep, (kg << 1) | g, tag, key0, key1);
+          const uint32_t ns = c ? ob_l1_streams(c) : 0u;
+          for (uint32_t q = 0; q < ns; ++q) left += ob_l1_split_stream(q, c, rep, (kg << 1) | g, tag, key0, key1, ky);
           const uint32_t right = c - left;
           if (to_m1) {
             emit(2 * kg, left);
@@ -979,6 +992,82 @@ __global__ __launch_bounds__(kBlock) void ob_residual_kernel(const double* cols,
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
+// Knuth-Yao tables of B(2^j, 1/2) for OBRS-2's level-1 split (ob_spec.h): W_k = C(2^j, k) exactly
+// (multi-limb integers, C(n, k + 1) = C(n, k) (n - k) / (k + 1)); column i = 1 .. n lists the k
+// with bit n - i of W_k set. Built once per process, uploaded once per device (~22 MB).
+struct KyHost {
+  std::vector<uint32_t> off[OB_KY_MAX_LOG - OB_KY_MIN_LOG + 1];
+  std::vector<uint16_t> list[OB_KY_MAX_LOG - OB_KY_MIN_LOG + 1];
+  uint32_t i0[OB_KY_MAX_LOG - OB_KY_MIN_LOG + 1] = {};
+};
+
+const KyHost& ky_host() {
+  static const KyHost h = [] {
+    KyHost t;
+    for (int j = OB_KY_MIN_LOG; j <= OB_KY_MAX_LOG; ++j) {
+      const uint32_t n = 1u << j, L = n / 64 + 1;
+      std::vector<uint64_t> w((size_t)(n + 1) * L, 0);
+      w[0] = 1;
+      for (uint32_t k = 0; k < n; ++k) {
+        const uint64_t* a = &w[(size_t)k * L];
+        uint64_t* b = &w[(size_t)(k + 1) * L];
+        unsigned __int128 carry = 0;
+        for (uint32_t i = 0; i < L; ++i) {
+          const unsigned __int128 v = (unsigned __int128)a[i] * (n - k) + carry;
+          b[i] = (uint64_t)v;
+          carry = v >> 64;
+        }
+        unsigned __int128 rem = 0;
+        for (uint32_t i = L; i-- > 0;) {
+          const unsigned __int128 v = (rem << 64) | b[i];
+          b[i] = (uint64_t)(v / (k + 1));
+          rem = v % (k + 1);
+        }
+      }
+      const int x = j - OB_KY_MIN_LOG;
+      std::vector<uint32_t>& off = t.off[x];
+      std::vector<uint16_t>& list = t.list[x];
+      off.assign(n + 2, 0);
+      t.i0[x] = 0;
+      for (uint32_t i = 1; i <= n; ++i) {
+        off[i] = (uint32_t)list.size();
+        const uint32_t bit = n - i;
+        for (uint32_t k = 0; k <= n; ++k)
+          if ((w[(size_t)k * L + bit / 64] >> (bit % 64)) & 1u) list.push_back((uint16_t)k);
+        if (!t.i0[x] && list.size() > off[i]) t.i0[x] = i;
+      }
+      off[n + 1] = (uint32_t)list.size();
+    }
+    return t;
+  }();
+  return h;
+}
+
+int ky_device(int device, ob_ky_tables* out) {
+  static std::mutex mu;
+  static std::map<int, ob_ky_tables> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache.find(device);
+  if (it == cache.end()) {
+    const KyHost& h = ky_host();
+    ob_ky_tables t{};
+    for (int x = 0; x <= OB_KY_MAX_LOG - OB_KY_MIN_LOG; ++x) {
+      uint32_t* off = nullptr;
+      uint16_t* list = nullptr;
+      HIP_OK(hipMalloc(&off, sizeof(uint32_t) * h.off[x].size()));
+      HIP_OK(hipMalloc(&list, sizeof(uint16_t) * h.list[x].size()));
+      HIP_OK(hipMemcpy(off, h.off[x].data(), sizeof(uint32_t) * h.off[x].size(), hipMemcpyHostToDevice));
+      HIP_OK(hipMemcpy(list, h.list[x].data(), sizeof(uint16_t) * h.list[x].size(), hipMemcpyHostToDevice));
+      t.off[x] = off;
+      t.list[x] = list;
+      t.i0[x] = h.i0[x];
+    }
+    it = cache.emplace(device, t).first;
+  }
+  *out = it->second;
+  return OB_OK;
+}
+
 struct Plan {
   uint32_t nb_rep, rep_pad, n_cg;
   int cb;
@@ -1338,8 +1427,10 @@ int engine_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_rep
   const uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
   const size_t lds_l1 = sizeof(uint32_t) * std::max(l1_lds_words(p->ntiles[0]), l1_lds_words(p->ntiles[1]));
   HIP_OK(hipFuncSetAttribute((const void*)ob_level1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_l1));
+  ob_ky_tables ky{};
+  OB_TRY(ky_device(p->ctx->device, &ky));
   hipLaunchKernelGGL(ob_level1_kernel, dim3(n_reps, 2), dim3(kBlock), lds_l1, s, p->n[0], p->n[1], p->ntiles[0],
-                     (uint32_t)first_rep, tiles, key0, key1, p->d_m1);
+                     (uint32_t)first_rep, tiles, key0, key1, p->d_m1, ky);
   HIP_OK(hipGetLastError());
   GramArgs ga = gram_args(p, pl);
   ga.m1 = p->d_m1;
@@ -1405,6 +1496,8 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   HIP_OK(hipMemsetAsync(p->d_flags, 0, sizeof(uint32_t), s));
 
   const size_t lds_l1 = sizeof(uint32_t) * std::max(l1_lds_words(p->ntiles[0]), l1_lds_words(p->ntiles[1]));
+  ob_ky_tables ky{};
+  OB_TRY(ky_device(ctx->device, &ky));
   HIP_OK(hipFuncSetAttribute((const void*)ob_level1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_l1));
   HIP_OK(hipFuncSetAttribute((const void*)ob_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)solve_lds_bytes(p)));
@@ -1429,7 +1522,7 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     const bool timed = true;
     if (timed) HIP_OK(hipEventRecord(ev[0], s));
     hipLaunchKernelGGL(ob_level1_kernel, dim3(ns, 2), dim3(kBlock), lds_l1, s, p->n[0], p->n[1], p->ntiles[0], frep,
-                       tiles, key0, key1, p->d_m1);
+                       tiles, key0, key1, p->d_m1, ky);
     HIP_OK(hipGetLastError());
     if (timed) HIP_OK(hipEventRecord(ev[1], s));
     GramArgs ga = gram_args(p, plx);

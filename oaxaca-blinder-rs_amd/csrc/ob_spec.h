@@ -1,24 +1,26 @@
-// ob_spec.h -- the OBRS-1 resample stream and the per-replicate row layout, shared by the HIP
+// ob_spec.h -- the OBRS-2 resample stream and the per-replicate row layout, shared by the HIP
 // kernels (device) and the host runtime. DESIGN.md §3 is the normative description.
 //
 // The reference resamples each group with polars `sample_n_literal(n_g, with_replacement=true,
 // shuffle=false, seed=None)` (oaxaca_blinder/src/builder.rs:822-827): n_g i.i.d. uniform row
-// draws per group, unseeded. OBRS-1 produces the same distribution (an exact multinomial with
+// draws per group, unseeded. OBRS-2 produces the same distribution (an exact multinomial with
 // cell probability 1/n_g) from a counter-based stream so that replicate r is reproducible from
 // (seed, r) alone on any GPU count:
-//   level 1: the tile counts m_j of n_g uniform row draws, by fair-bit splitting (no per-draw
-//            index): over the dyadic tree of 2^D >= T tiles a node holding c draws sends
-//            popcount(first c bits of its stream) left and the rest right
-//            (ob_l1_split_bits); children past the last tile and draws a partial last tile
-//            rejects (byte >= its rows) are drawn again in further rounds, the last <= 256 by
-//            Lemire's multiply-and-reject over [0, n_g). DESIGN.md §3, oracle
-//            orc_level1_counts.
+//   level 1: the tile counts m_j of n_g uniform row draws, by binomial splitting (no per-draw
+//            index): over the dyadic tree of 2^D >= T tiles a node holding c draws sends an exact
+//            Binomial(c, 1/2) left and the rest right (ob_l1_split_stream: Knuth-Yao samples of
+//            B(2^j, 1/2) over the binary digits of c, OBRS-1's popcount of c fair bits for the
+//            low 7); children past the last tile and draws a partial last tile rejects (byte >=
+//            its rows) are drawn again in further rounds, the last <= 256 by Lemire's
+//            multiply-and-reject over [0, n_g). DESIGN.md §3, oracle orc_level1_counts.
 //   level 2: m_j draws inside tile j (S_j rows). Full tiles (S_j = OB_TILE_ROWS = 2^8): Philox
 //            call p yields draws 16p..16p+15, draw 16p + 4i + b = byte b (LSB first) of output
 //            word i (exactly uniform, independent). The partial last tile: call p yields draws
 //            2p, 2p+1, local = mulhi64(u64, S_j) of words (x,y) and (z,w).
 // Conditional on the tile counts the level-2 draws are i.i.d. uniform in their tile, so the
 // joint law of per-row counts equals that of n_g i.i.d. uniform draws over the group.
+// (OBRS-1, rounds 1-2, split a level-1 node by the popcount of c fair bits: ~5.5M bits per group
+// and replicate at 500k rows against ~0.5M for OBRS-2; its level 2 is unchanged.)
 #pragma once
 #include <stdint.h>
 
@@ -30,7 +32,7 @@
 
 #define OB_TILE_ROWS 256u
 #define OB_TILE_SHIFT 8u
-#define OB_TAG_L1T 0x4C310000u /* "L1" + (round << 5) + level: split bits of node k, {q, rep, 2k | g} */
+#define OB_TAG_L1K 0x4B310000u /* "K1" + (round << 5) + level: split streams of node k, {q << 12 | call, rep, 2k | g} */
 #define OB_TAG_L1S 0x4C530000u /* "LS" + round: partial-tile acceptance bytes, {q, rep, g} */
 #define OB_TAG_L1D 0x4C440000u /* "LD" + (j >> 2): direct draw r, attempt j, {r, rep, g} */
 #define OB_L1_DIRECT 256u      /* rejected draws at most this many are drawn directly */
@@ -89,19 +91,107 @@ OB_HD ob_u32x4 ob_philox_x3(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, 
   return o;
 }
 
-// Fair bits [128 q, min(c, 128 q + 128)) of a level-1 node stream, counted: bit b of the stream
-// is bit (b & 31) of word ((b >> 5) & 3) of Philox({b >> 7, rep, c2, tag}).
-OB_HD uint32_t ob_l1_split_bits(uint32_t q, uint32_t c, uint32_t rep, uint32_t c2, uint32_t tag, uint32_t k0,
-                                uint32_t k1) {
-  const ob_u32x4 u = ob_philox(q, rep, c2, tag, k0, k1);
-  const uint32_t r = c - 128u * q;
-  const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
-  uint32_t s = 0;
-  for (uint32_t i = 0; i < 4; ++i) {
-    const uint32_t nb = r > 32u * i ? r - 32u * i : 0u;
-    s += (uint32_t)__builtin_popcount(nb >= 32u ? wd[i] : (wd[i] & ((1u << nb) - 1u)));
+// ---- OBRS-2 level-1 split ---------------------------------------------------------------------
+// Binomial(c, 1/2) = the sum of exact B(2^j, 1/2) samples over the binary digits of c: c >> 12
+// samples of B(4096), one B(2^j) per set bit j = 11 .. 7, and the popcount of c & 127 fair bits.
+// B(n = 2^j) is a Knuth-Yao walk (discrete distribution generating tree) over the dyadic
+// probabilities p_k = C(n, k) / 2^n: column i = 1 .. n of the tree holds the k whose bit n - i of
+// C(n, k) is set, in ascending k (list[off[i] .. off[i+1])); the walk reads one stream bit per
+// column, d = 2 d + bit, returns the d-th entry when d < the column's count and subtracts the
+// count otherwise. Exact, ~H + 2 ~ 9 bits per sample. Streams: q < nb = ceil((c >> 12) / 8)
+// carries B(4096) samples 8q .. min(8q + 8, c >> 12) - 1, stream nb the B(2^j), j = 11 .. 7, then
+// the popcount bits; bit b of stream q is bit (b & 31) of word ((b >> 5) & 3) of
+// Philox({q << 12 | b >> 7, rep, c2, tag}). Tables: ob_ky_build (host), KyTables (device).
+#define OB_KY_MIN_LOG 7
+#define OB_KY_MAX_LOG 12
+#define OB_KY_HOT 32  // columns i0 .. i0 + 31 of each table, staged in LDS (a walk rarely goes deeper)
+
+struct ob_ky_tables {  // device pointers, per n = 2^j for j = OB_KY_MIN_LOG .. OB_KY_MAX_LOG
+  const uint32_t* off[OB_KY_MAX_LOG - OB_KY_MIN_LOG + 1];  // n + 2 entries
+  const uint16_t* list[OB_KY_MAX_LOG - OB_KY_MIN_LOG + 1];
+  uint32_t i0[OB_KY_MAX_LOG - OB_KY_MIN_LOG + 1];  // first column with an entry
+  const uint32_t* hot[OB_KY_MAX_LOG - OB_KY_MIN_LOG + 1];  // off[i0 .. i0 + OB_KY_HOT] (LDS), or null
+};
+
+OB_HD uint32_t ob_l1_streams(uint32_t c) { return (((c >> 12) + 7) >> 3) + 1; }
+
+struct ob_bitstream {
+  uint32_t ctr0, rep, c2, tag, k0, k1;
+  uint32_t pos;
+  uint32_t w[4];
+};
+
+OB_HD uint32_t ob_bs_word(ob_bitstream& s) {  // the 32-bit word holding bit s.pos (refilled per 128 bits)
+  if ((s.pos & 127u) == 0) {
+    const ob_u32x4 u = ob_philox(s.ctr0 | (s.pos >> 7), s.rep, s.c2, s.tag, s.k0, s.k1);
+    s.w[0] = u.x;
+    s.w[1] = u.y;
+    s.w[2] = u.z;
+    s.w[3] = u.w;
   }
-  return s;
+  const uint32_t q = (s.pos >> 5) & 3u;
+  return q == 0 ? s.w[0] : q == 1 ? s.w[1] : q == 2 ? s.w[2] : s.w[3];
+}
+
+OB_HD uint32_t ob_bs_bit(ob_bitstream& s) {
+  const uint32_t b = (ob_bs_word(s) >> (s.pos & 31u)) & 1u;
+  ++s.pos;
+  return b;
+}
+
+// The next m <= 32 stream bits as an integer, the first bit most significant (d = 2 d + bit, m times).
+OB_HD uint32_t ob_bs_take_msb(ob_bitstream& s, uint32_t m) {
+  uint32_t v = 0;
+  while (m) {
+    const uint32_t sh = s.pos & 31u, take = m < 32u - sh ? m : 32u - sh;
+    const uint32_t w = ob_bs_word(s) >> sh;
+    const uint32_t chunk = take == 32u ? w : (w & ((1u << take) - 1u));
+    const uint32_t rev = __builtin_bitreverse32(chunk) >> (32u - take);
+    v = take == 32u ? rev : ((v << take) | rev);
+    s.pos += take;
+    m -= take;
+  }
+  return v;
+}
+
+OB_HD uint32_t ob_ky_sample(ob_bitstream& s, const uint32_t* off, const uint16_t* list, uint32_t i0,
+                            const uint32_t* hot) {
+  uint32_t d = ob_bs_take_msb(s, i0 - 1u);  // columns 1 .. i0 - 1 hold no entries
+  for (uint32_t i = i0;; ++i) {
+    d = 2u * d + ob_bs_bit(s);
+    const uint32_t t = i - i0;
+    const uint32_t lo = (hot && t < OB_KY_HOT) ? hot[t] : off[i];
+    const uint32_t cnt = ((hot && t < OB_KY_HOT) ? hot[t + 1] : off[i + 1]) - lo;
+    if (d < cnt) return list[lo + d];
+    d -= cnt;
+  }
+}
+
+// Stream q's part of node c's split (the node's left count is the sum over q < ob_l1_streams(c)).
+OB_HD uint32_t ob_l1_split_stream(uint32_t q, uint32_t c, uint32_t rep, uint32_t c2, uint32_t tag, uint32_t k0,
+                                  uint32_t k1, const ob_ky_tables& ky) {
+  const uint32_t c4 = c >> 12, nb = (c4 + 7u) >> 3;
+  ob_bitstream s = {q << 12, rep, c2, tag, k0, k1, 0u, {0u, 0u, 0u, 0u}};
+  uint32_t left = 0;
+  if (q < nb) {
+    const uint32_t s1 = 8u * q + 8u < c4 ? 8u * q + 8u : c4;
+    const int t = OB_KY_MAX_LOG - OB_KY_MIN_LOG;
+    for (uint32_t i = 8u * q; i < s1; ++i) left += ob_ky_sample(s, ky.off[t], ky.list[t], ky.i0[t], ky.hot[t]);
+  } else {
+    for (int j = OB_KY_MAX_LOG - 1; j >= OB_KY_MIN_LOG; --j)
+      if ((c >> j) & 1u) {
+        const int t = j - OB_KY_MIN_LOG;
+        left += ob_ky_sample(s, ky.off[t], ky.list[t], ky.i0[t], ky.hot[t]);
+      }
+    for (uint32_t m = c & 127u; m;) {  // popcount of the next m bits, word by word
+      const uint32_t sh = s.pos & 31u, take = m < 32u - sh ? m : 32u - sh;
+      const uint32_t w = ob_bs_word(s) >> sh;
+      left += (uint32_t)__builtin_popcount(take == 32u ? w : (w & ((1u << take) - 1u)));
+      s.pos += take;
+      m -= take;
+    }
+  }
+  return left;
 }
 
 // floor(u * s / 2^64), s < 2^32.

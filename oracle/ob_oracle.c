@@ -58,37 +58,138 @@ static inline uint64_t orc_draw_u64(const uint32_t w[4], int odd) {
     return odd ? (((uint64_t)w[3] << 32) | w[2]) : (((uint64_t)w[1] << 32) | w[0]);
 }
 
-/* Level 1 (OBRS-1): the tile counts m of n i.i.d. uniform row draws over [0, n),
- * drawn by fair-bit splitting instead of one index per draw. T = ceil(n / 256) tiles, D =
+/* Level 1 (OBRS-2): the tile counts m of n i.i.d. uniform row draws over [0, n),
+ * drawn by binomial splitting instead of one index per draw. T = ceil(n / 256) tiles, D =
  * ceil(log2 T); the dyadic tree over 2^D tiles (rows [0, 2^(D+8))) has node (l, k) = tiles
  * [k 2^(D-l), (k+1) 2^(D-l)). A round with c_0 draws at the root splits every node (l < D) with
- * count c into its left child L = popcount of bits [0, c) of the node's bit stream and its right
- * child c - L: bit b is bit (b & 31) of word ((b >> 5) & 3) of
- * Philox({b >> 7, rep, (k << 1) | g, ORC_TAG_L1T + (round << 5) + l}). A child starting at tile
- * >= T is padding: its draws are rejected. At the tiles, a partial last tile (S = n - 256 (T-1)
- * < 256 rows) accepts draw i iff byte (i & 3) of word ((i >> 2) & 3) of
+ * count c into its left child L ~ Binomial(c, 1/2) and its right child c - L (orc_split_left).
+ * A child starting at tile >= T is padding: its draws are rejected. At the tiles, a partial last
+ * tile (S = n - 256 (T-1) < 256 rows) accepts draw i iff byte (i & 3) of word ((i >> 2) & 3) of
  * Philox({i >> 4, rep, g, ORC_TAG_L1S + round}) is < S. Rejected draws R start the next round
  * while R > 256; the last R <= 256 are direct: draw r is Lemire's multiply-and-reject on word
- * (j & 3) of Philox({r, rep, g, ORC_TAG_L1D + (j >> 2)}), attempt j. Each fair split is a
- * Binomial(c, 1/2), so the accepted draws are i.i.d. uniform over the valid rows. */
-#define ORC_TAG_L1T 0x4C310000u /* "L1" + (round << 5) + level */
+ * (j & 3) of Philox({r, rep, g, ORC_TAG_L1D + (j >> 2)}), attempt j. Each split is an exact
+ * Binomial(c, 1/2), so the accepted draws are i.i.d. uniform over the valid rows.
+ *
+ * The split (OBRS-2; OBRS-1 drew c fair bits and counted them, ~5.5M bits per group per
+ * replicate at 500k rows): L = the sum of exact Binomial(2^j, 1/2) samples over the binary
+ * digits of c -- c >> 12 samples of B(4096), one B(2^j) for each set bit j = 11 .. 7, and the
+ * popcount of c & 127 fair bits. Each B(2^j) is a Knuth-Yao walk (discrete distribution
+ * generating tree) over the exact dyadic probabilities C(2^j, k) / 2^(2^j): ~9 random bits per
+ * sample instead of 2^j. Bits come from per-node streams: stream q of node (l, k) in round r has
+ * bit b = bit (b & 31) of word ((b >> 5) & 3) of Philox({(q << 12) | (b >> 7), rep, (k << 1) | g,
+ * ORC_TAG_L1K + (r << 5) + l}). Streams q < nb = ceil((c >> 12) / 8) carry B(4096) samples
+ * 8q .. min(8q + 8, c >> 12) - 1 in order; stream nb carries the B(2^j) for j = 11 down to 7,
+ * then the c & 127 popcount bits. */
+#define ORC_TAG_L1T 0x4C310000u /* OBRS-1 "L1" + (round << 5) + level (superseded) */
+#define ORC_TAG_L1K 0x4B310000u /* OBRS-2 "K1" + (round << 5) + level */
 #define ORC_TAG_L1S 0x4C530000u /* "LS" + round */
 #define ORC_TAG_L1D 0x4C440000u /* "LD" + (j >> 2) */
 #define ORC_L1_DIRECT 256u
 
+/* Knuth-Yao tables for B(n, 1/2), n = 2^j: W_k = C(n, k), p_k = W_k / 2^n; column i (1..n) of the
+ * DDG tree holds the k whose bit n - i of W_k is set, ascending: list[off[i] .. off[i+1]). */
+typedef struct {
+    uint32_t n;
+    uint32_t* off; /* n + 2 entries */
+    uint16_t* list;
+} orc_ky;
+static orc_ky orc_ky_tab[13];
+static pthread_once_t orc_ky_once = PTHREAD_ONCE_INIT;
+
+static void orc_ky_build(orc_ky* t, uint32_t n) {
+    const uint32_t L = n / 64 + 1;
+    uint64_t* w = (uint64_t*)calloc((size_t)(n + 1) * L, sizeof(uint64_t));
+    w[0] = 1;
+    for (uint32_t k = 0; k < n; ++k) { /* C(n, k+1) = C(n, k) (n - k) / (k + 1), exact */
+        const uint64_t* a = w + (size_t)k * L;
+        uint64_t* b = w + (size_t)(k + 1) * L;
+        unsigned __int128 carry = 0;
+        for (uint32_t i = 0; i < L; ++i) {
+            unsigned __int128 v = (unsigned __int128)a[i] * (n - k) + carry;
+            b[i] = (uint64_t)v;
+            carry = v >> 64;
+        }
+        unsigned __int128 rem = 0;
+        for (uint32_t i = L; i-- > 0;) {
+            unsigned __int128 v = (rem << 64) | b[i];
+            b[i] = (uint64_t)(v / (k + 1));
+            rem = v % (k + 1);
+        }
+    }
+    t->n = n;
+    t->off = (uint32_t*)calloc(n + 2, sizeof(uint32_t));
+    size_t total = 0;
+    for (uint32_t i = 1; i <= n; ++i) {
+        t->off[i] = (uint32_t)total;
+        const uint32_t bit = n - i;
+        for (uint32_t k = 0; k <= n; ++k) total += (w[(size_t)k * L + bit / 64] >> (bit % 64)) & 1u;
+    }
+    t->off[n + 1] = (uint32_t)total;
+    t->list = (uint16_t*)malloc(sizeof(uint16_t) * (total ? total : 1));
+    size_t pos = 0;
+    for (uint32_t i = 1; i <= n; ++i) {
+        const uint32_t bit = n - i;
+        for (uint32_t k = 0; k <= n; ++k)
+            if ((w[(size_t)k * L + bit / 64] >> (bit % 64)) & 1u) t->list[pos++] = (uint16_t)k;
+    }
+    free(w);
+}
+
+static void orc_ky_init(void) {
+    for (uint32_t j = 7; j <= 12; ++j) orc_ky_build(&orc_ky_tab[j], 1u << j);
+}
+
+typedef struct {
+    uint32_t ctr[4]; /* {(q << 12) | call, rep, c2, tag}; the call word is set per 128 bits */
+    const uint32_t* key;
+    uint64_t pos;
+    uint32_t w[4];
+} orc_bits;
+
+static uint32_t orc_bit(orc_bits* s) {
+    if ((s->pos & 127u) == 0) {
+        uint32_t ctr[4] = {s->ctr[0] | (uint32_t)(s->pos >> 7), s->ctr[1], s->ctr[2], s->ctr[3]};
+        orc_philox4x32_10(ctr, s->key, s->w);
+    }
+    const uint32_t b = (s->w[(s->pos >> 5) & 3u] >> (s->pos & 31u)) & 1u;
+    ++s->pos;
+    return b;
+}
+
+/* One B(2^j, 1/2) sample: the Knuth-Yao walk, one stream bit per tree level. */
+static uint32_t orc_ky_sample(orc_bits* s, const orc_ky* t) {
+    uint64_t d = 0;
+    for (uint32_t i = 1;; ++i) {
+        d = 2 * d + orc_bit(s);
+        const uint32_t cnt = t->off[i + 1] - t->off[i];
+        if (d < cnt) return t->list[t->off[i] + d];
+        d -= cnt;
+    }
+}
+
+/* Binomial(c, 1/2) for node k of level l, group g (OBRS-2, above). */
 static uint32_t orc_split_left(uint32_t c, uint32_t rep, uint32_t g, uint32_t k, uint32_t tag, const uint32_t key[2]) {
+    pthread_once(&orc_ky_once, orc_ky_init);
+    const uint32_t c4 = c >> 12, nb = (c4 + 7) / 8;
     uint32_t left = 0;
-    for (uint32_t q = 0; 128u * q < c; ++q) {
-        uint32_t ctr[4] = {q, rep, (k << 1) | g, tag}, w[4];
-        orc_philox4x32_10(ctr, key, w);
-        uint32_t r = c - 128u * q;
-        for (uint32_t i = 0; i < 4; ++i) {
-            uint32_t nb = r > 32u * i ? r - 32u * i : 0u;
-            uint32_t mask = nb >= 32u ? 0xFFFFFFFFu : ((1u << nb) - 1u);
-            left += (uint32_t)__builtin_popcount(w[i] & mask);
+    for (uint32_t q = 0; q <= nb; ++q) {
+        orc_bits s = {{q << 12, rep, (k << 1) | g, tag}, key, 0, {0, 0, 0, 0}};
+        if (q < nb) {
+            const uint32_t s1 = 8 * q + 8 < c4 ? 8 * q + 8 : c4;
+            for (uint32_t i = 8 * q; i < s1; ++i) left += orc_ky_sample(&s, &orc_ky_tab[12]);
+        } else {
+            for (uint32_t j = 11; j >= 7; --j)
+                if ((c >> j) & 1u) left += orc_ky_sample(&s, &orc_ky_tab[j]);
+            for (uint32_t i = 0; i < (c & 127u); ++i) left += orc_bit(&s);
         }
     }
     return left;
+}
+
+/* Test hook: one OBRS-2 split of c draws (node k of a level with tag `tag`). */
+uint32_t orc_binomial_half(uint32_t c, uint64_t seed, uint32_t rep, uint32_t g, uint32_t k, uint32_t tag) {
+    const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    return orc_split_left(c, rep, g, k, tag, key);
 }
 
 void orc_level1_counts(uint64_t seed, uint32_t rep, uint32_t g, uint32_t n, uint32_t* m) {
@@ -109,7 +210,7 @@ void orc_level1_counts(uint64_t seed, uint32_t rep, uint32_t g, uint32_t n, uint
             uint32_t span = 1u << (depth - l - 1); /* tiles per child */
             uint32_t nnext = (ntiles + span - 1) / span;
             for (uint32_t k = 0; k < nodes; ++k) {
-                uint32_t c = cur[k], left = c ? orc_split_left(c, rep, g, k, ORC_TAG_L1T + (round << 5) + l, key) : 0;
+                uint32_t c = cur[k], left = c ? orc_split_left(c, rep, g, k, ORC_TAG_L1K + (round << 5) + l, key) : 0;
                 nxt[2 * k] = left;
                 if (2 * k + 1 < nnext) nxt[2 * k + 1] = c - left;
                 else rejected += c - left;

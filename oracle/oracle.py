@@ -70,6 +70,8 @@ def lib():
         L.orc_single_pass.restype = C.c_int
         L.orc_boot_ref.argtypes = [C.POINTER(_Cfg), D, D, D, I64, D, D, D, I64, C.c_uint64, C.c_uint32,
                                    C.c_uint32, C.c_int, C.c_int, D, C.POINTER(C.c_uint8)]
+        L.orc_binomial_half.argtypes = [C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
+        L.orc_binomial_half.restype = C.c_uint32
         L.orc_bootstrap_stats.argtypes = [D, I64, D]
         L.orc_rif.argtypes = [D, I64, C.c_double, D]
         _lib = L
@@ -95,6 +97,11 @@ def level1_counts(seed, rep, g, n):
     m = np.zeros(max((n + 255) // 256, 1), dtype=np.uint32)
     lib().orc_level1_counts(seed & (2**64 - 1), rep, g, n, m.ctypes.data_as(C.POINTER(C.c_uint32)))
     return m[: (n + 255) // 256]
+
+
+def binomial_half(c, seed, rep, g=0, k=0, tag=0x4B310000):
+    """One OBRS-2 level-1 split of c draws (Knuth-Yao B(2^j, 1/2) samples + popcount bits)."""
+    return int(lib().orc_binomial_half(c, seed & (2**64 - 1), rep, g, k, tag))
 
 
 def resample_indices(seed, rep, g, n):

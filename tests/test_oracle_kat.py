@@ -201,8 +201,30 @@ def test_reference_groups_kat(O, mode):  # tests/features_test.rs:14-35 (Cotton,
     assert ob.run(threads=2)["total_gap"] > 0.0
 
 
+@pytest.mark.parametrize("c", [1, 100, 128, 129, 777, 4096, 4097, 9000, 70001, 500000])
+def test_obrs2_split_is_binomial(O, c):
+    """OBRS-2's level-1 split (Knuth-Yao B(2^j, 1/2) samples over the binary digits of c plus a
+    popcount of c & 127 bits): Binomial(c, 1/2) in law -- chi-square over central quantile bins,
+    mean and variance within 5 standard errors."""
+    from scipy import stats
+
+    n = 6000 if c < 100_000 else 2000
+    xs = np.array([O.binomial_half(c, 0xB17, r, 1, 5) for r in range(n)], dtype=float)
+    assert xs.min() >= 0 and xs.max() <= c
+    assert abs(xs.mean() - c / 2) < 5 * np.sqrt(c / 4 / n)
+    assert abs(xs.var() - c / 4) < 5 * (c / 4) * np.sqrt(2.0 / n) + 1e-9
+    if c >= 100:
+        edges = np.unique(np.round(stats.binom.ppf(np.linspace(0.002, 0.998, 21), c, 0.5)))
+        edges = np.concatenate([[-1.0], edges, [float(c)]])
+        obs = np.histogram(xs, bins=edges + 0.5)[0]
+        exp = np.diff(stats.binom.cdf(edges, c, 0.5)) * n
+        keep = exp > 5
+        chi2 = ((obs[keep] - exp[keep]) ** 2 / exp[keep]).sum()
+        assert stats.chi2.sf(chi2, keep.sum() - 1) > 1e-4, chi2
+
+
 def test_resample_is_multinomial(O):
-    """OBRS-1 draws: exact count n per replicate and a uniform per-row law (chi-square)."""
+    """OBRS-2 draws: exact count n per replicate and a uniform per-row law (chi-square)."""
     n = 1500
     tot = np.zeros(n)
     for rep in range(200):
@@ -214,13 +236,21 @@ def test_resample_is_multinomial(O):
     assert abs(chi2 - (n - 1)) < 6 * np.sqrt(2 * (n - 1))
     m = O.level1_counts(0xABC, 7, 0, 100_000)
     assert m.sum() == 100_000 and len(m) == (100_000 + 255) // 256
-    # the fair-bit tree's shape edges: one tile, exact powers of two, 257 tiles with a 1-row tail
+    # the binomial tree's shape edges: one tile, exact powers of two, 257 tiles with a 1-row tail
     for n in (1, 3, 255, 256, 257, 512, 65536, 65537, 131372):
         for rep in range(3):
             m = O.level1_counts(0x5EED, rep, 1, n)
             assert m.sum() == n and len(m) == (n + 255) // 256
     tail = np.array([O.level1_counts(0x5EED, rep, 0, 257)[-1] for rep in range(400)])
     assert abs(tail.mean() - 1.0) < 0.25  # a 1-row tail tile: E m = 257 / 257
+    # tile counts of a 2M-row group (splits of ~2M, 1M, ... draws): each ~ Binomial(n, 1/T)
+    n, reps = 2_000_003, 40
+    ms = np.array([O.level1_counts(0x5EED, rep, 0, n) for rep in range(reps)], dtype=float)
+    t = ms.shape[1]
+    p = np.full(t, 256.0 / n)
+    p[-1] = (n - 256 * (t - 1)) / n
+    z = (ms.sum(0) - reps * n * p) / np.sqrt(reps * n * p * (1 - p))
+    assert abs(z.mean()) < 6 / np.sqrt(t) and abs(z.var() - 1.0) < 0.1
 
 
 # --- Heckman two-step (heckman.rs, estimation.rs:114-260, math/probit.rs) ---------------------

@@ -14,4 +14,12 @@ tail -5 "gpurun_out/${TAG}_tests.log"
 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > "gpurun_out/${TAG}_bench.json" 2> "gpurun_out/${TAG}_bench.err"
 rc=$?
 tail -c 3000 "gpurun_out/${TAG}_bench.json"
+[ $rc -ne 0 ] && exit $rc
+if [ -n "${AB:-}" ] && [ -f oaxaca-blinder-rs_amd/liboaxaca_boot_alt.so ]; then  # A/B: the alternative build
+  OB_LIB_PATH=$PWD/oaxaca-blinder-rs_amd/liboaxaca_boot_alt.so timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 \
+    --cpu-seconds 0 --no-e2e > "gpurun_out/${TAG}_bench_alt.json" 2> "gpurun_out/${TAG}_bench_alt.err"
+  rc=$?
+  timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --cpu-seconds 0 --no-e2e > "gpurun_out/${TAG}_bench_b.json" \
+    2> "gpurun_out/${TAG}_bench_b.err" || exit $?
+fi
 exit $rc

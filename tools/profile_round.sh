@@ -14,14 +14,14 @@ if [ -z "${SKIP_BENCH:-}" ]; then
 fi
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_stats" -o run -- \
-  python3 "$REPO/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 > "$OUT/${TAG}_stats.log" 2>&1
+  python3 "$REPO/bench.py" --steps 3 --warmup 1 --cpu-seconds 0 --no-e2e > "$OUT/${TAG}_stats.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/${TAG}_fetch" -o run -- \
-  python3 "$REPO/bench.py" --steps 1 --warmup 0 --cpu-seconds 0 > "$OUT/${TAG}_fetch.log" 2>&1
+  python3 "$REPO/bench.py" --steps 1 --warmup 0 --cpu-seconds 0 --no-e2e > "$OUT/${TAG}_fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/${TAG}_write" -o run -- \
-  python3 "$REPO/bench.py" --steps 1 --warmup 0 --cpu-seconds 0 > "$OUT/${TAG}_write.log" 2>&1
+  python3 "$REPO/bench.py" --steps 1 --warmup 0 --cpu-seconds 0 --no-e2e > "$OUT/${TAG}_write.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES --output-format csv \
   -d "$OUT/${TAG}_clock" -o run -- \
-  python3 "$REPO/bench.py" --steps 1 --warmup 0 --cpu-seconds 0 > "$OUT/${TAG}_clock.log" 2>&1
+  python3 "$REPO/bench.py" --steps 1 --warmup 0 --cpu-seconds 0 --no-e2e > "$OUT/${TAG}_clock.log" 2>&1
 cd "$REPO"
 python tools/pmc_summary.py "$OUT/${TAG}_fetch" "$OUT/${TAG}_write" 1000000 20 10000 "$OUT/${TAG}_pmc_gram.json" "$KERNEL"
 python tools/pmc_clock.py "$OUT/${TAG}_clock" "$KERNEL" > "$OUT/${TAG}_clock_mfma.txt"
