@@ -58,14 +58,6 @@ constexpr int kSlo = 4;                // slices of slice group 0 (waves 0-3); g
 #define OB_OZ_A_NT 0
 #endif
 
-#ifndef OB_OZ_MANUAL_A
-// A fragments by inline-asm loads with hand-counted waits (1), or by ordinary loads the compiler
-// waits for (0). The compiler cannot see the B LDS-DMA (inline asm), so its waits for an A load
-// also drain every DMA issued after it -- one sub-tile of prefetch lost; the manual count knows
-// both streams (oz_gram_body).
-#define OB_OZ_MANUAL_A 1
-#endif
-
 #define OZ_HIP(expr)                                                                                  \
   do {                                                                                                \
     hipError_t e_ = (expr);                                                                           \
@@ -433,25 +425,6 @@ __device__ __forceinline__ void oz_dma16(const void* src, uint32_t lds) {
 
 __device__ __forceinline__ void oz_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// The four A units of a sub-tile batch (1 KB apart) by untracked 16-byte loads, SGPR base + lane
-// offset (waited for by oz_wait_a).
-__device__ __forceinline__ void oz_load_a4(ob_v4i (&d)[4], const ob_v4i* base, uint32_t lane_off) {
-  asm volatile(
-      "global_load_dwordx4 %0, %4, %5\n\t"
-      "global_load_dwordx4 %1, %4, %5 offset:1024\n\t"
-      "global_load_dwordx4 %2, %4, %5 offset:2048\n\t"
-      "global_load_dwordx4 %3, %4, %5 offset:3072"
-      : "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3])
-      : "v"(lane_off), "s"(base)
-      : "memory");
-}
-
-// s_waitcnt vmcnt(N) that the four A registers depend on, so no MFMA reading them moves above it.
-template <int N>
-__device__ __forceinline__ void oz_wait_a(ob_v4i (&a)[4]) {
-  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]) : "n"(N) : "memory");
-}
-
 template <int N>
 struct IC {
   static constexpr int value = N;
@@ -512,14 +485,9 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   // sub-tile s is 4 x 1 KB, [replicate block][lane]
   ob_v4i ar[3][4];
   auto aload = [&](ob_v4i (&dst)[4], uint32_t s) {
-    const ob_v4i* blk = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256;
-    if constexpr (OB_OZ_MANUAL_A) {
-      oz_load_a4(dst, blk, (uint32_t)lane * 16u);
-    } else {
-      const ob_v4i* src_a = blk + lane;
+    const ob_v4i* src_a = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256 + lane;
 #pragma unroll
-      for (int m = 0; m < 4; ++m) dst[m] = OB_OZ_A_NT ? __builtin_nontemporal_load(src_a + m * 64) : src_a[m * 64];
-    }
+    for (int m = 0; m < 4; ++m) dst[m] = OB_OZ_A_NT ? __builtin_nontemporal_load(src_a + m * 64) : src_a[m * 64];
   };
   // B fragments of half-step h (sub-tile in ring stage buf)
   auto read = [&](int buf, int h, ob_v4i (&bf)[kSlo]) {
@@ -559,15 +527,6 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   auto step = [&](uint32_t s, auto J) {
     constexpr int j = decltype(J)::value;
     const int buf = (int)((s - s0) & (kNbuf - 1));
-    if constexpr (LIVE && OB_OZ_MANUAL_A && !(DIAG & 4)) {
-      // A(s) was issued at the end of step s - 3 (or waited for in the prologue); after it each of
-      // steps s - 2, s - 1 issued four A loads and, while s + 2 / s + 3 < s1, this wave's NB DMA
-      // pieces of B(s + 2) / B(s + 3). A(s) complete implies B(s + 1) (issued before it) landed.
-      const int nd = (s + 2 < s1 ? 1 : 0) + (s + 3 < s1 ? 1 : 0);
-      if (nd == 2) oz_wait_a<8 + 2 * NB>(ar[j]);
-      else if (nd == 1) oz_wait_a<8 + NB>(ar[j]);
-      else oz_wait_a<8>(ar[j]);
-    }
     if constexpr (LIVE) {
       read(buf, 1, fb1);
       __builtin_amdgcn_sched_barrier(0);
@@ -575,19 +534,8 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
       __builtin_amdgcn_sched_barrier(0);
     }
     const uint32_t ahead = (DIAG & 4) ? 0u : s1 - 1 - s;  // sub-tiles after s
-    if constexpr (OB_OZ_MANUAL_A && !(DIAG & 4)) {
-      // publish B(s + 1): newer than it are A(s) (LIVE), then steps s - 2 and s - 1's A loads and
-      // DMA pieces (B(s + 2), B(s + 3) while below s1)
-      const int nd = (s + 2 < s1 ? 1 : 0) + (s + 3 < s1 ? 1 : 0);
-      constexpr int NA = LIVE ? 4 : 0;
-      if (nd == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NA + 2 * NB) : "memory");
-      else if (nd == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NA + NB) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * NA) : "memory");
-    } else if (ahead >= 3) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (ahead >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if constexpr (DIAG & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // timing only: no barrier
     else oz_barrier();
     if (!(DIAG & 4) && s + kNbuf < s1) dma(buf, s + kNbuf);
