@@ -216,7 +216,7 @@ def test_boot_device_returns_before_the_work_finishes(ob, O):
         n = 10_000
         rows = torch.empty((n, panel.row_len), dtype=torch.float64, device="cuda:0")
         ok = torch.empty(n, dtype=torch.uint8, device="cuda:0")
-        stream = torch.cuda.current_stream(0)
+        stream = torch.cuda.Stream(device=0)  # a real stream (the default stream's handle, 0, means the engine's own)
         panel.boot_device(SEED, 0, n, rows.data_ptr(), ok.data_ptr(), 0, stream=stream.cuda_stream)
         panel.sync()  # first call: builds the digit images
         t0 = time.perf_counter()
