@@ -111,23 +111,73 @@ __host__ __device__ inline uint32_t l1_lds_words(uint32_t ntiles) {
   return (t + 3) / 4 + (t + 1) / 2 + (ntiles > kL1FlatTiles ? 2 * kL1TopWords : 0u);
 }
 
+// OBRS-2 split on the device (ob_spec.h; oracle orc_split_left). The hot columns of every table
+// live in LDS, so a walk that ends within OB_KY_HOT columns of its first (p > 0.9999) makes no
+// global access; deeper columns read the global tables.
+struct KyLds {
+  uint32_t i0[OB_KY_TABLES], obase[OB_KY_TABLES], lbase[OB_KY_TABLES];
+  uint32_t hoff[OB_KY_TABLES][OB_KY_HOT + 1];  // positions in hlist
+  uint16_t hlist[OB_KY_HOT_CAP];
+};
+
+__device__ __forceinline__ void ky_stage(KyLds& L, const ob_ky_tables& g, uint32_t tid) {
+  if (tid < OB_KY_TABLES) {
+    L.i0[tid] = g.i0[tid];
+    L.obase[tid] = g.off_base[tid];
+    L.lbase[tid] = g.list_base[tid];
+  }
+  for (uint32_t i = tid; i < OB_KY_TABLES * (OB_KY_HOT + 1); i += kBlock) (&L.hoff[0][0])[i] = g.hot[i];
+  const uint32_t* he = g.hot + OB_KY_TABLES * (OB_KY_HOT + 1);
+  for (uint32_t i = tid; 2 * i < g.hot_entries; i += kBlock) reinterpret_cast<uint32_t*>(L.hlist)[i] = he[i];
+}
+
+// One B(2^(t + 7), 1/2) sample: the Knuth-Yao walk (ob_spec.h), one stream bit per column.
+__device__ __forceinline__ uint32_t ky_walk(ob_bitstream& s, const KyLds& L, int t, const uint32_t* __restrict__ goff,
+                                            const uint16_t* __restrict__ glist) {
+  const uint32_t i0 = L.i0[t];
+  uint32_t d = ob_bs_take_msb(s, i0 - 1u);  // columns 1 .. i0 - 1 hold no entries
+  for (uint32_t c = 0;; ++c) {
+    d = 2u * d + ob_bs_bit(s);
+    if (c < OB_KY_HOT) {
+      const uint32_t lo = L.hoff[t][c], cnt = L.hoff[t][c + 1] - lo;
+      if (d < cnt) return L.hlist[lo + d];
+      d -= cnt;
+    } else {
+      const uint32_t* off = goff + L.obase[t];
+      const uint32_t i = i0 + c, lo = off[i], cnt = off[i + 1] - lo;
+      if (d < cnt) return glist[L.lbase[t] + lo + d];
+      d -= cnt;
+    }
+  }
+}
+
+// Work item q of the split of a node holding c draws (ob_spec.h, OBRS-2): a popcount word below
+// OB_KY_MIN_C draws, else one Knuth-Yao stream. rl = (round << 5) + level.
+__device__ __forceinline__ uint32_t l1_split_item(uint32_t q, uint32_t c, uint32_t rep, uint32_t c2, uint32_t rl,
+                                                  uint32_t k0, uint32_t k1, const KyLds& L,
+                                                  const uint32_t* __restrict__ goff,
+                                                  const uint16_t* __restrict__ glist) {
+  if (c < OB_KY_MIN_C) return ob_l1_split_bits(q, c, rep, c2, OB_TAG_L1T + rl, k0, k1);
+  const uint32_t c4 = c >> 12;
+  ob_bitstream s = {q << 12, rep, c2, OB_TAG_L1K + rl, k0, k1, 0u, 0u, 0u, 0u, 0u};
+  if (q < c4) return ky_walk(s, L, OB_KY_TABLES - 1, goff, glist);
+  uint32_t left = 0;
+  for (int j = OB_KY_MAX_LOG - 1; j >= OB_KY_MIN_LOG; --j)
+    if ((c >> j) & 1u) left += ky_walk(s, L, j - OB_KY_MIN_LOG, goff, glist);
+  return left + ob_bs_popcount(s, c & 127u);
+}
+
 __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t n1, uint32_t tiles0,
                                                            uint32_t first_rep, uint32_t stride,
                                                            uint32_t key0, uint32_t key1, uint32_t* m1,
                                                            const ob_ky_tables ky_g) {
   extern __shared__ __attribute__((aligned(16))) uint32_t l1s[];
   __shared__ uint32_t s_rej, s_tail, s_acc;
-  constexpr int kKy = OB_KY_MAX_LOG - OB_KY_MIN_LOG + 1;
-  __shared__ uint32_t ky_hot[kKy][OB_KY_HOT + 1];  // the Knuth-Yao tables' first columns
+  __shared__ KyLds kyl;  // the Knuth-Yao tables' hot columns and bases
   const uint32_t g = blockIdx.y, rl = blockIdx.x, rep = first_rep + rl, tid = threadIdx.x;
   const uint32_t n = g ? n1 : n0;
   if (n == 0) return;
-  for (uint32_t i = tid; i < kKy * (OB_KY_HOT + 1); i += kBlock) {
-    const uint32_t t = i / (OB_KY_HOT + 1), c = i % (OB_KY_HOT + 1);
-    ky_hot[t][c] = ky_g.off[t][ky_g.i0[t] + c];
-  }
-  ob_ky_tables ky = ky_g;
-  for (int t = 0; t < kKy; ++t) ky.hot[t] = ky_hot[t];
+  ky_stage(kyl, ky_g, tid);  // published by the first barrier of the round loop
   const uint32_t T = (n + OB_TILE_ROWS - 1) >> OB_TILE_SHIFT, D = l1_depth(T), J = l1_top_levels(T);
   const uint32_t tail = n - (T - 1) * OB_TILE_ROWS;
   const bool small = l1_small(T), partial = tail < OB_TILE_ROWS;
@@ -160,7 +210,7 @@ __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t
     auto level = [&](uint32_t l, uint32_t ll, uint32_t kb, uint32_t nodes, const uint32_t* cur, uint32_t* nxt) {
       const uint32_t span = 1u << (D - l - 1);  // tiles per child
       const uint32_t nnext = (T + span - 1) / span;
-      const uint32_t tag = OB_TAG_L1K + (round << 5) + l;
+      const uint32_t rl = (round << 5) + l;
       if (ll < 8) {  // nodes <= 2^ll: 256 >> ll threads per node; never the large last level
         const uint32_t sh = 8 - ll, k = tid >> sh, j = tid & ((1u << sh) - 1);
         if (j == 0 && k < nodes) nxt[2 * k] = 0;
@@ -168,9 +218,9 @@ __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t
         if (k < nodes) {
           const uint32_t c = cur[k];
           uint32_t left = 0;
-          const uint32_t ns = c ? ob_l1_streams(c) : 0u;
+          const uint32_t ns = c ? ob_l1_items(c) : 0u;
           for (uint32_t q = j; q < ns; q += 1u << sh)
-            left += ob_l1_split_stream(q, c, rep, ((kb + k) << 1) | g, tag, key0, key1, ky);
+            left += l1_split_item(q, c, rep, ((kb + k) << 1) | g, rl, key0, key1, kyl, ky_g.off, ky_g.list);
           if (left) atomicAdd(&nxt[2 * k], left);
         }
         __syncthreads();
@@ -185,8 +235,9 @@ __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t
         for (uint32_t k = tid; k < nodes; k += kBlock) {
           const uint32_t c = cur[k], kg = kb + k;
           uint32_t left = 0;
-          const uint32_t ns = c ? ob_l1_streams(c) : 0u;
-          for (uint32_t q = 0; q < ns; ++q) left += ob_l1_split_stream(q, c, rep, (kg << 1) | g, tag, key0, key1, ky);
+          const uint32_t ns = c ? ob_l1_items(c) : 0u;
+          for (uint32_t q = 0; q < ns; ++q)
+            left += l1_split_item(q, c, rep, (kg << 1) | g, rl, key0, key1, kyl, ky_g.off, ky_g.list);
           const uint32_t right = c - left;
           if (to_m1) {
             emit(2 * kg, left);
@@ -996,14 +1047,18 @@ __global__ __launch_bounds__(kBlock) void ob_residual_kernel(const double* cols,
 // (multi-limb integers, C(n, k + 1) = C(n, k) (n - k) / (k + 1)); column i = 1 .. n lists the k
 // with bit n - i of W_k set. Built once per process, uploaded once per device (~22 MB).
 struct KyHost {
-  std::vector<uint32_t> off[OB_KY_MAX_LOG - OB_KY_MIN_LOG + 1];
-  std::vector<uint16_t> list[OB_KY_MAX_LOG - OB_KY_MIN_LOG + 1];
-  uint32_t i0[OB_KY_MAX_LOG - OB_KY_MIN_LOG + 1] = {};
+  std::vector<uint32_t> off;   // all tables' column offsets, table t at off_base[t]
+  std::vector<uint16_t> list;  // all tables' lists, table t at list_base[t]
+  std::vector<uint32_t> hot;   // [tables][OB_KY_HOT + 1] hot offsets, then the hot entries as uint16 pairs
+  uint32_t off_base[OB_KY_TABLES] = {}, list_base[OB_KY_TABLES] = {}, i0[OB_KY_TABLES] = {};
+  uint32_t hot_entries = 0;
 };
 
 const KyHost& ky_host() {
   static const KyHost h = [] {
     KyHost t;
+    std::vector<uint16_t> hot_list;
+    std::vector<uint32_t> hot_off;
     for (int j = OB_KY_MIN_LOG; j <= OB_KY_MAX_LOG; ++j) {
       const uint32_t n = 1u << j, L = n / 64 + 1;
       std::vector<uint64_t> w((size_t)(n + 1) * L, 0);
@@ -1025,10 +1080,10 @@ const KyHost& ky_host() {
         }
       }
       const int x = j - OB_KY_MIN_LOG;
-      std::vector<uint32_t>& off = t.off[x];
-      std::vector<uint16_t>& list = t.list[x];
-      off.assign(n + 2, 0);
-      t.i0[x] = 0;
+      t.off_base[x] = (uint32_t)t.off.size();
+      t.list_base[x] = (uint32_t)t.list.size();
+      std::vector<uint32_t> off(n + 2, 0);
+      std::vector<uint16_t> list;
       for (uint32_t i = 1; i <= n; ++i) {
         off[i] = (uint32_t)list.size();
         const uint32_t bit = n - i;
@@ -1037,7 +1092,15 @@ const KyHost& ky_host() {
         if (!t.i0[x] && list.size() > off[i]) t.i0[x] = i;
       }
       off[n + 1] = (uint32_t)list.size();
+      for (uint32_t c = 0; c <= OB_KY_HOT; ++c) hot_off.push_back((uint32_t)hot_list.size() + off[t.i0[x] + c] - off[t.i0[x]]);
+      hot_list.insert(hot_list.end(), list.begin() + off[t.i0[x]], list.begin() + off[t.i0[x] + OB_KY_HOT]);
+      t.off.insert(t.off.end(), off.begin(), off.end());
+      t.list.insert(t.list.end(), list.begin(), list.end());
     }
+    t.hot_entries = (uint32_t)hot_list.size();
+    if (hot_list.size() % 2) hot_list.push_back(0);
+    t.hot = hot_off;
+    for (size_t i = 0; i < hot_list.size(); i += 2) t.hot.push_back((uint32_t)hot_list[i] | ((uint32_t)hot_list[i + 1] << 16));
     return t;
   }();
   return h;
@@ -1050,18 +1113,25 @@ int ky_device(int device, ob_ky_tables* out) {
   auto it = cache.find(device);
   if (it == cache.end()) {
     const KyHost& h = ky_host();
+    if (h.hot_entries > OB_KY_HOT_CAP) return ob::fail(OB_E_INVALID, "internal: Knuth-Yao hot columns exceed the LDS stage");
     ob_ky_tables t{};
-    for (int x = 0; x <= OB_KY_MAX_LOG - OB_KY_MIN_LOG; ++x) {
-      uint32_t* off = nullptr;
-      uint16_t* list = nullptr;
-      HIP_OK(hipMalloc(&off, sizeof(uint32_t) * h.off[x].size()));
-      HIP_OK(hipMalloc(&list, sizeof(uint16_t) * h.list[x].size()));
-      HIP_OK(hipMemcpy(off, h.off[x].data(), sizeof(uint32_t) * h.off[x].size(), hipMemcpyHostToDevice));
-      HIP_OK(hipMemcpy(list, h.list[x].data(), sizeof(uint16_t) * h.list[x].size(), hipMemcpyHostToDevice));
-      t.off[x] = off;
-      t.list[x] = list;
+    uint32_t *off = nullptr, *hot = nullptr;
+    uint16_t* list = nullptr;
+    HIP_OK(hipMalloc(&off, sizeof(uint32_t) * h.off.size()));
+    HIP_OK(hipMalloc(&list, sizeof(uint16_t) * h.list.size()));
+    HIP_OK(hipMalloc(&hot, sizeof(uint32_t) * h.hot.size()));
+    HIP_OK(hipMemcpy(off, h.off.data(), sizeof(uint32_t) * h.off.size(), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(list, h.list.data(), sizeof(uint16_t) * h.list.size(), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(hot, h.hot.data(), sizeof(uint32_t) * h.hot.size(), hipMemcpyHostToDevice));
+    t.off = off;
+    t.list = list;
+    t.hot = hot;
+    for (int x = 0; x < OB_KY_TABLES; ++x) {
+      t.off_base[x] = h.off_base[x];
+      t.list_base[x] = h.list_base[x];
       t.i0[x] = h.i0[x];
     }
+    t.hot_entries = h.hot_entries;
     it = cache.emplace(device, t).first;
   }
   *out = it->second;

@@ -32,7 +32,9 @@
 
 #define OB_TILE_ROWS 256u
 #define OB_TILE_SHIFT 8u
-#define OB_TAG_L1K 0x4B310000u /* "K1" + (round << 5) + level: split streams of node k, {q << 12 | call, rep, 2k | g} */
+#define OB_TAG_L1T 0x4C310000u /* "L1" + (round << 5) + level: popcount bits of node k (c < 4096), {q, rep, 2k | g} */
+#define OB_TAG_L1K 0x4B310000u /* "K1" + (round << 5) + level: KY streams of node k (c >= 4096), {q << 12 | call, rep, 2k | g} */
+#define OB_KY_MIN_C 4096u      /* a node of at least this many draws splits by Knuth-Yao samples */
 #define OB_TAG_L1S 0x4C530000u /* "LS" + round: partial-tile acceptance bytes, {q, rep, g} */
 #define OB_TAG_L1D 0x4C440000u /* "LD" + (j >> 2): direct draw r, attempt j, {r, rep, g} */
 #define OB_L1_DIRECT 256u      /* rejected draws at most this many are drawn directly */
@@ -92,45 +94,71 @@ OB_HD ob_u32x4 ob_philox_x3(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, 
 }
 
 // ---- OBRS-2 level-1 split ---------------------------------------------------------------------
-// Binomial(c, 1/2) = the sum of exact B(2^j, 1/2) samples over the binary digits of c: c >> 12
-// samples of B(4096), one B(2^j) per set bit j = 11 .. 7, and the popcount of c & 127 fair bits.
+// Binomial(c, 1/2) of a node with c < OB_KY_MIN_C draws: the popcount of c fair bits (OBRS-1's
+// split, ob_l1_split_bits). From OB_KY_MIN_C up, the sum of exact B(2^j, 1/2) samples over the binary
+// digits of c: c >> 12 samples of B(4096), one B(2^j) per set bit j = 11 .. 7, and the popcount of
+// c & 127 fair bits.
 // B(n = 2^j) is a Knuth-Yao walk (discrete distribution generating tree) over the dyadic
 // probabilities p_k = C(n, k) / 2^n: column i = 1 .. n of the tree holds the k whose bit n - i of
 // C(n, k) is set, in ascending k (list[off[i] .. off[i+1])); the walk reads one stream bit per
 // column, d = 2 d + bit, returns the d-th entry when d < the column's count and subtracts the
-// count otherwise. Exact, ~H + 2 ~ 9 bits per sample. Streams: q < nb = ceil((c >> 12) / 8)
-// carries B(4096) samples 8q .. min(8q + 8, c >> 12) - 1, stream nb the B(2^j), j = 11 .. 7, then
-// the popcount bits; bit b of stream q is bit (b & 31) of word ((b >> 5) & 3) of
-// Philox({q << 12 | b >> 7, rep, c2, tag}). Tables: ob_ky_build (host), KyTables (device).
+// count otherwise. Exact, ~H + 2 ~ 9 bits per sample. Streams: q < c >> 12 carries B(4096) sample
+// q, stream c >> 12 the B(2^j), j = 11 .. 7, then the popcount bits; bit b of stream q is bit
+// (b & 31) of word ((b >> 5) & 3) of Philox({q << 12 | b >> 7, rep, c2, tag}).
 #define OB_KY_MIN_LOG 7
 #define OB_KY_MAX_LOG 12
-#define OB_KY_HOT 32  // columns i0 .. i0 + 31 of each table, staged in LDS (a walk rarely goes deeper)
+#define OB_KY_TABLES (OB_KY_MAX_LOG - OB_KY_MIN_LOG + 1)
+#define OB_KY_HOT 16        // columns i0 .. i0 + 15 of each table staged in LDS: a walk ends there with p > 0.9999
+#define OB_KY_HOT_CAP 5120  // their entries, all tables (4,996 at OB_KY_HOT = 16)
 
-struct ob_ky_tables {  // device pointers, per n = 2^j for j = OB_KY_MIN_LOG .. OB_KY_MAX_LOG
-  const uint32_t* off[OB_KY_MAX_LOG - OB_KY_MIN_LOG + 1];  // n + 2 entries
-  const uint16_t* list[OB_KY_MAX_LOG - OB_KY_MIN_LOG + 1];
-  uint32_t i0[OB_KY_MAX_LOG - OB_KY_MIN_LOG + 1];  // first column with an entry
-  const uint32_t* hot[OB_KY_MAX_LOG - OB_KY_MIN_LOG + 1];  // off[i0 .. i0 + OB_KY_HOT] (LDS), or null
+// The tables on the device (built once per process, ob_engine.hip ky_host): table t (n = 2^(t + 7))
+// has n + 2 column offsets at off + off_base[t] (positions in its own list) and its list at
+// list + list_base[t]; hot = [OB_KY_TABLES][OB_KY_HOT + 1] offsets of the hot columns into the hot
+// entries that follow as uint16 pairs.
+struct ob_ky_tables {
+  const uint32_t* off;
+  const uint16_t* list;
+  const uint32_t* hot;
+  uint32_t off_base[OB_KY_TABLES], list_base[OB_KY_TABLES], i0[OB_KY_TABLES];
+  uint32_t hot_entries;
 };
 
-OB_HD uint32_t ob_l1_streams(uint32_t c) { return (((c >> 12) + 7) >> 3) + 1; }
+// Fair bits [128 q, min(c, 128 q + 128)) of a node's popcount stream, counted (nodes of c < 4096
+// draws): bit b is bit (b & 31) of word ((b >> 5) & 3) of Philox({b >> 7, rep, c2, tag}).
+OB_HD uint32_t ob_l1_split_bits(uint32_t q, uint32_t c, uint32_t rep, uint32_t c2, uint32_t tag, uint32_t k0,
+                                uint32_t k1) {
+  const ob_u32x4 u = ob_philox(q, rep, c2, tag, k0, k1);
+  const uint32_t r = c - 128u * q;
+  const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
+  uint32_t s = 0;
+  for (uint32_t i = 0; i < 4; ++i) {
+    const uint32_t nb = r > 32u * i ? r - 32u * i : 0u;
+    s += (uint32_t)__builtin_popcount(nb >= 32u ? wd[i] : (wd[i] & ((1u << nb) - 1u)));
+  }
+  return s;
+}
 
+// Work items of a node's split: popcount words below OB_KY_MIN_C, else c >> 12 B(4096) streams plus
+// the stream of the low digits.
+OB_HD uint32_t ob_l1_items(uint32_t c) { return c < OB_KY_MIN_C ? (c + 127u) >> 7 : (c >> 12) + 1u; }
+
+// A node stream: bit b is bit (b & 31) of word ((b >> 5) & 3) of Philox({ctr0 | b >> 7, rep, c2, tag}).
 struct ob_bitstream {
   uint32_t ctr0, rep, c2, tag, k0, k1;
   uint32_t pos;
-  uint32_t w[4];
+  uint32_t w0, w1, w2, w3;
 };
 
 OB_HD uint32_t ob_bs_word(ob_bitstream& s) {  // the 32-bit word holding bit s.pos (refilled per 128 bits)
   if ((s.pos & 127u) == 0) {
     const ob_u32x4 u = ob_philox(s.ctr0 | (s.pos >> 7), s.rep, s.c2, s.tag, s.k0, s.k1);
-    s.w[0] = u.x;
-    s.w[1] = u.y;
-    s.w[2] = u.z;
-    s.w[3] = u.w;
+    s.w0 = u.x;
+    s.w1 = u.y;
+    s.w2 = u.z;
+    s.w3 = u.w;
   }
   const uint32_t q = (s.pos >> 5) & 3u;
-  return q == 0 ? s.w[0] : q == 1 ? s.w[1] : q == 2 ? s.w[2] : s.w[3];
+  return q == 0 ? s.w0 : q == 1 ? s.w1 : q == 2 ? s.w2 : s.w3;
 }
 
 OB_HD uint32_t ob_bs_bit(ob_bitstream& s) {
@@ -154,45 +182,20 @@ OB_HD uint32_t ob_bs_take_msb(ob_bitstream& s, uint32_t m) {
   return v;
 }
 
-OB_HD uint32_t ob_ky_sample(ob_bitstream& s, const uint32_t* off, const uint16_t* list, uint32_t i0,
-                            const uint32_t* hot) {
-  uint32_t d = ob_bs_take_msb(s, i0 - 1u);  // columns 1 .. i0 - 1 hold no entries
-  for (uint32_t i = i0;; ++i) {
-    d = 2u * d + ob_bs_bit(s);
-    const uint32_t t = i - i0;
-    const uint32_t lo = (hot && t < OB_KY_HOT) ? hot[t] : off[i];
-    const uint32_t cnt = ((hot && t < OB_KY_HOT) ? hot[t + 1] : off[i + 1]) - lo;
-    if (d < cnt) return list[lo + d];
-    d -= cnt;
-  }
-}
-
-// Stream q's part of node c's split (the node's left count is the sum over q < ob_l1_streams(c)).
-OB_HD uint32_t ob_l1_split_stream(uint32_t q, uint32_t c, uint32_t rep, uint32_t c2, uint32_t tag, uint32_t k0,
-                                  uint32_t k1, const ob_ky_tables& ky) {
-  const uint32_t c4 = c >> 12, nb = (c4 + 7u) >> 3;
-  ob_bitstream s = {q << 12, rep, c2, tag, k0, k1, 0u, {0u, 0u, 0u, 0u}};
+// Popcount of the next m stream bits.
+OB_HD uint32_t ob_bs_popcount(ob_bitstream& s, uint32_t m) {
   uint32_t left = 0;
-  if (q < nb) {
-    const uint32_t s1 = 8u * q + 8u < c4 ? 8u * q + 8u : c4;
-    const int t = OB_KY_MAX_LOG - OB_KY_MIN_LOG;
-    for (uint32_t i = 8u * q; i < s1; ++i) left += ob_ky_sample(s, ky.off[t], ky.list[t], ky.i0[t], ky.hot[t]);
-  } else {
-    for (int j = OB_KY_MAX_LOG - 1; j >= OB_KY_MIN_LOG; --j)
-      if ((c >> j) & 1u) {
-        const int t = j - OB_KY_MIN_LOG;
-        left += ob_ky_sample(s, ky.off[t], ky.list[t], ky.i0[t], ky.hot[t]);
-      }
-    for (uint32_t m = c & 127u; m;) {  // popcount of the next m bits, word by word
-      const uint32_t sh = s.pos & 31u, take = m < 32u - sh ? m : 32u - sh;
-      const uint32_t w = ob_bs_word(s) >> sh;
-      left += (uint32_t)__builtin_popcount(take == 32u ? w : (w & ((1u << take) - 1u)));
-      s.pos += take;
-      m -= take;
-    }
+  while (m) {
+    const uint32_t sh = s.pos & 31u, take = m < 32u - sh ? m : 32u - sh;
+    const uint32_t w = ob_bs_word(s) >> sh;
+    left += (uint32_t)__builtin_popcount(take == 32u ? w : (w & ((1u << take) - 1u)));
+    s.pos += take;
+    m -= take;
   }
   return left;
 }
+// The walk and the stream split (device, LDS-staged hot columns): ob_engine.hip ky_walk,
+// l1_split_stream; restated independently in oracle/ob_oracle.c orc_split_left.
 
 // floor(u * s / 2^64), s < 2^32.
 OB_HD uint32_t ob_mulhi64(uint32_t lo, uint32_t hi, uint32_t s) {

@@ -70,16 +70,17 @@ static inline uint64_t orc_draw_u64(const uint32_t w[4], int odd) {
  * (j & 3) of Philox({r, rep, g, ORC_TAG_L1D + (j >> 2)}), attempt j. Each split is an exact
  * Binomial(c, 1/2), so the accepted draws are i.i.d. uniform over the valid rows.
  *
- * The split (OBRS-2; OBRS-1 drew c fair bits and counted them, ~5.5M bits per group per
- * replicate at 500k rows): L = the sum of exact Binomial(2^j, 1/2) samples over the binary
- * digits of c -- c >> 12 samples of B(4096), one B(2^j) for each set bit j = 11 .. 7, and the
- * popcount of c & 127 fair bits. Each B(2^j) is a Knuth-Yao walk (discrete distribution
+ * The split (OBRS-2): a node with c < 4096 draws takes OBRS-1's popcount of c fair bits (bit b =
+ * bit (b & 31) of word ((b >> 5) & 3) of Philox({b >> 7, rep, (k << 1) | g, ORC_TAG_L1T + rl}),
+ * rl = (round << 5) + level). A node with c >= 4096 sums exact Binomial(2^j, 1/2) samples over
+ * the binary digits of c -- c >> 12 samples of B(4096), one B(2^j) for each set bit j = 11 .. 7,
+ * and the popcount of c & 127 fair bits. Each B(2^j) is a Knuth-Yao walk (discrete distribution
  * generating tree) over the exact dyadic probabilities C(2^j, k) / 2^(2^j): ~9 random bits per
- * sample instead of 2^j. Bits come from per-node streams: stream q of node (l, k) in round r has
- * bit b = bit (b & 31) of word ((b >> 5) & 3) of Philox({(q << 12) | (b >> 7), rep, (k << 1) | g,
- * ORC_TAG_L1K + (r << 5) + l}). Streams q < nb = ceil((c >> 12) / 8) carry B(4096) samples
- * 8q .. min(8q + 8, c >> 12) - 1 in order; stream nb carries the B(2^j) for j = 11 down to 7,
- * then the c & 127 popcount bits. */
+ * sample instead of 2^j. Bits come from per-node streams: stream q has bit b = bit (b & 31) of
+ * word ((b >> 5) & 3) of Philox({(q << 12) | (b >> 7), rep, (k << 1) | g, ORC_TAG_L1K + rl});
+ * stream q < c >> 12 carries B(4096) sample q, stream c >> 12 the B(2^j), j = 11 down to 7, then
+ * the c & 127 popcount bits. (OBRS-1 used the popcount at every node: ~5.5M bits per group and
+ * replicate at 500k rows, ~2.5M of them at nodes of 4096 draws or more.) */
 #define ORC_TAG_L1T 0x4C310000u /* OBRS-1 "L1" + (round << 5) + level (superseded) */
 #define ORC_TAG_L1K 0x4B310000u /* OBRS-2 "K1" + (round << 5) + level */
 #define ORC_TAG_L1S 0x4C530000u /* "LS" + round */
@@ -167,16 +168,30 @@ static uint32_t orc_ky_sample(orc_bits* s, const orc_ky* t) {
     }
 }
 
-/* Binomial(c, 1/2) for node k of level l, group g (OBRS-2, above). */
-static uint32_t orc_split_left(uint32_t c, uint32_t rep, uint32_t g, uint32_t k, uint32_t tag, const uint32_t key[2]) {
-    pthread_once(&orc_ky_once, orc_ky_init);
-    const uint32_t c4 = c >> 12, nb = (c4 + 7) / 8;
+/* Binomial(c, 1/2) for node k of a level, group g; rl = (round << 5) + level (OBRS-2, above). */
+#define ORC_KY_MIN_C 4096u
+static uint32_t orc_split_left(uint32_t c, uint32_t rep, uint32_t g, uint32_t k, uint32_t rl, const uint32_t key[2]) {
+    const uint32_t c2 = (k << 1) | g;
     uint32_t left = 0;
-    for (uint32_t q = 0; q <= nb; ++q) {
-        orc_bits s = {{q << 12, rep, (k << 1) | g, tag}, key, 0, {0, 0, 0, 0}};
-        if (q < nb) {
-            const uint32_t s1 = 8 * q + 8 < c4 ? 8 * q + 8 : c4;
-            for (uint32_t i = 8 * q; i < s1; ++i) left += orc_ky_sample(&s, &orc_ky_tab[12]);
+    if (c < ORC_KY_MIN_C) { /* OBRS-1: the popcount of c fair bits, 128 per Philox call */
+        for (uint32_t q = 0; 128u * q < c; ++q) {
+            uint32_t ctr[4] = {q, rep, c2, ORC_TAG_L1T + rl}, w[4];
+            orc_philox4x32_10(ctr, key, w);
+            uint32_t r = c - 128u * q;
+            for (uint32_t i = 0; i < 4; ++i) {
+                uint32_t nb = r > 32u * i ? r - 32u * i : 0u;
+                uint32_t mask = nb >= 32u ? 0xFFFFFFFFu : ((1u << nb) - 1u);
+                left += (uint32_t)__builtin_popcount(w[i] & mask);
+            }
+        }
+        return left;
+    }
+    pthread_once(&orc_ky_once, orc_ky_init);
+    const uint32_t c4 = c >> 12;
+    for (uint32_t q = 0; q <= c4; ++q) {
+        orc_bits s = {{q << 12, rep, c2, ORC_TAG_L1K + rl}, key, 0, {0, 0, 0, 0}};
+        if (q < c4) {
+            left += orc_ky_sample(&s, &orc_ky_tab[12]);
         } else {
             for (uint32_t j = 11; j >= 7; --j)
                 if ((c >> j) & 1u) left += orc_ky_sample(&s, &orc_ky_tab[j]);
@@ -186,10 +201,10 @@ static uint32_t orc_split_left(uint32_t c, uint32_t rep, uint32_t g, uint32_t k,
     return left;
 }
 
-/* Test hook: one OBRS-2 split of c draws (node k of a level with tag `tag`). */
-uint32_t orc_binomial_half(uint32_t c, uint64_t seed, uint32_t rep, uint32_t g, uint32_t k, uint32_t tag) {
+/* Test hook: one OBRS-2 split of c draws (node k, rl = (round << 5) + level). */
+uint32_t orc_binomial_half(uint32_t c, uint64_t seed, uint32_t rep, uint32_t g, uint32_t k, uint32_t rl) {
     const uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
-    return orc_split_left(c, rep, g, k, tag, key);
+    return orc_split_left(c, rep, g, k, rl, key);
 }
 
 void orc_level1_counts(uint64_t seed, uint32_t rep, uint32_t g, uint32_t n, uint32_t* m) {
@@ -210,7 +225,7 @@ void orc_level1_counts(uint64_t seed, uint32_t rep, uint32_t g, uint32_t n, uint
             uint32_t span = 1u << (depth - l - 1); /* tiles per child */
             uint32_t nnext = (ntiles + span - 1) / span;
             for (uint32_t k = 0; k < nodes; ++k) {
-                uint32_t c = cur[k], left = c ? orc_split_left(c, rep, g, k, ORC_TAG_L1K + (round << 5) + l, key) : 0;
+                uint32_t c = cur[k], left = c ? orc_split_left(c, rep, g, k, (round << 5) + l, key) : 0;
                 nxt[2 * k] = left;
                 if (2 * k + 1 < nnext) nxt[2 * k + 1] = c - left;
                 else rejected += c - left;

@@ -99,9 +99,10 @@ def level1_counts(seed, rep, g, n):
     return m[: (n + 255) // 256]
 
 
-def binomial_half(c, seed, rep, g=0, k=0, tag=0x4B310000):
-    """One OBRS-2 level-1 split of c draws (Knuth-Yao B(2^j, 1/2) samples + popcount bits)."""
-    return int(lib().orc_binomial_half(c, seed & (2**64 - 1), rep, g, k, tag))
+def binomial_half(c, seed, rep, g=0, k=0, rl=0):
+    """One OBRS-2 level-1 split of c draws (popcount below 4096 draws; Knuth-Yao B(2^j, 1/2)
+    samples + popcount bits from 4096 up); rl = (round << 5) + level."""
+    return int(lib().orc_binomial_half(c, seed & (2**64 - 1), rep, g, k, rl))
 
 
 def resample_indices(seed, rep, g, n):

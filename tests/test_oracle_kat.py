@@ -201,11 +201,11 @@ def test_reference_groups_kat(O, mode):  # tests/features_test.rs:14-35 (Cotton,
     assert ob.run(threads=2)["total_gap"] > 0.0
 
 
-@pytest.mark.parametrize("c", [1, 100, 128, 129, 777, 4096, 4097, 9000, 70001, 500000])
+@pytest.mark.parametrize("c", [1, 100, 128, 129, 777, 4095, 4096, 4097, 9000, 70001, 500000])
 def test_obrs2_split_is_binomial(O, c):
-    """OBRS-2's level-1 split (Knuth-Yao B(2^j, 1/2) samples over the binary digits of c plus a
-    popcount of c & 127 bits): Binomial(c, 1/2) in law -- chi-square over central quantile bins,
-    mean and variance within 5 standard errors."""
+    """OBRS-2's level-1 split (popcount below 4096 draws; from 4096 up Knuth-Yao B(2^j, 1/2)
+    samples over the binary digits of c plus a popcount of c & 127 bits): Binomial(c, 1/2) in law
+    -- chi-square over central quantile bins, mean and variance within 5 standard errors."""
     from scipy import stats
 
     n = 6000 if c < 100_000 else 2000
