@@ -58,6 +58,11 @@ constexpr int kSlo = 4;                // slices of slice group 0 (waves 0-3); g
 #define OB_OZ_A_NT 0
 #endif
 
+#ifndef OB_OZ_A_LDS
+// 1: A fragments by LDS-DMA beside B (oz_gram_la_kernel); 0: from L2 into registers (oz_gram_kernel)
+#define OB_OZ_A_LDS 1
+#endif
+
 #define OZ_HIP(expr)                                                                                  \
   do {                                                                                                \
     hipError_t e_ = (expr);                                                                           \
@@ -608,6 +613,188 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   }
 }
 
+// ---- A through LDS (OB_OZ_A_LDS, the default) --------------------------------------------------
+// Every operand arrives by LDS-DMA: per 64-row sub-tile a ring stage holds the 14 KB B image and
+// the block's 16 KB of A fragments (4 replicate batches x 4 x 1 KB), 30 one-KB pieces spread over
+// the 8 waves. The two waves of a batch (slice groups 0 and 1) read one copy of its A from LDS
+// instead of each loading it from L2, and no vector-memory load is tracked by the compiler, so the
+// hand-counted wait before each barrier covers exactly the stage it publishes (the tracked A
+// loads of the register path also waited for the DMA issued after them, a sub-tile early).
+constexpr int kAUnits = 4 * 4 * 64;                      // A fragments of a stage (16 KB)
+constexpr int kStageUnits = kSubUnits + kAUnits;          // 30 KB
+constexpr int kPieces = kStageUnits / 64;                 // 30 one-KB DMA pieces per stage
+constexpr size_t kLdsLA = kNbuf * (size_t)kStageUnits * 16;  // 120 KB
+constexpr size_t kLdsBytesLA = kLdsLA > kLdsX ? kLdsLA : kLdsX;
+static_assert(kPieces == 30, "piece split below: 4 per wave on waves 0-5, 3 on waves 6-7");
+
+template <int NQ, int NP, bool LIVE, int DIAG>
+__device__ __forceinline__ void oz_gram_body_la(const OzArgs& a, unsigned char* smem, int wave) {
+  const ob_v4i* st = reinterpret_cast<const ob_v4i*>(smem);  // [kNbuf][kStageUnits]
+  const int lane = threadIdx.x & 63;
+  const int wb = wave & 3, grp = wave >> 2;
+  const int slo = grp ? kSlo : 0;
+  const uint32_t nwg = gridDim.x, bid = blockIdx.x;
+  const uint32_t xcd = bid & 7u, slot = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7u;
+  const uint32_t wi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int ct = (int)(wi % (uint32_t)a.n_ct);
+  const uint32_t tq = wi / (uint32_t)a.n_ct;
+  const uint32_t rt = tq % a.n_rt, chunk = tq / a.n_rt;
+  const uint32_t g = a.chunks[3 * chunk];
+  const uint32_t n = g ? a.n1 : a.n0, tg0 = g ? a.tiles0 : 0u;
+  const uint32_t s0 = a.chunks[3 * chunk + 1] * 4u;
+  const uint32_t s1 = min(a.chunks[3 * chunk + 2] * 4u, (n + 63u) >> 6);
+  const ob_v4i* Bg = g ? a.B1 : a.B0;
+  const uint32_t batch = rt * 4u + (uint32_t)wb;
+  // this wave's pieces p = 8 t + wave of stage buf <- sub-tile s: B pieces 0..13, then A piece
+  // p - 14 = (batch in tile) * 4 + m (a batch past the last loads the last one's, never read)
+  auto dma = [&](int buf, uint32_t s) {
+#pragma unroll
+    for (int t = 0; t < NP; ++t) {
+      const int p = t * kWaves + wave;
+      const ob_v4i* src;
+      if (p < kBDmaTotal) {
+        src = Bg + ((size_t)s * a.n_ct + ct) * kSubUnits + p * 64;
+      } else {
+        const int ap = p - kBDmaTotal;
+        const uint32_t bb = min(rt * 4u + (uint32_t)(ap >> 2), a.nb_rep - 1u);
+        src = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + bb) * 4 + (s & 3)) * 256 + (ap & 3) * 64;
+      }
+      oz_dma16(src + lane, (uint32_t)(buf * kStageUnits + p * 64) * 16u);
+    }
+  };
+  auto read_b = [&](int buf, int h, ob_v4i (&bf)[kSlo]) {
+    const ob_v4i* bb = st + buf * kStageUnits + (slo * 2 + h) * 64 + lane;
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) bf[q] = bb[q * 128];
+  };
+  auto read_a = [&](int buf, ob_v4i (&af)[4]) {
+    const ob_v4i* ab = st + buf * kStageUnits + kSubUnits + wb * 256 + lane;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) af[m] = ab[m * 64];
+  };
+
+  ob_v4i acc[4][kSlo][2];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int q = 0; q < kSlo; ++q) acc[m][q][0] = acc[m][q][1] = (ob_v4i){};
+#pragma unroll
+  for (int j = 0; j < kNbuf; ++j)
+    if (s0 + j < s1) dma(j, s0 + j);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  ob_v4i fb0[kSlo], fb1[kSlo], ar[2][4];
+  if constexpr (LIVE) {
+    read_b(0, 0, fb0);
+    read_a(0, ar[0]);
+  }
+  // Step s: read B (s, 1); MFMAs (s, 0). Barrier B_s publishes stage s + 1: its DMA was issued
+  // after B_(s-3), and after it at most the DMA rounds of B_(s-2), B_(s-1) (while s + 2, s + 3 <
+  // s1), NP pieces each. Then refill stage s with s + 4, read B (s + 1, 0) and A (s + 1), MFMAs
+  // (s, 1).
+  auto step = [&](uint32_t s, auto J) {
+    constexpr int j = decltype(J)::value;
+    const int buf = (int)((s - s0) & (kNbuf - 1));
+    if constexpr (LIVE) {
+      read_b(buf, 1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(DIAG & 2)) oz_mfmas<NQ>(acc, 0, ar[j], fb0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const int nd = (s + 2 < s1 ? 1 : 0) + (s + 3 < s1 ? 1 : 0);
+    if (nd == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NP) : "memory");
+    else if (nd == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    oz_barrier();
+    if (s + kNbuf < s1) dma(buf, s + kNbuf);
+    if constexpr (LIVE) {
+      const int nb = (buf + 1) & (kNbuf - 1);
+      read_b(nb, 0, fb0);
+      read_a(nb, ar[j ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(DIAG & 2)) oz_mfmas<NQ>(acc, 1, ar[j], fb1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  uint32_t s = s0;
+  for (; s + 2 <= s1; s += 2) {
+    step(s, IC<0>{});
+    step(s + 1, IC<1>{});
+  }
+  if (s < s1) step(s, IC<0>{});
+  // slices -> f64 (as oz_gram_body)
+  int E[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int pair = ct * kPairsPerTile + 16 * h + (lane & 15);
+    E[h] = a.pexp[chunk * a.n_pairs_pad + min(pair, a.n_pairs_pad - 1)];
+  }
+  double v[4][2][4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int shift = E[h] - kFracBits + 8 * (kS - slo - NQ);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        long long part = 0;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) part = part * 256 + acc[m][q][h][i];
+        v[m][h][i] = ldexp((double)part, shift);
+      }
+    }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // every wave is done with the ring: the exchange overlays it
+  double* xch = reinterpret_cast<double*>(smem);
+  if (grp) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          xch[(wb * 64 + 16 * m + 4 * (lane >> 4) + i) * kPairsPerTile + 16 * h + (lane & 15)] = v[m][h][i];
+  }
+  __syncthreads();
+  if (grp || !LIVE) return;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int pair = ct * kPairsPerTile + 16 * h + (lane & 15);
+    if (pair >= a.e_pad) continue;
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int rl = 16 * m + 4 * (lane >> 4) + i;
+        const uint32_t rep = batch * 64u + (uint32_t)rl;
+        const double val = v[m][h][i] + xch[(wb * 64 + rl) * kPairsPerTile + 16 * h + (lane & 15)];
+        if (rep < a.n_reps) a.partial[((size_t)chunk * a.rep_pad + rep) * a.e_pad + pair] = val;
+      }
+  }
+}
+
+template <int DIAG>
+__global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_la_kernel(const OzArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nwg = gridDim.x, bid = blockIdx.x;
+  const uint32_t xcd = bid & 7u, slot = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7u;
+  const uint32_t wi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const uint32_t rt = (wi / (uint32_t)a.n_ct) % a.n_rt;
+  const bool live = rt * 4u + (uint32_t)(wave & 3) < a.nb_rep;
+  // waves 0-3: slices 0-3; 4-7: slices 4-6; DMA pieces: 4 on waves 0-5, 3 on waves 6-7
+  if (wave < 4) {
+    if (live) oz_gram_body_la<kSlo, 4, true, DIAG>(a, smem, wave);
+    else oz_gram_body_la<kSlo, 4, false, DIAG>(a, smem, wave);
+  } else if (wave < 6) {
+    if (live) oz_gram_body_la<kS - kSlo, 4, true, DIAG>(a, smem, wave);
+    else oz_gram_body_la<kS - kSlo, 4, false, DIAG>(a, smem, wave);
+  } else {
+    if (live) oz_gram_body_la<kS - kSlo, 3, true, DIAG>(a, smem, wave);
+    else oz_gram_body_la<kS - kSlo, 3, false, DIAG>(a, smem, wave);
+  }
+}
+
 template <int DIAG>
 __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -831,6 +1018,17 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(kWaves * 64), kLdsBytes, s, a);
     return hipGetLastError();
   };
+  if (OB_OZ_A_LDS && (diag == 0 || diag == 2)) {
+    auto launch_la = [&](auto kern) -> hipError_t {
+      hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytesLA);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(kern, dim3(blocks), dim3(kWaves * 64), kLdsBytesLA, s, a);
+      return hipGetLastError();
+    };
+    if (diag == 2) OZ_HIP(launch_la(oz_gram_la_kernel<2>));
+    else OZ_HIP(launch_la(oz_gram_la_kernel<0>));
+    return OB_OK;
+  }
   switch (diag) {
     case 2: OZ_HIP(launch(oz_gram_kernel<2>)); break;
     case 4: OZ_HIP(launch(oz_gram_kernel<4>)); break;
