@@ -59,8 +59,10 @@ constexpr int kSlo = 4;                // slices of slice group 0 (waves 0-3); g
 #endif
 
 #ifndef OB_OZ_A_LDS
-// 1: A fragments by LDS-DMA beside B (oz_gram_la_kernel); 0: from L2 into registers (oz_gram_kernel)
-#define OB_OZ_A_LDS 1
+// 1: A fragments by LDS-DMA beside B (oz_gram_la_kernel); 0: from L2 into registers (oz_gram_kernel,
+// the default). The LDS variant measured 14.42 ms per Gram launch against 13.62 ms at configs[1]
+// (profiles/r03_ab_gram.txt): the 120 KB ring allows one block per CU instead of two.
+#define OB_OZ_A_LDS 0
 #endif
 
 #define OZ_HIP(expr)                                                                                  \
@@ -613,7 +615,7 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   }
 }
 
-// ---- A through LDS (OB_OZ_A_LDS, the default) --------------------------------------------------
+// ---- A through LDS (OB_OZ_A_LDS=1, measured slower) ----------------------------------------------
 // Every operand arrives by LDS-DMA: per 64-row sub-tile a ring stage holds the 14 KB B image and
 // the block's 16 KB of A fragments (4 replicate batches x 4 x 1 KB), 30 one-KB pieces spread over
 // the 8 waves. The two waves of a batch (slice groups 0 and 1) read one copy of its A from LDS
