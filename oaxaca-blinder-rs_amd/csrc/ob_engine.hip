@@ -536,6 +536,53 @@ __device__ __forceinline__ void level2_draws(const GramArgs& a, const Work& w, u
   }
 }
 
+// Full tiles of the count kernel (OB_CNT_MAP): the whole calls of all 64 replicates form one list
+// that the block's waves walk in 64-call windows, window j on wave j mod 4. Call f's replicate and
+// its index among that replicate's calls come from an LDS call map (word f = index << 6 | r),
+// written by wave 0 when it publishes the tile's counts, instead of a per-window search over the
+// replicate boundaries. The part calls (m % 16 draws, one per replicate) form one extra window,
+// one lane per replicate. Same (call, replicate) -> draws as level2_draws, so the same counts.
+constexpr uint32_t kCallMapCap = 2048;  // whole calls of a (tile, batch) the map holds (mean 1024)
+
+__device__ __forceinline__ void level2_map_draws(const GramArgs& a, const Work& w, uint32_t tile, uint32_t* cnt,
+                                                 const uint32_t* mc, const uint32_t* cmap, uint32_t C, int wv,
+                                                 int lane) {
+  const uint32_t nwin = (C + 63u) >> 6;
+  const uint32_t c2 = (tile << 1) | w.g;
+  const uint32_t rep0 = a.first_rep + w.rep0;
+  const uint32_t one = 1u;
+  for (uint32_t win = (uint32_t)wv; win <= nwin; win += 4) {
+    if (win < nwin) {
+      const uint32_t f = win * 64u + (uint32_t)lane;
+      if (f < C) {
+        const uint32_t e = cmap[f], r = e & 63u, pp = e >> 6;
+        ob_u32x4 u;
+        if (a.diag & 64)  // timing ablation (OB_GRAM_DIAG 64): no Philox, wrong draws
+          u = ob_u32x4{pp * 0x9E3779B9u ^ r, pp * 0x85EBCA6Bu ^ c2, pp * 0xC2B2AE35u, pp ^ 0x27D4EB2Fu};
+        else
+          u = ob_philox_x3(pp, rep0 + r, c2, OB_TAG_L2, a.key0, a.key1);
+        if (a.diag & 32) {  // timing ablation (OB_GRAM_DIAG 32): no LDS atomics
+          if ((u.x ^ u.y ^ u.z ^ u.w) == 0x5EED5EEDu) cnt[r * kCntStride] = 1u;
+        } else {
+          const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i) add_draws_word(cnt, r * (kCntStride * 4), wd[i], one);
+        }
+      }
+    } else {  // the part calls
+      const uint32_t m = mc[lane], nd = m & 15u;
+      if (nd) {
+        const ob_u32x4 u = ob_philox_x3(m >> 4, rep0 + (uint32_t)lane, c2, OB_TAG_L2, a.key0, a.key1);
+        const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
+        uint32_t* row = cnt + lane * kCntStride;
+#pragma unroll
+        for (uint32_t d = 0; d < 15; ++d)
+          if (d < nd) add_draw(row, (wd[d >> 2] >> (8 * (d & 3))) & 0xFFu);
+      }
+    }
+  }
+}
+
 // A row drawn 256+ times wraps its byte and carries into the next one, which lowers the
 // replicate's byte sum below m: comparing sums with the level-1 counts is an exact check.
 // Four threads per replicate (consecutive lanes); thread my in [0, 256) holds replicate my >> 2's
@@ -587,10 +634,12 @@ __device__ __forceinline__ uint32_t level1_count(const GramArgs& a, uint32_t rep
 }
 
 __device__ __forceinline__ void publish_counts(const Work& w, uint32_t tile, uint32_t m, uint32_t* mc, uint32_t* cum,
-                                               int lane) {
+                                               int lane, uint32_t* cmap) {
   mc[lane] = m;
   // calls in the whole-call list: full tile floor(m/16) (the part call goes apart), else ceil(m/2)
-  uint32_t v = full_tile(w, tile) ? m >> 4 : (m + 1) >> 1;
+  const bool full = full_tile(w, tile);
+  const uint32_t c = full ? m >> 4 : (m + 1) >> 1;
+  uint32_t v = c;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
     const uint32_t t = __shfl_up(v, o);
@@ -598,6 +647,9 @@ __device__ __forceinline__ void publish_counts(const Work& w, uint32_t tile, uin
   }
   cum[lane + 1] = v;
   if (lane == 0) cum[0] = 0;
+  // the call map of a full tile (level2_map_draws), when the tile's calls fit it
+  if (cmap && full && (uint32_t)__builtin_amdgcn_readlane(v, 63) <= kCallMapCap)
+    for (uint32_t j = 0, f = v - c; j < c; ++j, ++f) cmap[f] = (j << 6) | (uint32_t)lane;
 }
 
 template <int CB>
@@ -625,6 +677,9 @@ __device__ __forceinline__ void store_partials(const GramArgs& a, const Work& w,
 // Gram kernel fetches a sub-tile with a plain LDS-DMA copy. Counts are drawn once per replicate
 // batch, whatever the number of column groups.
 // ---------------------------------------------------------------------------------------------
+#ifndef OB_CNT_MAP
+#define OB_CNT_MAP 1  // full tiles walk one call list through an LDS call map (level2_map_draws)
+#endif
 #ifndef OB_CNT_TILES
 #define OB_CNT_TILES 8  // tiles per count block (A/B builds: tools/build_alt.sh ... -DOB_CNT_TILES=n)
 #endif
@@ -637,6 +692,7 @@ template <bool I8>
 __global__ __launch_bounds__(kBlock) void ob_count_kernel(const GramArgs a) {
   __shared__ uint32_t img[64 * kCntStride];
   __shared__ uint32_t mcb[2][64], cumb[2][65];
+  __shared__ uint32_t cmap[OB_CNT_MAP ? kCallMapCap : 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   Work w{};
   w.rb = blockIdx.y;
@@ -657,11 +713,15 @@ __global__ __launch_bounds__(kBlock) void ob_count_kernel(const GramArgs a) {
     w.n = w.g ? a.n1 : a.n0;
     const uint32_t tile = tt - (w.g ? a.tiles0 : 0u);
     if (wave == 0) {
-      publish_counts(w, tile, m_next, mc, cum, lane);
+      publish_counts(w, tile, m_next, mc, cum, lane, OB_CNT_MAP ? cmap : nullptr);
       if (tt + 1 < tt1) m_next = level1_count(a, w.rep0, tt + 1, lane);
     }
     __syncthreads();
-    level2_draws(a, w, tile, img, mc, cum, 0, 1, wave, 4, lane);
+    const uint32_t C = cum[64];
+    if (OB_CNT_MAP && full_tile(w, tile) && C <= kCallMapCap)
+      level2_map_draws(a, w, tile, img, mc, cmap, C, wave, lane);
+    else
+      level2_draws(a, w, tile, img, mc, cum, 0, 1, wave, 4, lane);
     __syncthreads();
     const uint32_t ns = (min(OB_TILE_ROWS, w.n - tile * OB_TILE_ROWS) + 63) >> 6;
     check_store_counts<I8>(a, img, mc, tid, tt, w.rb, ns);
