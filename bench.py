@@ -570,6 +570,7 @@ def main():
     launches = 0
     stats = None
     gram_path = 1
+    tiles6 = (0, 0)
     for i in range(args.steps):
         s_, tm = step(args.warmup + i)
         stats = s_ if s_ is not None else stats
@@ -577,6 +578,7 @@ def main():
             sums[k_] += tm[k_]
         launches += tm["gram_launches"]
         gram_path = tm["gram_path"]
+        tiles6 = (tm["oz_tiles6"], tm["oz_tiles"])
     stats = drain() if rank == 0 else None  # the last step's aggregation, inside the timed region
     if dist:
         dist.barrier()
@@ -601,15 +603,19 @@ def main():
         traffic = load_traffic(args.rows, args.preds, per_rank, gram_path) if not taus else None
         if gram_path == 2:
             # exact integer-sliced Gram (ob_gram_i8.hip): the algorithmic work is one i8 multiply-add per
-            # (replicate, row, live pair, 7-bit digit); the MFMA work pads pairs to 32-wide column tiles
+            # (replicate, row, live pair, 8-bit digit slice run): 7 slices, 6 on the (chunk, column tile)
+            # blocks of narrow magnitude range (oz_tiles6 of oz_tiles); the MFMA work pads pairs to
+            # 32-wide column tiles
             pairs = (k + ny) * (k + ny + 1) // 2
-            ops_rep = 2.0 * args.rows * pairs * OZ_SLICES
-            ops_issued = 2.0 * args.rows * (-(-pairs // OZ_PAIRS_PER_TILE) * OZ_PAIRS_PER_TILE) * OZ_SLICES
+            slices = OZ_SLICES - (tiles6[0] / tiles6[1] if tiles6[1] else 0.0)
+            ops_rep = 2.0 * args.rows * pairs * slices
+            ops_issued = 2.0 * args.rows * (-(-pairs // OZ_PAIRS_PER_TILE) * OZ_PAIRS_PER_TILE) * slices
             i8_tops = ops_rep * reps_per_launch / (gram_launch_ms * 1e-3) / 1e12 if gram_launch_ms else 0.0
             roof = {"bound": "mfma", "achieved": i8_tops, "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS (i8)",
                     "frac": i8_tops / I8_MFMA_PEAK_TOPS, "traffic": traffic, "kernel": "oz_gram_kernel",
                     "avg_launch_ms": gram_launch_ms, "i8_ops_per_replicate": ops_rep,
-                    "i8_ops_issued_per_replicate": ops_issued,
+                    "i8_ops_issued_per_replicate": ops_issued, "digit_slices_mean": slices,
+                    "tiles_on_6_slices": list(tiles6),
                     "f64_equivalent_tflops": achieved, "f64_flops_per_replicate": flops_rep,
                     "f64_equivalent_x_of_f64_mfma_peak": achieved / F64_MFMA_PEAK_TFLOPS}
         else:
@@ -639,7 +645,8 @@ def main():
                        "replicates_per_step": total, "replicates_per_gpu_per_step": per_rank,
                        "parallelism": f"replicates sharded x{world}, engine RCCL all-gather (ob_boot_run_sharded_device)"},
             "roofline": roof,
-            "gram_path": "i8 MFMA (v_mfma_i32_16x16x64_i8), exact 7 x 8-bit digit slices (f64-equivalent)" if gram_path == 2 else "f64 MFMA",
+            "gram_path": ("i8 MFMA (v_mfma_i32_16x16x64_i8), 7 balanced 8-bit digit slices of a 54-bit fixed point, "
+                          "the last dropped on narrow-range tiles (DESIGN.md §5.0)") if gram_path == 2 else "f64 MFMA",
             # what a per-replicate row gather would have to stream: a rate, not a
             # roofline fraction -- the Gram reads each panel byte once per 256-replicate tile instead
             "gather_equivalent": {"algorithmic_bytes_per_replicate": bytes_rep,

@@ -172,6 +172,9 @@ typedef struct {
   int32_t oz_exceptions;     /* i8 Gram: exception rows, summed in f64 beside the integer Gram */
   int32_t oz_bits;           /* i8 Gram: a row is an exception when some |v_c| >= 2^oz_bits x its chunk's
                                 scale for column c (geometric mean over nonzero rows), or not finite */
+  int32_t oz_tiles6;         /* i8 Gram: (chunk, 32-pair column tile) blocks that run 6 of the 7 digit
+                                slices (pairs of narrow magnitude range) */
+  int32_t oz_tiles;          /* i8 Gram: all (chunk, column tile) blocks */
 } ob_timing;
 int ob_panel_last_timing(const ob_panel* panel, ob_timing* out);
 /* Synchronize the stream used by the last *_device call and collect its timings. */

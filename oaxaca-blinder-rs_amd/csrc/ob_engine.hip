@@ -152,7 +152,8 @@ __device__ __forceinline__ uint32_t ky_walk(ob_bitstream& s, const KyLds& L, int
 }
 
 // Work item q of the split of a node holding c draws (ob_spec.h, OBRS-2): a popcount word below
-// OB_KY_MIN_C draws, else one Knuth-Yao stream. rl = (round << 5) + level.
+// OB_KY_MIN_C draws, else one stream (one Knuth-Yao sample or the low popcount). rl = (round << 5)
+// + level.
 __device__ __forceinline__ uint32_t l1_split_item(uint32_t q, uint32_t c, uint32_t rep, uint32_t c2, uint32_t rl,
                                                   uint32_t k0, uint32_t k1, const KyLds& L,
                                                   const uint32_t* __restrict__ goff,
@@ -161,10 +162,9 @@ __device__ __forceinline__ uint32_t l1_split_item(uint32_t q, uint32_t c, uint32
   const uint32_t c4 = c >> 12;
   ob_bitstream s = {q << 12, rep, c2, OB_TAG_L1K + rl, k0, k1, 0u, 0u, 0u, 0u, 0u};
   if (q < c4) return ky_walk(s, L, OB_KY_TABLES - 1, goff, glist);
-  uint32_t left = 0;
-  for (int j = OB_KY_MAX_LOG - 1; j >= OB_KY_MIN_LOG; --j)
-    if ((c >> j) & 1u) left += ky_walk(s, L, j - OB_KY_MIN_LOG, goff, glist);
-  return left + ob_bs_popcount(s, c & 127u);
+  const uint32_t i = q - c4, nd = (uint32_t)__builtin_popcount((c >> 7) & 31u);
+  if (i < nd) return ky_walk(s, L, (int)ob_l1_digit_log(c, i) - OB_KY_MIN_LOG, goff, glist);
+  return ob_bs_popcount(s, c & 127u);
 }
 
 __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t n1, uint32_t tiles0,

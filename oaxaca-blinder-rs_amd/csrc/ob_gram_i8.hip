@@ -268,12 +268,15 @@ __device__ __forceinline__ void oz_stage(double* vs, int k1p, const double* cols
 // ex + kExpBias (atomicMax; 2^(ex-1) <= max |P| < 2^ex). Grid: the group's tiles.
 __global__ __launch_bounds__(256) void oz_pexp_kernel(const double* cols, int64_t ld, uint32_t n, int nxy,
                                                       int weighted, int k1, int e, int npp, const int32_t* tile_chunk,
-                                                      const int8_t* dev, const int32_t* meta, int32_t* raw) {
+                                                      const int8_t* dev, const int32_t* meta, int32_t* raw,
+                                                      unsigned long long* psum) {
   extern __shared__ __attribute__((aligned(16))) double ozs[];
   const int k1p = k1 | 1, tid = threadIdx.x;
   double* vs = ozs;               // [64][k1p]
   double* mx = ozs + 64 * k1p;    // [e]
-  uint8_t* pa = reinterpret_cast<uint8_t*>(mx + e);
+  int32_t* xs = reinterpret_cast<int32_t*>(mx + e);  // [e] exponent sums of the nonzero |P|
+  int32_t* xc = xs + e;                              // [e] their count
+  uint8_t* pa = reinterpret_cast<uint8_t*>(xc + e);
   uint8_t* pb = pa + e;
   const uint32_t tile = blockIdx.x;
   const int chunk = tile_chunk[tile], bits = meta[0];
@@ -283,6 +286,8 @@ __global__ __launch_bounds__(256) void oz_pexp_kernel(const double* cols, int64_
     pa[q] = (uint8_t)a;
     pb[q] = (uint8_t)b;
     mx[q] = 0.0;
+    xs[q] = 0;
+    xc[q] = 0;
   }
   for (int sub = 0; sub < 4; ++sub) {
     __syncthreads();
@@ -291,9 +296,21 @@ __global__ __launch_bounds__(256) void oz_pexp_kernel(const double* cols, int64_
     for (int q = tid; q < e; q += 256) {
       const int a = pa[q], b = pb[q];
       double m = mx[q];
+      int sx = 0, sc = 0;
 #pragma unroll 8
-      for (int r = 0; r < 64; ++r) m = fmax(m, fabs(vs[r * k1p + a] * vs[r * k1p + b]));
+      for (int r = 0; r < 64; ++r) {
+        const double P = fabs(vs[r * k1p + a] * vs[r * k1p + b]);
+        m = fmax(m, P);
+        if (P > 0.0) {
+          int ex = 0;
+          (void)frexp(P, &ex);
+          sx += ex;
+          ++sc;
+        }
+      }
       mx[q] = m;
+      xs[q] += sx;
+      xc[q] += sc;
     }
   }
   for (int q = tid; q < e; q += 256)
@@ -301,7 +318,47 @@ __global__ __launch_bounds__(256) void oz_pexp_kernel(const double* cols, int64_
       int ex = 0;
       (void)frexp(mx[q], &ex);
       atomicMax(&raw[(size_t)chunk * npp + q], ex + kExpBias);
+      atomicAdd(&psum[2 * ((size_t)chunk * npp + q)], (unsigned long long)(long long)xs[q]);
+      atomicAdd(&psum[2 * ((size_t)chunk * npp + q) + 1], (unsigned long long)xc[q]);
     }
+}
+
+// Digit slices per (chunk, column tile): 6 when every pair of the tile has a narrow range, else 7.
+// Dropping the last of the 7 balanced digits moves each product by at most 2^(E-47) (E: the pair's
+// chunk exponent, 2^(E-1) <= max |P| < 2^E). Summed over the chunk that is at most 2^(E-47) sum c,
+// against the f64 rounding bound n u sum c |P| (u = 2^-53) of summing the same terms in f64; with
+// 2^(r-1) <= (geometric mean of the nonzero |P|) <= their mean, r = floor(mean frexp exponent),
+// the ratio is at most 2^(E - r + 7) / n. A pair takes six digits when that is <= 1/4:
+// E - r <= floor(log2 n) - 9 (n = the group's rows); its seventh digit is then written as zero, so
+// its Gram entries do not depend on the other pairs of its tile (a multi-outcome panel's entries
+// equal the single-outcome panel's bitwise). A tile whose pairs all take six runs six slices.
+// force7 (OB_GRAM_DIGITS=7) keeps seven everywhere. pnsl: [chunk][pair]; nsl: [chunk][column tile].
+__global__ __launch_bounds__(256) void oz_nsl_kernel(const int32_t* pexp, const long long* psum, const uint32_t* chunks,
+                                                     uint32_t n0, uint32_t n1, int e, int n_ct, int npp, int n_chunks,
+                                                     int force7, uint8_t* pnsl, uint8_t* nsl, int32_t* meta) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n_chunks * n_ct) return;
+  const int chunk = i / n_ct, ct = i - chunk * n_ct;
+  const uint32_t n = chunks[3 * chunk] ? n1 : n0;
+  const int thr = n ? (31 - __builtin_clz(n)) - 9 : -1;
+  bool all6 = true;
+  for (int q = 0; q < kPairsPerTile; ++q) {
+    const int pair = ct * kPairsPerTile + q;
+    const size_t x = (size_t)chunk * npp + pair;
+    bool six = true;  // padding pairs and all-zero pairs are exact in any number of slices
+    if (pair < e) {
+      const long long sum = psum[2 * x], cnt = psum[2 * x + 1];
+      if (force7 || thr < 0) six = false;
+      else if (cnt > 0) {
+        const long long r = sum >= 0 ? sum / cnt : -((-sum + cnt - 1) / cnt);  // floor
+        six = (long long)pexp[x] - r <= thr;
+      }
+    }
+    pnsl[x] = six ? 6 : 7;
+    all6 = all6 && six;
+  }
+  nsl[i] = all6 ? 6 : 7;
+  if (all6) atomicAdd(&meta[5], 1);
 }
 
 __global__ __launch_bounds__(256) void oz_pexp_finish_kernel(int32_t* pexp, int count) {
@@ -315,7 +372,8 @@ __global__ __launch_bounds__(256) void oz_pexp_finish_kernel(int32_t* pexp, int 
 __global__ __launch_bounds__(256) void oz_digits_kernel(const double* cols, int64_t ld, uint32_t n, int nxy,
                                                         int weighted, int k1, int e, int n_ct, int n_pairs_pad,
                                                         const int32_t* tile_chunk, const int8_t* dev,
-                                                        const int32_t* meta, const int32_t* pexp, ob_v4i* B) {
+                                                        const int32_t* meta, const int32_t* pexp, const uint8_t* pnsl,
+                                                        ob_v4i* B) {
   extern __shared__ __attribute__((aligned(16))) double ozs[];
   const int k1p = k1 | 1;
   const uint32_t sub = blockIdx.x;
@@ -329,6 +387,7 @@ __global__ __launch_bounds__(256) void oz_digits_kernel(const double* cols, int6
     const bool live = pair < e;
     if (live) oz_pair_cols(pair, k1, &a, &b);
     const int E = live ? pexp[(size_t)chunk * n_pairs_pad + pair] : 0;
+    const bool six = live && pnsl[(size_t)chunk * n_pairs_pad + pair] == 6;  // digit 6 written as zero
     const double* v0 = ozs + 16 * (lane >> 4) * k1p;
     long long m[16];
 #pragma unroll
@@ -346,6 +405,7 @@ __global__ __launch_bounds__(256) void oz_digits_kernel(const double* cols, int6
         w[j >> 2] |= (uint32_t)(uint8_t)d << (8 * (j & 3));
         m[j] = (m[j] - d) >> 8;
       }
+      if (sl == kS - 1 && six) w[0] = w[1] = w[2] = w[3] = 0u;
       dst[sl * 128] = (ob_v4i){(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
     }
   }
@@ -405,6 +465,7 @@ struct OzArgs {
   const ob_v4i* counts;    // I8 count images (ob_count_kernel<true>): [tile][batch][1024 units]
   const uint32_t* chunks;  // [chunk][3] = (group, first tile, end tile)
   const int32_t* pexp;     // [chunk][n_pairs_pad]
+  const uint8_t* nsl;      // [chunk][column tile]: 6 or 7 digit slices (oz_nsl_kernel)
   double* partial;         // [chunk][rep_pad][e_pad]
   uint32_t n0, n1, tiles0, nb_rep, n_reps, rep_pad, n_rt;
   int n_ct, e_pad, n_pairs_pad;
@@ -805,12 +866,17 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
   const uint32_t nwg = gridDim.x, bid = blockIdx.x;
   const uint32_t xcd = bid & 7u, slot = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7u;
   const uint32_t wi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
-  const uint32_t rt = (wi / (uint32_t)a.n_ct) % a.n_rt;
+  const uint32_t tq = wi / (uint32_t)a.n_ct, rt = tq % a.n_rt, chunk = tq / a.n_rt;
   const bool live = rt * 4u + (uint32_t)(wave & 3) < a.nb_rep;
-  // waves 0-3: slices 0-3, two B pieces; 4-5: slices 4-6, two B pieces; 6-7: slices 4-6, one piece
+  const bool six = a.nsl[chunk * (uint32_t)a.n_ct + wi % (uint32_t)a.n_ct] == 6;
+  // waves 0-3: slices 0-3, two B pieces; 4-5: slices 4-6, two B pieces; 6-7: slices 4-6, one piece.
+  // Six slices: waves 4-7 take slices 4-5, one piece each; pieces 12-13 (slice 6) are not loaded.
   if (wave < 4) {
     if (live) oz_gram_body<kSlo, 2, true, DIAG>(a, smem, wave);
     else oz_gram_body<kSlo, 2, false, DIAG>(a, smem, wave);
+  } else if (six) {
+    if (live) oz_gram_body<kS - kSlo - 1, 1, true, DIAG>(a, smem, wave);
+    else oz_gram_body<kS - kSlo - 1, 1, false, DIAG>(a, smem, wave);
   } else if (wave < 6) {
     if (live) oz_gram_body<kS - kSlo, 2, true, DIAG>(a, smem, wave);
     else oz_gram_body<kS - kSlo, 2, false, DIAG>(a, smem, wave);
@@ -856,6 +922,9 @@ int oz_prepare(ob_panel* p, hipStream_t s) {
     p->oz_tile_chunk[g].assign(std::max(p->ntiles[g], 1u), 0);
   }
   if (!p->d_oz_pexp) OZ_HIP(hipMalloc(&p->d_oz_pexp, sizeof(int32_t) * (size_t)n_chunks * npp));
+  if (!p->d_oz_psum) OZ_HIP(hipMalloc(&p->d_oz_psum, sizeof(int64_t) * 2 * (size_t)n_chunks * npp));
+  if (!p->d_oz_nsl) OZ_HIP(hipMalloc(&p->d_oz_nsl, (size_t)n_chunks * n_ct));
+  if (!p->d_oz_pnsl) OZ_HIP(hipMalloc(&p->d_oz_pnsl, (size_t)n_chunks * npp));
   if (!p->d_oz_acc) OZ_HIP(hipMalloc(&p->d_oz_acc, sizeof(int64_t) * 2 * (size_t)n_chunks * p->k1));
   if (!p->d_oz_meta) OZ_HIP(hipMalloc(&p->d_oz_meta, sizeof(int32_t) * kMetaWords));
   if (!p->d_oz_exc) OZ_HIP(hipMalloc(&p->d_oz_exc, sizeof(uint32_t) * kOzExcCap));
@@ -872,6 +941,7 @@ int oz_prepare(ob_panel* p, hipStream_t s) {
   OZ_HIP(hipMemsetAsync(p->d_oz_acc, 0, sizeof(int64_t) * 2 * (size_t)n_chunks * p->k1, s));
   OZ_HIP(hipMemsetAsync(p->d_oz_meta, 0, sizeof(int32_t) * kMetaWords, s));
   OZ_HIP(hipMemsetAsync(p->d_oz_pexp, 0, sizeof(int32_t) * (size_t)n_chunks * npp, s));
+  OZ_HIP(hipMemsetAsync(p->d_oz_psum, 0, sizeof(int64_t) * 2 * (size_t)n_chunks * npp, s));
   OZ_HIP(hipMemsetAsync(p->d_oz_exc, 0xFF, sizeof(uint32_t) * kOzExcCap, s));
   const int nxy = p->p + p->n_y;
   const double* cols[2] = {p->d_cols[0], p->d_cols[1]};
@@ -904,7 +974,7 @@ int oz_prepare(ob_panel* p, hipStream_t s) {
                      p->d_oz_excp);
   OZ_HIP(hipGetLastError());
   const int k1p = p->k1 | 1;
-  const size_t lds_pexp = sizeof(double) * ((size_t)64 * k1p + p->e) + 2 * (size_t)p->e;
+  const size_t lds_pexp = sizeof(double) * ((size_t)64 * k1p + p->e) + (2 * sizeof(int32_t) + 2) * (size_t)p->e;
   const size_t lds_dig = sizeof(double) * (size_t)64 * k1p;
   OZ_HIP(hipFuncSetAttribute((const void*)oz_pexp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_pexp));
   OZ_HIP(hipFuncSetAttribute((const void*)oz_digits_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dig));
@@ -912,19 +982,30 @@ int oz_prepare(ob_panel* p, hipStream_t s) {
     if (p->ntiles[g]) {
       hipLaunchKernelGGL(oz_pexp_kernel, dim3(p->ntiles[g]), dim3(256), lds_pexp, s, cols[g], p->ld[g], p->n[g], nxy,
                          p->weighted, p->k1, p->e, npp, (const int32_t*)p->d_oz_tile_chunk[g],
-                         (const int8_t*)p->d_oz_dev[g], (const int32_t*)p->d_oz_meta, p->d_oz_pexp);
+                         (const int8_t*)p->d_oz_dev[g], (const int32_t*)p->d_oz_meta, p->d_oz_pexp,
+                         reinterpret_cast<unsigned long long*>(p->d_oz_psum));
       OZ_HIP(hipGetLastError());
     }
   const int npe = n_chunks * npp;
   hipLaunchKernelGGL(oz_pexp_finish_kernel, dim3((npe + 255) / 256), dim3(256), 0, s, p->d_oz_pexp, npe);
   OZ_HIP(hipGetLastError());
+  static const int force7 = [] {
+    const char* e = getenv("OB_GRAM_DIGITS");
+    return e && atoi(e) == 7 ? 1 : 0;
+  }();
+  const int nct_all = n_chunks * n_ct;
+  hipLaunchKernelGGL(oz_nsl_kernel, dim3((nct_all + 255) / 256), dim3(256), 0, s, (const int32_t*)p->d_oz_pexp,
+                     (const long long*)p->d_oz_psum, (const uint32_t*)p->d_chunks, p->n[0], p->n[1], p->e, n_ct, npp,
+                     n_chunks, force7, p->d_oz_pnsl, p->d_oz_nsl, p->d_oz_meta);
+  OZ_HIP(hipGetLastError());
+  p->oz_tiles = nct_all;
   for (int g = 0; g < 2; ++g) {
     const uint32_t nsub = (uint32_t)(p->ld[g] >> 6);
     if (p->ntiles[g] == 0 || nsub == 0) continue;
     hipLaunchKernelGGL(oz_digits_kernel, dim3(nsub), dim3(256), lds_dig, s, cols[g], p->ld[g], p->n[g], nxy,
                        p->weighted, p->k1, p->e, n_ct, npp, (const int32_t*)p->d_oz_tile_chunk[g],
                        (const int8_t*)p->d_oz_dev[g], (const int32_t*)p->d_oz_meta, (const int32_t*)p->d_oz_pexp,
-                       reinterpret_cast<ob_v4i*>(p->d_oz_b[g]));
+                       (const uint8_t*)p->d_oz_pnsl, reinterpret_cast<ob_v4i*>(p->d_oz_b[g]));
     OZ_HIP(hipGetLastError());
   }
   OZ_HIP(hipEventRecord(p->oz_ev[1], s));
@@ -958,14 +1039,17 @@ int oz_collect(ob_panel* p) {
     p->oz_timed = false;
   }
   if (p->oz_nexc < 0) {
-    int32_t meta[4] = {0, 0, 0, 0};
+    int32_t meta[6] = {0, 0, 0, 0, 0, 0};
     OZ_HIP(hipMemcpy(meta, p->d_oz_meta, sizeof(meta), hipMemcpyDeviceToHost));
     p->oz_bits = meta[0];
     p->oz_nexc = meta[1];
     p->oz_overflow = meta[3] != 0;
+    p->oz_tiles6 = meta[5];
   }
   p->timing.oz_bits = p->oz_bits;
   p->timing.oz_exceptions = p->oz_nexc;
+  p->timing.oz_tiles6 = p->oz_tiles6;
+  p->timing.oz_tiles = p->oz_tiles;
   if (p->oz_overflow)
     return ob::fail(OB_E_UNSUPPORTED, "more than %d rows hold non-finite values (NaN or inf); the i8 Gram keeps at most "
                                       "that many exception rows (OB_GRAM_PATH=f64 runs the f64 MFMA Gram)",
@@ -980,6 +1064,9 @@ void oz_free(ob_panel* p) {
     (void)hipFree(p->d_oz_tile_chunk[g]);
   }
   (void)hipFree(p->d_oz_pexp);
+  (void)hipFree(p->d_oz_psum);
+  (void)hipFree(p->d_oz_nsl);
+  (void)hipFree(p->d_oz_pnsl);
   (void)hipFree(p->d_oz_acc);
   (void)hipFree(p->d_oz_meta);
   (void)hipFree(p->d_oz_exc);
@@ -998,6 +1085,7 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
   a.counts = reinterpret_cast<const ob_v4i*>(counts);
   a.chunks = d_chunks;
   a.pexp = p->d_oz_pexp;
+  a.nsl = p->d_oz_nsl;
   a.partial = partial;
   a.n0 = p->n[0];
   a.n1 = p->n[1];

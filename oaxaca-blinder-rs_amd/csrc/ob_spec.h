@@ -102,9 +102,10 @@ OB_HD ob_u32x4 ob_philox_x3(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, 
 // probabilities p_k = C(n, k) / 2^n: column i = 1 .. n of the tree holds the k whose bit n - i of
 // C(n, k) is set, in ascending k (list[off[i] .. off[i+1])); the walk reads one stream bit per
 // column, d = 2 d + bit, returns the d-th entry when d < the column's count and subtracts the
-// count otherwise. Exact, ~H + 2 ~ 9 bits per sample. Streams: q < c >> 12 carries B(4096) sample
-// q, stream c >> 12 the B(2^j), j = 11 .. 7, then the popcount bits; bit b of stream q is bit
-// (b & 31) of word ((b >> 5) & 3) of Philox({q << 12 | b >> 7, rep, c2, tag}).
+// count otherwise. Exact, ~H + 2 ~ 9 bits per sample. Streams, one sample each: q < c >> 12 carries
+// B(4096) sample q, the next ones one B(2^j) per set bit j = 11 .. 7 (high to low), the last, when
+// c & 127 != 0, the c & 127 popcount bits; bit b of stream q is bit (b & 31) of word ((b >> 5) & 3)
+// of Philox({q << 12 | b >> 7, rep, c2, tag}).
 #define OB_KY_MIN_LOG 7
 #define OB_KY_MAX_LOG 12
 #define OB_KY_TABLES (OB_KY_MAX_LOG - OB_KY_MIN_LOG + 1)
@@ -138,9 +139,22 @@ OB_HD uint32_t ob_l1_split_bits(uint32_t q, uint32_t c, uint32_t rep, uint32_t c
   return s;
 }
 
-// Work items of a node's split: popcount words below OB_KY_MIN_C, else c >> 12 B(4096) streams plus
-// the stream of the low digits.
-OB_HD uint32_t ob_l1_items(uint32_t c) { return c < OB_KY_MIN_C ? (c + 127u) >> 7 : (c >> 12) + 1u; }
+// Work items of a node's split: popcount words below OB_KY_MIN_C, else its streams (c >> 12 of
+// B(4096), one per set bit 11 .. 7, one for the popcount of c & 127 when nonzero).
+OB_HD uint32_t ob_l1_items(uint32_t c) {
+  return c < OB_KY_MIN_C ? (c + 127u) >> 7
+                         : (c >> 12) + (uint32_t)__builtin_popcount((c >> 7) & 31u) + ((c & 127u) ? 1u : 0u);
+}
+// Stream i (< the digit streams) after the B(4096) ones: the table exponent j of the i-th set bit of
+// c among bits 11 .. 7, high to low.
+OB_HD uint32_t ob_l1_digit_log(uint32_t c, uint32_t i) {
+  uint32_t j = OB_KY_MAX_LOG - 1;
+  for (;; --j)
+    if ((c >> j) & 1u) {
+      if (i == 0) return j;
+      --i;
+    }
+}
 
 // A node stream: bit b is bit (b & 31) of word ((b >> 5) & 3) of Philox({ctr0 | b >> 7, rep, c2, tag}).
 struct ob_bitstream {

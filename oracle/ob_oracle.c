@@ -78,8 +78,9 @@ static inline uint64_t orc_draw_u64(const uint32_t w[4], int odd) {
  * generating tree) over the exact dyadic probabilities C(2^j, k) / 2^(2^j): ~9 random bits per
  * sample instead of 2^j. Bits come from per-node streams: stream q has bit b = bit (b & 31) of
  * word ((b >> 5) & 3) of Philox({(q << 12) | (b >> 7), rep, (k << 1) | g, ORC_TAG_L1K + rl});
- * stream q < c >> 12 carries B(4096) sample q, stream c >> 12 the B(2^j), j = 11 down to 7, then
- * the c & 127 popcount bits. (OBRS-1 used the popcount at every node: ~5.5M bits per group and
+ * stream q < c >> 12 carries B(4096) sample q; the next streams carry one B(2^j) each, for the set
+ * bits j = 11 down to 7 in that order; the last one, when c & 127 != 0, the c & 127 popcount bits.
+ * One sample per stream, so the samples of a node are independent work items. (OBRS-1 used the popcount at every node: ~5.5M bits per group and
  * replicate at 500k rows, ~2.5M of them at nodes of 4096 draws or more.) */
 #define ORC_TAG_L1T 0x4C310000u /* OBRS-1 "L1" + (round << 5) + level (superseded) */
 #define ORC_TAG_L1K 0x4B310000u /* OBRS-2 "K1" + (round << 5) + level */
@@ -187,16 +188,19 @@ static uint32_t orc_split_left(uint32_t c, uint32_t rep, uint32_t g, uint32_t k,
         return left;
     }
     pthread_once(&orc_ky_once, orc_ky_init);
-    const uint32_t c4 = c >> 12;
-    for (uint32_t q = 0; q <= c4; ++q) {
+    uint32_t q = 0;
+    for (; q < (c >> 12); ++q) { /* one B(4096) sample per stream */
         orc_bits s = {{q << 12, rep, c2, ORC_TAG_L1K + rl}, key, 0, {0, 0, 0, 0}};
-        if (q < c4) {
-            left += orc_ky_sample(&s, &orc_ky_tab[12]);
-        } else {
-            for (uint32_t j = 11; j >= 7; --j)
-                if ((c >> j) & 1u) left += orc_ky_sample(&s, &orc_ky_tab[j]);
-            for (uint32_t i = 0; i < (c & 127u); ++i) left += orc_bit(&s);
+        left += orc_ky_sample(&s, &orc_ky_tab[12]);
+    }
+    for (uint32_t j = 11; j >= 7; --j) /* then one stream per set bit j of c, high to low */
+        if ((c >> j) & 1u) {
+            orc_bits s = {{q++ << 12, rep, c2, ORC_TAG_L1K + rl}, key, 0, {0, 0, 0, 0}};
+            left += orc_ky_sample(&s, &orc_ky_tab[j]);
         }
+    if (c & 127u) { /* and the popcount of c & 127 fair bits */
+        orc_bits s = {{q << 12, rep, c2, ORC_TAG_L1K + rl}, key, 0, {0, 0, 0, 0}};
+        for (uint32_t i = 0; i < (c & 127u); ++i) left += orc_bit(&s);
     }
     return left;
 }

@@ -61,6 +61,32 @@ def test_i8_gram_equals_f64_gram(ob, O, n, p, weighted, ny):
         panel.close()
 
 
+def test_i8_gram_six_slices(ob, O):
+    """Tiles whose pairs all have a narrow magnitude range run 6 of the 7 digit slices
+    (oz_nsl_kernel); their Gram still agrees with the f64 Gram to 1e-12 of sqrt(G_aa G_bb).
+    A heavy-tailed column keeps the tiles holding its pairs on 7 slices."""
+    d = O.synthetic_panel(400_000, 20, True, seed=5)
+    rng = np.random.default_rng(5)
+    for heavy in (False, True):
+        xa, xb = d["xa"].copy(), d["xb"].copy()
+        if heavy:
+            xa[:, 4] = np.exp(rng.normal(0.0, 1.5, xa.shape[0]))
+            xb[:, 4] = np.exp(rng.normal(0.0, 1.5, xb.shape[0]))
+        panel = ob.Panel(xa, d["ya"], xb, d["yb"], d["wa"], d["wb"])
+        try:
+            g64 = panel.debug_gram(SEED, 3, 64, path=1)
+            g8 = panel.debug_gram(SEED, 3, 64, path=2)
+            t = panel.timing()
+            assert t["gram_path"] == 2 and t["oz_tiles"] > 0
+            if heavy:
+                assert 0 < t["oz_tiles6"] < t["oz_tiles"], (t["oz_tiles6"], t["oz_tiles"])
+            else:
+                assert t["oz_tiles6"] == t["oz_tiles"], (t["oz_tiles6"], t["oz_tiles"])
+            assert _check_gram(g8, g64, 22) < 1e-12
+        finally:
+            panel.close()
+
+
 def test_i8_rows_equal_f64_rows(ob, O):
     """Default (i8) rows vs OB_GRAM_PATH=f64 rows, all reference modes, with dummies."""
     d = O.synthetic_panel(12000, 6, True, seed=4)
