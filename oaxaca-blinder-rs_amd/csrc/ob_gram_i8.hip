@@ -14,6 +14,8 @@
 // each inner sum an exact int32 (|c| <= 127, |d| <= 128, sum_i c_i <= n_g < 2^24 (oz_prepare), so
 // |sum| < 2^31). The slices meet in int64, two f64 roundings per chunk partial, so the Gram
 // equals the f64 MFMA Gram to ~1e-15 relative (tests/test_gpu_gram_i8.py holds it to 1e-12).
+// Pairs of narrow magnitude range take six digits (the seventh written as zero, oz_nsl_kernel:
+// error bound below a quarter of an f64 summation's), and column tiles of such pairs run 6 slices.
 //
 // v_mfma_i32_16x16x64_i8 issues in 16 cycles like v_mfma_f32_16x16x32_bf16 (MI355X_MICROARCH.md,
 // Matrix cores): 64x the f64 MFMA rate, so 7 slices cost 7x the f64 multiply count and still
