@@ -167,6 +167,9 @@ __device__ __forceinline__ uint32_t l1_split_item(uint32_t q, uint32_t c, uint32
   return ob_bs_popcount(s, c & 127u);
 }
 
+// DIAG (OB_L1_DIAG, timing ablations only, wrong counts): 1 no random bits (left = c / 2),
+// 2 one round only, 4 no Knuth-Yao staging, 8 no m1 stores, 16 return after the staging barrier.
+template <int DIAG>
 __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t n1, uint32_t tiles0,
                                                            uint32_t first_rep, uint32_t stride,
                                                            uint32_t key0, uint32_t key1, uint32_t* m1,
@@ -177,7 +180,12 @@ __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t
   const uint32_t g = blockIdx.y, rl = blockIdx.x, rep = first_rep + rl, tid = threadIdx.x;
   const uint32_t n = g ? n1 : n0;
   if (n == 0) return;
-  ky_stage(kyl, ky_g, tid);  // published by the first barrier of the round loop
+  if constexpr (!(DIAG & 4)) ky_stage(kyl, ky_g, tid);  // published by the first barrier of the round loop
+  if constexpr ((DIAG & 16) != 0) {
+    __syncthreads();
+    if (tid == 0 && kyl.hlist[7] == 0xFFFFu) m1[0] = 0u;  // keeps the staging
+    return;
+  }
   const uint32_t T = (n + OB_TILE_ROWS - 1) >> OB_TILE_SHIFT, D = l1_depth(T), J = l1_top_levels(T);
   const uint32_t tail = n - (T - 1) * OB_TILE_ROWS;
   const bool small = l1_small(T), partial = tail < OB_TILE_ROWS;
@@ -200,6 +208,7 @@ __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t
     uint32_t rej = 0;
     // large T, round r: tile t of the last split gets c (tail tile: parked for acceptance)
     auto emit = [&](uint32_t t, uint32_t c) {
+      if constexpr ((DIAG & 8) != 0) return;
       if (partial && t == T - 1) s_tail = c;
       else if (round == 0) mcol[t] = c;
       else if (c) mcol[t] += c;
@@ -219,8 +228,10 @@ __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t
           const uint32_t c = cur[k];
           uint32_t left = 0;
           const uint32_t ns = c ? ob_l1_items(c) : 0u;
-          for (uint32_t q = j; q < ns; q += 1u << sh)
-            left += l1_split_item(q, c, rep, ((kb + k) << 1) | g, rl, key0, key1, kyl, ky_g.off, ky_g.list);
+          if constexpr (DIAG & 1) left = j == 0 ? c >> 1 : 0u;
+          else
+            for (uint32_t q = j; q < ns; q += 1u << sh)
+              left += l1_split_item(q, c, rep, ((kb + k) << 1) | g, rl, key0, key1, kyl, ky_g.off, ky_g.list);
           if (left) atomicAdd(&nxt[2 * k], left);
         }
         __syncthreads();
@@ -236,8 +247,10 @@ __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t
           const uint32_t c = cur[k], kg = kb + k;
           uint32_t left = 0;
           const uint32_t ns = c ? ob_l1_items(c) : 0u;
-          for (uint32_t q = 0; q < ns; ++q)
-            left += l1_split_item(q, c, rep, (kg << 1) | g, rl, key0, key1, kyl, ky_g.off, ky_g.list);
+          if constexpr (DIAG & 1) left = c >> 1;
+          else
+            for (uint32_t q = 0; q < ns; ++q)
+              left += l1_split_item(q, c, rep, (kg << 1) | g, rl, key0, key1, kyl, ky_g.off, ky_g.list);
           const uint32_t right = c - left;
           if (to_m1) {
             emit(2 * kg, left);
@@ -305,8 +318,15 @@ __global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t
     todo = s_rej;
     __syncthreads();
     if (todo <= OB_L1_DIRECT) break;
+    if constexpr ((DIAG & 2) != 0) {
+      todo = 0;
+      break;
+    }
   }
-  if (!small) __threadfence();
+  // The direct draws' global atomics (L2) add to m1 words other threads of this block stored:
+  // __syncthreads() waits for this wave's stores (vmcnt(0)) before the barrier, which is all the
+  // ordering a block on one CU needs. A device-scope __threadfence() here compiled to an L2
+  // write-back and invalidate per block (buffer_wbl2 / buffer_inv): 1.6 of the kernel's 3.4 ms.
   __syncthreads();
   if (tid < todo) {  // direct draws: Lemire over [0, n)
     const uint32_t thresh = (0u - n) % n;
@@ -1556,10 +1576,10 @@ int engine_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_rep
   HIP_OK(hipMemsetAsync(p->d_flags, 0, sizeof(uint32_t), s));
   const uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
   const size_t lds_l1 = sizeof(uint32_t) * std::max(l1_lds_words(p->ntiles[0]), l1_lds_words(p->ntiles[1]));
-  HIP_OK(hipFuncSetAttribute((const void*)ob_level1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_l1));
+  HIP_OK(hipFuncSetAttribute((const void*)ob_level1_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_l1));
   ob_ky_tables ky{};
   OB_TRY(ky_device(p->ctx->device, &ky));
-  hipLaunchKernelGGL(ob_level1_kernel, dim3(n_reps, 2), dim3(kBlock), lds_l1, s, p->n[0], p->n[1], p->ntiles[0],
+  hipLaunchKernelGGL(ob_level1_kernel<0>, dim3(n_reps, 2), dim3(kBlock), lds_l1, s, p->n[0], p->n[1], p->ntiles[0],
                      (uint32_t)first_rep, tiles, key0, key1, p->d_m1, ky);
   HIP_OK(hipGetLastError());
   GramArgs ga = gram_args(p, pl);
@@ -1628,7 +1648,20 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   const size_t lds_l1 = sizeof(uint32_t) * std::max(l1_lds_words(p->ntiles[0]), l1_lds_words(p->ntiles[1]));
   ob_ky_tables ky{};
   OB_TRY(ky_device(ctx->device, &ky));
-  HIP_OK(hipFuncSetAttribute((const void*)ob_level1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_l1));
+  static const int l1_diag = [] {
+    const char* e = getenv("OB_L1_DIAG");
+    return e ? atoi(e) & 31 : 0;
+  }();
+  using L1Kernel = void (*)(uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t*,
+                            const ob_ky_tables);
+  const L1Kernel l1k = l1_diag == 0    ? ob_level1_kernel<0>
+                       : l1_diag == 1  ? ob_level1_kernel<1>
+                       : l1_diag == 3  ? ob_level1_kernel<3>
+                       : l1_diag == 11 ? ob_level1_kernel<11>
+                       : l1_diag == 16 ? ob_level1_kernel<16>
+                       : l1_diag == 20 ? ob_level1_kernel<20>
+                                       : ob_level1_kernel<0>;
+  HIP_OK(hipFuncSetAttribute((const void*)l1k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_l1));
   HIP_OK(hipFuncSetAttribute((const void*)ob_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)solve_lds_bytes(p)));
   p->timing.chunks = nch;
@@ -1651,7 +1684,7 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     hipEvent_t* ev = p->seg_events.data() + kSegEvents * (size_t)p->pending_segments;
     const bool timed = true;
     if (timed) HIP_OK(hipEventRecord(ev[0], s));
-    hipLaunchKernelGGL(ob_level1_kernel, dim3(ns, 2), dim3(kBlock), lds_l1, s, p->n[0], p->n[1], p->ntiles[0], frep,
+    hipLaunchKernelGGL(l1k, dim3(ns, 2), dim3(kBlock), lds_l1, s, p->n[0], p->n[1], p->ntiles[0], frep,
                        tiles, key0, key1, p->d_m1, ky);
     HIP_OK(hipGetLastError());
     if (timed) HIP_OK(hipEventRecord(ev[1], s));
