@@ -603,6 +603,9 @@ __device__ __forceinline__ void level2_map_draws(const GramArgs& a, const Work& 
   }
 }
 
+#ifndef OB_CNT_NT
+#define OB_CNT_NT 0  // 1: the i8 count images are written with nontemporal stores
+#endif
 // A row drawn 256+ times wraps its byte and carries into the next one, which lowers the
 // replicate's byte sum below m: comparing sums with the level-1 counts is an exact check.
 // Four threads per replicate (consecutive lanes); thread my in [0, 256) holds replicate my >> 2's
@@ -631,7 +634,15 @@ __device__ __forceinline__ void check_store_counts(const GramArgs& a, uint32_t* 
       uint4* out = reinterpret_cast<uint4*>(const_cast<uint32_t*>(a.counts)) + ((size_t)tt * a.nb_rep + rb) * 1024 +
                    part * 256 + (r >> 4) * 64 + (r & 15);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) out[q * 16] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+      for (int q = 0; q < 4; ++q) {
+        if (OB_CNT_NT) {
+          typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+          const u32x4_t u4 = {v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+          __builtin_nontemporal_store(u4, reinterpret_cast<u32x4_t*>(out + q * 16));
+        } else {
+          out[q * 16] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+        }
+      }
     } else {
       uint32_t* out = const_cast<uint32_t*>(a.counts) + ((size_t)tt * a.nb_rep + rb) * 4 * kCimgWords +
                       part * kCimgWords + r * kCimgStride;

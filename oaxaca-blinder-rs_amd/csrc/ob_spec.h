@@ -34,7 +34,9 @@
 #define OB_TILE_SHIFT 8u
 #define OB_TAG_L1T 0x4C310000u /* "L1" + (round << 5) + level: popcount bits of node k (c < 4096), {q, rep, 2k | g} */
 #define OB_TAG_L1K 0x4B310000u /* "K1" + (round << 5) + level: KY streams of node k (c >= 4096), {q << 12 | call, rep, 2k | g} */
+#ifndef OB_KY_MIN_C
 #define OB_KY_MIN_C 4096u      /* a node of at least this many draws splits by Knuth-Yao samples */
+#endif
 #define OB_TAG_L1S 0x4C530000u /* "LS" + round: partial-tile acceptance bytes, {q, rep, g} */
 #define OB_TAG_L1D 0x4C440000u /* "LD" + (j >> 2): direct draw r, attempt j, {r, rep, g} */
 #define OB_L1_DIRECT 256u      /* rejected draws at most this many are drawn directly */
@@ -65,8 +67,8 @@ OB_HD ob_u32x4 ob_philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uin
 
 // The same function with each three-way xor as one v_bitop3_b32 (truth table 0x96) on gfx950,
 // where the compiler otherwise emits two v_xor_b32 per output word. The level-2 count kernel
-// draws with it (4.78 -> 4.48 ms at configs[1]); level 1 measured slower with it (3.38 -> 3.49 ms,
-// its unrolling changes), so it keeps ob_philox. Identical outputs by construction.
+// draws with it (4.78 -> 4.48 ms at configs[1]), level 1's streams too (OB_L1_PHILOX). Identical
+// outputs by construction.
 OB_HD uint32_t ob_xor3(uint32_t a, uint32_t b, uint32_t c) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -94,6 +96,12 @@ OB_HD ob_u32x4 ob_philox_x3(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, 
 }
 
 // ---- OBRS-2 level-1 split ---------------------------------------------------------------------
+#ifndef OB_L1_PHILOX
+// the level-1 streams' Philox: ob_philox_x3, the same function with bitop3 xors (2.19 -> 2.03 ms per
+// level-1 launch at configs[1], tools/ab_libs.sh; ob_philox measured faster before the level-1
+// kernel lost its per-block L2 write-back)
+#define OB_L1_PHILOX ob_philox_x3
+#endif
 // Binomial(c, 1/2) of a node with c < OB_KY_MIN_C draws: the popcount of c fair bits (OBRS-1's
 // split, ob_l1_split_bits). From OB_KY_MIN_C up, the sum of exact B(2^j, 1/2) samples over the binary
 // digits of c: c >> 12 samples of B(4096), one B(2^j) per set bit j = 11 .. 7, and the popcount of
@@ -128,7 +136,7 @@ struct ob_ky_tables {
 // draws): bit b is bit (b & 31) of word ((b >> 5) & 3) of Philox({b >> 7, rep, c2, tag}).
 OB_HD uint32_t ob_l1_split_bits(uint32_t q, uint32_t c, uint32_t rep, uint32_t c2, uint32_t tag, uint32_t k0,
                                 uint32_t k1) {
-  const ob_u32x4 u = ob_philox(q, rep, c2, tag, k0, k1);
+  const ob_u32x4 u = OB_L1_PHILOX(q, rep, c2, tag, k0, k1);
   const uint32_t r = c - 128u * q;
   const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
   uint32_t s = 0;
@@ -165,7 +173,7 @@ struct ob_bitstream {
 
 OB_HD uint32_t ob_bs_word(ob_bitstream& s) {  // the 32-bit word holding bit s.pos (refilled per 128 bits)
   if ((s.pos & 127u) == 0) {
-    const ob_u32x4 u = ob_philox(s.ctr0 | (s.pos >> 7), s.rep, s.c2, s.tag, s.k0, s.k1);
+    const ob_u32x4 u = OB_L1_PHILOX(s.ctr0 | (s.pos >> 7), s.rep, s.c2, s.tag, s.k0, s.k1);
     s.w0 = u.x;
     s.w1 = u.y;
     s.w2 = u.z;
