@@ -53,6 +53,10 @@ constexpr int kFracBits = 54;          // m = rint(P 2^(kFracBits - E))
 constexpr int kPairsPerTile = 32;      // pairs per column tile (one 32-wide MFMA column block)
 constexpr int kSubUnits = kS * 2 * 64; // 16-byte units of one (sub-tile, column tile) B image (14 KB)
 constexpr int kSlo = 4;                // slices of slice group 0 (waves 0-3); group 1 has kS - kSlo
+#ifndef OB_OZ_SIX0
+#define OB_OZ_SIX0 4
+#endif
+constexpr int kSix0 = OB_OZ_SIX0;      // six-slice blocks: slices of group 0 (group 1: 6 - kSix0)
 #ifndef OB_OZ_A_NT
 // A fragments by ordinary loads, so that the 8 column-tile blocks of a (chunk, replicate tile),
 // which run together on one XCD, share them through its L2. Nontemporal loads (OB_OZ_A_NT=1,
@@ -522,13 +526,13 @@ __device__ __forceinline__ void oz_mfmas(ob_v4i (&acc)[4][kSlo][2], int h, const
 // an A fragment holds replicate 16 m + (l & 15), rows 16 (l >> 4) + j of the sub-tile; lane l of a B
 // fragment pair 16 h + (l & 15) of the column tile, the same rows; D: pair 16 h + (l & 15),
 // replicates 16 m + 4 (l >> 4) + i.
-template <int NQ, int NB, bool LIVE, int DIAG>
+template <int NQ, int SLO, int NB, bool LIVE, int DIAG>
 __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* smem, int wave) {
   constexpr int PER = NB + (LIVE ? 4 : 0);  // this wave's vector-memory ops per sub-tile
   const ob_v4i* bs = reinterpret_cast<const ob_v4i*>(smem);  // [kNbuf][kSubUnits]
   const int lane = threadIdx.x & 63;
   const int wb = wave & 3, grp = wave >> 2;  // replicate batch in the tile, slice group
-  const int slo = grp ? kSlo : 0;
+  constexpr int slo = SLO;                    // this wave's first slice
   // XCD-aware remap (as ob_gram_kernel's map_work): consecutive work items -- the column tiles of
   // one replicate tile, then the replicate tiles of one chunk -- share an XCD's L2.
   const uint32_t nwg = gridDim.x, bid = blockIdx.x;
@@ -872,19 +876,25 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
   const bool live = rt * 4u + (uint32_t)(wave & 3) < a.nb_rep;
   const bool six = a.nsl[chunk * (uint32_t)a.n_ct + wi % (uint32_t)a.n_ct] == 6;
   // waves 0-3: slices 0-3, two B pieces; 4-5: slices 4-6, two B pieces; 6-7: slices 4-6, one piece.
-  // Six slices: waves 4-7 take slices 4-5, one piece each; pieces 12-13 (slice 6) are not loaded.
-  if (wave < 4) {
-    if (live) oz_gram_body<kSlo, 2, true, DIAG>(a, smem, wave);
-    else oz_gram_body<kSlo, 2, false, DIAG>(a, smem, wave);
-  } else if (six) {
-    if (live) oz_gram_body<kS - kSlo - 1, 1, true, DIAG>(a, smem, wave);
-    else oz_gram_body<kS - kSlo - 1, 1, false, DIAG>(a, smem, wave);
+  // Six slices: waves 0-3 take slices 0 .. kSix0 - 1, waves 4-7 the rest of 0-5, one piece each;
+  // pieces 12-13 (slice 6) are not loaded.
+  if (six) {
+    if (wave < 4) {
+      if (live) oz_gram_body<kSix0, 0, 2, true, DIAG>(a, smem, wave);
+      else oz_gram_body<kSix0, 0, 2, false, DIAG>(a, smem, wave);
+    } else {
+      if (live) oz_gram_body<6 - kSix0, kSix0, 1, true, DIAG>(a, smem, wave);
+      else oz_gram_body<6 - kSix0, kSix0, 1, false, DIAG>(a, smem, wave);
+    }
+  } else if (wave < 4) {
+    if (live) oz_gram_body<kSlo, 0, 2, true, DIAG>(a, smem, wave);
+    else oz_gram_body<kSlo, 0, 2, false, DIAG>(a, smem, wave);
   } else if (wave < 6) {
-    if (live) oz_gram_body<kS - kSlo, 2, true, DIAG>(a, smem, wave);
-    else oz_gram_body<kS - kSlo, 2, false, DIAG>(a, smem, wave);
+    if (live) oz_gram_body<kS - kSlo, kSlo, 2, true, DIAG>(a, smem, wave);
+    else oz_gram_body<kS - kSlo, kSlo, 2, false, DIAG>(a, smem, wave);
   } else {
-    if (live) oz_gram_body<kS - kSlo, 1, true, DIAG>(a, smem, wave);
-    else oz_gram_body<kS - kSlo, 1, false, DIAG>(a, smem, wave);
+    if (live) oz_gram_body<kS - kSlo, kSlo, 1, true, DIAG>(a, smem, wave);
+    else oz_gram_body<kS - kSlo, kSlo, 1, false, DIAG>(a, smem, wave);
   }
 }
 
