@@ -1956,11 +1956,23 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   const uint32_t rcF = rd.on ? kRcF : kRc;  // the full lists' chunk rows (= their capacity)
   const uint32_t nch0 = (p->n[0] + rcF - 1) / rcF, nch1 = (p->n[1] + rcF - 1) / rcF;
   // replicate slots per batch: IPM state (x, z, w: 3 f64 per fit and list entry, rcF entries per
-  // chunk) within 48 GB
+  // chunk) within OB_MM_STATE_GB (default 160 of the 288 GB): a batch's tail iterations (few live
+  // fits) and phase 1 cost about the same time for 2 or 12 replicates, so wider batches amortize them
+  static const uint64_t state_budget = [] {
+    const char* e = getenv("OB_MM_STATE_GB");
+    const double v = e ? atof(e) : 0.0;
+    return (uint64_t)((v > 0.0 ? v : 160.0) * (double)(1ull << 30));
+  }();
   const size_t state_rows = (size_t)(nch0 + nch1) * rcF;
   const size_t state_per_rep = 3 * state_rows * S_pad * sizeof(double);
   const uint64_t want = std::max<uint64_t>(n_reps, 1);
-  const uint32_t rb_cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({want, 256, (48ull << 30) / state_per_rep}));
+  size_t free_b = 0, total_b = 0;
+  MM_OK(hipMemGetInfo(&free_b, &total_b));
+  size_t held = 0;  // this panel's state slots from an earlier call count as free
+  if (p->mm_ws)
+    for (int i = 0; i < 3; ++i) held += static_cast<Buffers*>(p->mm_ws)->cap[i];
+  const uint64_t budget = std::min<uint64_t>(state_budget, (uint64_t)((free_b + held) * 0.8));
+  const uint32_t rb_cap = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>({want, 256, budget / state_per_rep}));
   const size_t fits = (size_t)rb_cap * 2 * S_pad;
   const size_t fitsx = 2 * fits;  // fit arrays: the full fits, then phase 1's (at most as many)
   const int nv_max = nv_asm(K);  // >= 5 + 2 K (affine) and nv_cls(K)
