@@ -454,7 +454,8 @@ def main():
                          "reports replicate-quantiles/s instead of the headline metric")
     ap.add_argument("--mm", action="store_true",
                     help="configs[4]: Machado-Mata (defaults 500k rows x 15 predictors, 1000 simulations, "
-                         "2 replicates per GPU per step); reports MM replicates/s")
+                         "12 replicates per GPU per step, one batch; configs[4] is 125 per GPU); reports MM "
+                         "replicates/s")
     ap.add_argument("--sims", type=int, default=1000, help="--mm: quantile regressions per group per replicate")
     ap.add_argument("--heckman", action="store_true",
                     help="Heckman two-step bootstrap on configs[1]'s panel plus a selection equation "
@@ -470,7 +471,7 @@ def main():
         if "--preds" not in explicit:
             args.preds = 15
         if "--reps" not in explicit:
-            args.reps = 2
+            args.reps = 12
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
