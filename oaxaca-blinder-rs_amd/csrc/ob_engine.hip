@@ -37,7 +37,11 @@ typedef double ob_d4 __attribute__((ext_vector_type(4)));
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kCntStride = OB_TILE_ROWS / 4 + 1;  // u32 words per replicate row of the u8 count image (+1 pad)
+// The count kernel's LDS u8 image of a (tile, 64-replicate batch) is replicate-minor: row word q
+// (rows 4q .. 4q+3 of the tile) of replicate r is word q * kImgRow + r. A wave whose lanes draw
+// for 64 distinct replicates then hits 32 distinct banks per lane group (bank = r mod 32).
+constexpr int kImgRow = 64;                            // words per row word (one per replicate)
+constexpr int kImgWords = (OB_TILE_ROWS / 4) * kImgRow;  // 4096
 constexpr uint64_t kSegReps = 16384;
 constexpr uint64_t kCountBudget = 24ull << 30;  // bytes of level-2 count images per segment
 // rows per group: 2^20 tiles (level 1 walks groups past 40960 tiles as subtrees, whose LDS
@@ -443,26 +447,24 @@ __device__ __forceinline__ bool full_tile(const Work& w, uint32_t tile) {
   return w.n - tile * OB_TILE_ROWS >= OB_TILE_ROWS;
 }
 
-__device__ __forceinline__ void add_draw(uint32_t* row, uint32_t lr) {
-  atomicAdd(&row[lr >> 2], 1u << ((lr & 3u) * 8u));
+__device__ __forceinline__ void add_draw(uint32_t* img, uint32_t r, uint32_t lr) {
+  atomicAdd(&img[(lr >> 2) * kImgRow + r], 1u << ((lr & 3u) * 8u));
 }
 
-// The four draws of one Philox word (byte b = a row of the tile): with a = w & 0xFCFCFCFC (byte b
-// = the row's word offset in bytes) and m = (w << 3) & 0x18181818 (byte b = its byte lane x 8), a
-// draw is one SDWA add (row offset + byte b of a) and one SDWA shift (1 << byte b of m) on gfx950,
-// where the compiler emits a shift-and-mask chain for each (5 VALU per draw -> 2 + 3/4). The
-// shifts read only byte b of their operand, so no mask per draw is needed.
-template <int B>
-__device__ __forceinline__ uint32_t sdwa_add_byte(uint32_t base, uint32_t a) {
+// The four draws of one Philox word (byte b = a row of the tile). The LDS byte address of row b of
+// replicate r is (b >> 2) * 4 kImgRow + 4 r = ((b & 0xFC) << 6) + 4 r: with lo = (w << 6) &
+// 0x3F003F00 (16-bit halves = bytes 0 and 2 of w, so placed) and hi = (w >> 2) & 0x3F003F00 (bytes
+// 1 and 3), a draw's address is one SDWA add (4 r + half h of lo or hi), and with m = (w << 3) &
+// 0x18181818 (byte b = its byte lane x 8) its increment one SDWA shift (1 << byte b of m), where the
+// compiler would emit a shift-and-mask chain for each. The shifts read only byte b of their
+// operand, so no mask per draw is needed.
+template <int H>
+__device__ __forceinline__ uint32_t sdwa_add_half(uint32_t base, uint32_t a) {
   uint32_t r;
-  if constexpr (B == 0)
-    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(base), "v"(a));
-  else if constexpr (B == 1)
-    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(base), "v"(a));
-  else if constexpr (B == 2)
-    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(base), "v"(a));
+  if constexpr (H == 0)
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_0" : "=v"(r) : "v"(base), "v"(a));
   else
-    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(base), "v"(a));
+    asm("v_add_u32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:WORD_1" : "=v"(r) : "v"(base), "v"(a));
   return r;
 }
 
@@ -481,17 +483,18 @@ __device__ __forceinline__ uint32_t sdwa_shl_byte(uint32_t m, uint32_t one) {
 }
 
 template <int B>
-__device__ __forceinline__ void add_draw_byte(uint32_t* img, uint32_t row_off, uint32_t a, uint32_t m, uint32_t one) {
-  atomicAdd(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(img) + sdwa_add_byte<B>(row_off, a)),
+__device__ __forceinline__ void add_draw_byte(uint32_t* img, uint32_t rep_off, uint32_t a, uint32_t m, uint32_t one) {
+  atomicAdd(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(img) + sdwa_add_half<(B >> 1)>(rep_off, a)),
             sdwa_shl_byte<B>(m, one));
 }
 
-__device__ __forceinline__ void add_draws_word(uint32_t* img, uint32_t row_off, uint32_t w, uint32_t one) {
-  const uint32_t a = w & 0xFCFCFCFCu, m = (w << 3) & 0x18181818u;
-  add_draw_byte<0>(img, row_off, a, m, one);
-  add_draw_byte<1>(img, row_off, a, m, one);
-  add_draw_byte<2>(img, row_off, a, m, one);
-  add_draw_byte<3>(img, row_off, a, m, one);
+// rep_off = 4 r, the replicate's byte offset in every row word
+__device__ __forceinline__ void add_draws_word(uint32_t* img, uint32_t rep_off, uint32_t w, uint32_t one) {
+  const uint32_t lo = (w << 6) & 0x3F003F00u, hi = (w >> 2) & 0x3F003F00u, m = (w << 3) & 0x18181818u;
+  add_draw_byte<0>(img, rep_off, lo, m, one);
+  add_draw_byte<1>(img, rep_off, hi, m, one);
+  add_draw_byte<2>(img, rep_off, lo, m, one);
+  add_draw_byte<3>(img, rep_off, hi, m, one);
 }
 
 __device__ __forceinline__ void level2_draws(const GramArgs& a, const Work& w, uint32_t tile, uint32_t* cnt,
@@ -529,16 +532,15 @@ __device__ __forceinline__ void level2_draws(const GramArgs& a, const Work& w, u
         u = ob_u32x4{pp * 0x9E3779B9u ^ r, pp * 0x85EBCA6Bu ^ c2, pp * 0xC2B2AE35u, pp ^ 0x27D4EB2Fu};
       else
         u = ob_philox_x3(pp, rep0 + r, c2, OB_TAG_L2, a.key0, a.key1);
-      uint32_t* row = cnt + r * kCntStride;
       if (full && (a.diag & 32)) {  // timing ablation (OB_GRAM_DIAG 32): no LDS atomics
-        if ((u.x ^ u.y ^ u.z ^ u.w) == 0x5EED5EEDu) row[0] = 1u;
+        if ((u.x ^ u.y ^ u.z ^ u.w) == 0x5EED5EEDu) cnt[r] = 1u;
       } else if (full) {
         const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
-        for (int i = 0; i < 4; ++i) add_draws_word(cnt, (uint32_t)r * (kCntStride * 4), wd[i], one);
+        for (int i = 0; i < 4; ++i) add_draws_word(cnt, (uint32_t)r * 4u, wd[i], one);
       } else {
-        add_draw(row, ob_mulhi64(u.x, u.y, S));
-        if (2 * pp + 1 < mc[r]) add_draw(row, ob_mulhi64(u.z, u.w, S));
+        add_draw(cnt, (uint32_t)r, ob_mulhi64(u.x, u.y, S));
+        if (2 * pp + 1 < mc[r]) add_draw(cnt, (uint32_t)r, ob_mulhi64(u.z, u.w, S));
       }
     }
   }
@@ -548,25 +550,28 @@ __device__ __forceinline__ void level2_draws(const GramArgs& a, const Work& w, u
     if (nd) {
       const ob_u32x4 u = ob_philox_x3(m >> 4, rep0 + r, c2, OB_TAG_L2, a.key0, a.key1);
       const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
-      uint32_t* row = cnt + r * kCntStride;
 #pragma unroll
       for (uint32_t d = 0; d < 15; ++d)
-        if (d < nd) add_draw(row, (wd[d >> 2] >> (8 * (d & 3))) & 0xFFu);
+        if (d < nd) add_draw(cnt, (uint32_t)r, (wd[d >> 2] >> (8 * (d & 3))) & 0xFFu);
     }
   }
 }
 
 // Full tiles of the count kernel (OB_CNT_MAP): the whole calls of all 64 replicates form one list
-// that the block's waves walk in 64-call windows, window j on wave j mod 4. Call f's replicate and
-// its index among that replicate's calls come from an LDS call map (word f = index << 6 | r),
-// written by wave 0 when it publishes the tile's counts, instead of a per-window search over the
-// replicate boundaries. The part calls (m % 16 draws, one per replicate) form one extra window,
-// one lane per replicate. Same (call, replicate) -> draws as level2_draws, so the same counts.
-constexpr uint32_t kCallMapCap = 2048;  // whole calls of a (tile, batch) the map holds (mean 1024)
+// that the block's waves walk in 64-call windows, window j on wave j mod 4, one lane per call. The
+// list is call-major: call index p of every replicate that has one, replicates ascending, then p + 1.
+// The first cmin = min_r(calls) indices hold all 64 replicates, so window p < cmin is call p of
+// replicate `lane` (no lookup); past them an LDS call map (word = p << 6 | r, written by wave 0
+// when it publishes the tile's counts) lists the rest. Either way the lanes of a window draw for
+// distinct replicates (up to the seam between two indices past cmin), and with the replicate-minor
+// image (kImgRow) their atomics fall on distinct banks. The part calls (m % 16 draws, one per
+// replicate) form one extra window, one lane per replicate. Same (call, replicate) -> draws as
+// level2_draws, so the same counts.
+constexpr uint32_t kCallMapCap = 2048;  // calls past the dense prefix a (tile, batch) map holds
 
 __device__ __forceinline__ void level2_map_draws(const GramArgs& a, const Work& w, uint32_t tile, uint32_t* cnt,
-                                                 const uint32_t* mc, const uint32_t* cmap, uint32_t C, int wv,
-                                                 int lane) {
+                                                 const uint32_t* mc, const uint32_t* cmap, uint32_t C,
+                                                 uint32_t cmin, int wv, int lane) {
   const uint32_t nwin = (C + 63u) >> 6;
   const uint32_t c2 = (tile << 1) | w.g;
   const uint32_t rep0 = a.first_rep + w.rep0;
@@ -575,18 +580,23 @@ __device__ __forceinline__ void level2_map_draws(const GramArgs& a, const Work& 
     if (win < nwin) {
       const uint32_t f = win * 64u + (uint32_t)lane;
       if (f < C) {
-        const uint32_t e = cmap[f], r = e & 63u, pp = e >> 6;
+        uint32_t r = (uint32_t)lane, pp = win;
+        if (win >= cmin) {
+          const uint32_t e = cmap[f - cmin * 64u];
+          r = e & 63u;
+          pp = e >> 6;
+        }
         ob_u32x4 u;
         if (a.diag & 64)  // timing ablation (OB_GRAM_DIAG 64): no Philox, wrong draws
           u = ob_u32x4{pp * 0x9E3779B9u ^ r, pp * 0x85EBCA6Bu ^ c2, pp * 0xC2B2AE35u, pp ^ 0x27D4EB2Fu};
         else
           u = ob_philox_x3(pp, rep0 + r, c2, OB_TAG_L2, a.key0, a.key1);
         if (a.diag & 32) {  // timing ablation (OB_GRAM_DIAG 32): no LDS atomics
-          if ((u.x ^ u.y ^ u.z ^ u.w) == 0x5EED5EEDu) cnt[r * kCntStride] = 1u;
+          if ((u.x ^ u.y ^ u.z ^ u.w) == 0x5EED5EEDu) cnt[r] = 1u;
         } else {
           const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
 #pragma unroll
-          for (int i = 0; i < 4; ++i) add_draws_word(cnt, r * (kCntStride * 4), wd[i], one);
+          for (int i = 0; i < 4; ++i) add_draws_word(cnt, r * 4u, wd[i], one);
         }
       }
     } else {  // the part calls
@@ -594,10 +604,9 @@ __device__ __forceinline__ void level2_map_draws(const GramArgs& a, const Work& 
       if (nd) {
         const ob_u32x4 u = ob_philox_x3(m >> 4, rep0 + (uint32_t)lane, c2, OB_TAG_L2, a.key0, a.key1);
         const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
-        uint32_t* row = cnt + lane * kCntStride;
 #pragma unroll
         for (uint32_t d = 0; d < 15; ++d)
-          if (d < nd) add_draw(row, (wd[d >> 2] >> (8 * (d & 3))) & 0xFFu);
+          if (d < nd) add_draw(cnt, (uint32_t)lane, (wd[d >> 2] >> (8 * (d & 3))) & 0xFFu);
       }
     }
   }
@@ -608,23 +617,24 @@ __device__ __forceinline__ void level2_map_draws(const GramArgs& a, const Work& 
 #endif
 // A row drawn 256+ times wraps its byte and carries into the next one, which lowers the
 // replicate's byte sum below m: comparing sums with the level-1 counts is an exact check.
-// Four threads per replicate (consecutive lanes); thread my in [0, 256) holds replicate my >> 2's
-// 16 words of sub-tile my & 3 in registers, stores them straight to the HBM image (the tile's
-// first ns sub-tiles), then clears them in LDS, recycling the image without another pass.
+// Thread (r = lane, sub-tile part = wave) reads replicate r's 16 words of sub-tile `part` (bank r
+// mod 32: conflict-free), stores them straight to the HBM image (the tile's first ns sub-tiles),
+// clears them in LDS, recycling the image without another pass, and adds its byte sum to the
+// replicate's LDS sum; wave 0 compares the sums with m after the next barrier (check_sums).
 // I8: the A-fragment units of ob_gram_i8.hip ([sub-tile][16-replicate block][lane][16 B], lane
 // = replicate 16 m + (l & 15) holding rows 16 (l >> 4) .. + 15), i.e. word group q of the thread
 // is unit sb * 256 + (r >> 4) * 64 + q * 16 + (r & 15). f64: replicate r's 16 words at r * 17 of
 // the sub-tile image, then its zero pad word.
 template <bool I8>
-__device__ __forceinline__ void check_store_counts(const GramArgs& a, uint32_t* cnt, const uint32_t* mc, int my,
+__device__ __forceinline__ void check_store_counts(const GramArgs& a, uint32_t* cnt, uint32_t* lsum, int my,
                                                    uint32_t tt, uint32_t rb, uint32_t ns) {
-  const int r = my >> 2, part = my & 3;
-  uint32_t* row = cnt + r * kCntStride + part * 16;
+  const int r = my & 63, part = my >> 6;
+  uint32_t* col = cnt + part * 16 * kImgRow + r;
   uint32_t v[16];
   uint32_t sum = 0, hib = 0;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    v[i] = row[i];
+    v[i] = col[i * kImgRow];
     sum = __builtin_amdgcn_sad_u8(v[i], 0u, sum);
     hib |= v[i] & 0x80808080u;
   }
@@ -652,10 +662,15 @@ __device__ __forceinline__ void check_store_counts(const GramArgs& a, uint32_t* 
     }
   }
 #pragma unroll
-  for (int i = 0; i < 16; ++i) row[i] = 0u;
-  sum += __shfl_xor(sum, 1);
-  sum += __shfl_xor(sum, 2);
-  if (part == 0 && sum != mc[r] && !(a.diag & 96)) atomicOr(a.flags, 1u);
+  for (int i = 0; i < 16; ++i) col[i * kImgRow] = 0u;
+  atomicAdd(&lsum[r], sum);
+}
+
+// Wave 0, after the barrier that follows a tile's check_store_counts: the tile's byte sums against
+// its level-1 counts, then the sums cleared for the tile after next.
+__device__ __forceinline__ void check_sums(const GramArgs& a, uint32_t* lsum, const uint32_t* mc, int lane) {
+  if (lsum[lane] != mc[lane] && !(a.diag & 96)) atomicOr(a.flags, 1u);
+  lsum[lane] = 0u;
 }
 
 // Level-1 count of global tile tt (group 0's tiles, then group 1's) for batch replicate r.
@@ -665,7 +680,7 @@ __device__ __forceinline__ uint32_t level1_count(const GramArgs& a, uint32_t rep
 }
 
 __device__ __forceinline__ void publish_counts(const Work& w, uint32_t tile, uint32_t m, uint32_t* mc, uint32_t* cum,
-                                               int lane, uint32_t* cmap) {
+                                               int lane, uint32_t* cmap, uint32_t* cminp) {
   mc[lane] = m;
   // calls in the whole-call list: full tile floor(m/16) (the part call goes apart), else ceil(m/2)
   const bool full = full_tile(w, tile);
@@ -678,9 +693,28 @@ __device__ __forceinline__ void publish_counts(const Work& w, uint32_t tile, uin
   }
   cum[lane + 1] = v;
   if (lane == 0) cum[0] = 0;
-  // the call map of a full tile (level2_map_draws), when the tile's calls fit it
-  if (cmap && full && (uint32_t)__builtin_amdgcn_readlane(v, 63) <= kCallMapCap)
-    for (uint32_t j = 0, f = v - c; j < c; ++j, ++f) cmap[f] = (j << 6) | (uint32_t)lane;
+  // the call map of a full tile (level2_map_draws): call-major past the dense prefix of cmin
+  // indices, when those calls fit it
+  if (cmap && full) {
+    uint32_t cmin = c, cmax = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      cmin = min(cmin, (uint32_t)__shfl_xor(cmin, o));
+      cmax = max(cmax, (uint32_t)__shfl_xor(cmax, o));
+    }
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane(v, 63);
+    if (total - cmin * 64u <= kCallMapCap) {
+      uint32_t base = 0;
+      for (uint32_t j = cmin; j < cmax; ++j) {
+        const uint64_t mask = __ballot(c > j);
+        if (c > j)
+          cmap[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u))] =
+              (j << 6) | (uint32_t)lane;
+        base += (uint32_t)__popcll(mask);
+      }
+    }
+    if (lane == 0) *cminp = cmin;
+  }
 }
 
 template <int CB>
@@ -721,8 +755,8 @@ constexpr int kCntTilesPerBlock = OB_CNT_TILES;
 // rows 16 (l >> 4) + j of the sub-tile -- 16 KB, one 16-byte store per thread and unit.
 template <bool I8>
 __global__ __launch_bounds__(kBlock) void ob_count_kernel(const GramArgs a) {
-  __shared__ uint32_t img[64 * kCntStride];
-  __shared__ uint32_t mcb[2][64], cumb[2][65];
+  __shared__ uint32_t img[kImgWords];
+  __shared__ uint32_t mcb[2][64], cumb[2][65], lsumb[2][64], cminb[2];
   __shared__ uint32_t cmap[OB_CNT_MAP ? kCallMapCap : 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   Work w{};
@@ -732,11 +766,12 @@ __global__ __launch_bounds__(kBlock) void ob_count_kernel(const GramArgs a) {
   const uint32_t tt1 = min(a.tiles_total, tt0 + kCntTilesPerBlock);
   // wave 0 loads tile tt+1's level-1 counts while the block draws tile tt
   uint32_t m_next = (wave == 0 && tt0 < tt1) ? level1_count(a, w.rep0, tt0, lane) : 0u;
-  // the image starts zeroed once; check_store_counts clears what it read (the pad words stay 0)
-  for (int i = tid; i < 64 * kCntStride; i += kBlock) img[i] = 0u;
-  // Two barriers per tile: the call prefix is double-buffered, so publishing tile tt + 1's
-  // (buffer (tt + 1) & 1) never races the checks of tile tt (buffer tt & 1), and the image
-  // clears of tile tt complete before the barrier that follows that publish.
+  // the image starts zeroed once; check_store_counts clears what it read
+  for (int i = tid; i < kImgWords; i += kBlock) img[i] = 0u;
+  if (tid < 128) lsumb[tid >> 6][tid & 63] = 0u;
+  // Two barriers per tile: the call prefix, counts and sums are double-buffered, so publishing
+  // tile tt + 1's (buffer (tt + 1) & 1) never races the checks of tile tt (buffer tt & 1), and the
+  // image clears of tile tt complete before the barrier that follows that publish.
   for (uint32_t tt = tt0; tt < tt1; ++tt) {
     uint32_t* mc = mcb[tt & 1];
     uint32_t* cum = cumb[tt & 1];
@@ -744,18 +779,24 @@ __global__ __launch_bounds__(kBlock) void ob_count_kernel(const GramArgs a) {
     w.n = w.g ? a.n1 : a.n0;
     const uint32_t tile = tt - (w.g ? a.tiles0 : 0u);
     if (wave == 0) {
-      publish_counts(w, tile, m_next, mc, cum, lane, OB_CNT_MAP ? cmap : nullptr);
+      publish_counts(w, tile, m_next, mc, cum, lane, OB_CNT_MAP ? cmap : nullptr, &cminb[tt & 1]);
       if (tt + 1 < tt1) m_next = level1_count(a, w.rep0, tt + 1, lane);
     }
     __syncthreads();
+    if (wave == 0 && tt > tt0) check_sums(a, lsumb[(tt - 1) & 1], mcb[(tt - 1) & 1], lane);
     const uint32_t C = cum[64];
-    if (OB_CNT_MAP && full_tile(w, tile) && C <= kCallMapCap)
-      level2_map_draws(a, w, tile, img, mc, cmap, C, wave, lane);
+    const uint32_t cmin = cminb[tt & 1];
+    if (OB_CNT_MAP && full_tile(w, tile) && C - cmin * 64u <= kCallMapCap)
+      level2_map_draws(a, w, tile, img, mc, cmap, C, cmin, wave, lane);
     else
       level2_draws(a, w, tile, img, mc, cum, 0, 1, wave, 4, lane);
     __syncthreads();
     const uint32_t ns = (min(OB_TILE_ROWS, w.n - tile * OB_TILE_ROWS) + 63) >> 6;
-    check_store_counts<I8>(a, img, mc, tid, tt, w.rb, ns);
+    check_store_counts<I8>(a, img, lsumb[tt & 1], tid, tt, w.rb, ns);
+  }
+  if (tt0 < tt1) {
+    __syncthreads();
+    if (wave == 0) check_sums(a, lsumb[(tt1 - 1) & 1], mcb[(tt1 - 1) & 1], lane);
   }
 }
 
