@@ -1291,8 +1291,12 @@ size_t gram_lds_bytes(const ob_panel* p) { return (size_t)kXtOff + 2 * (size_t)p
 // so a replicate's Gram -- summed over chunks in a fixed order -- is bitwise the same however
 // the replicates are segmented or sharded. Each group splits into balanced chunks; about
 // kTargetChunks in all, so a 16384-replicate segment (256 batches of 64) is a whole number of
-// rounds over 256 CUs.
-constexpr uint32_t kTargetChunks = 64;
+// rounds over 256 CUs. 32 rather than 64 (round 3, profiles/r03_ab_chunks.txt): half the chunk
+// partials to write and reduce, Gram 12.5 -> 12.3 ms and reduce 0.27 -> 0.14 ms at configs[1].
+#ifndef OB_TARGET_CHUNKS
+#define OB_TARGET_CHUNKS 32
+#endif
+constexpr uint32_t kTargetChunks = OB_TARGET_CHUNKS;
 
 Plan make_plan(const ob_panel* p, uint64_t n_reps, bool unit) {
   Plan pl;
