@@ -488,9 +488,28 @@ __device__ __forceinline__ void add_draw_byte(uint32_t* img, uint32_t rep_off, u
             sdwa_shl_byte<B>(m, one));
 }
 
+#ifndef OB_CNT_PERM
+#define OB_CNT_PERM 1  // 1: a draw's LDS address by one v_perm_b32 (byte 0 = 4 r, byte 1 = its row word)
+#endif
+template <int B>
+__device__ __forceinline__ void add_draw_perm(uint32_t* img, uint32_t rep_off, uint32_t q, uint32_t m, uint32_t one) {
+  // bytes of the address: rep_off's byte 0 (< 256), byte B of q (the row word), zero, zero
+  const uint32_t addr = __builtin_amdgcn_perm(q, rep_off, 0x0C0C0000u | ((4u + B) << 8));
+  atomicAdd(reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(img) + addr), sdwa_shl_byte<B>(m, one));
+}
+
 // rep_off = 4 r, the replicate's byte offset in every row word
 __device__ __forceinline__ void add_draws_word(uint32_t* img, uint32_t rep_off, uint32_t w, uint32_t one) {
-  const uint32_t lo = (w << 6) & 0x3F003F00u, hi = (w >> 2) & 0x3F003F00u, m = (w << 3) & 0x18181818u;
+  const uint32_t m = (w << 3) & 0x18181818u;
+  if (OB_CNT_PERM) {
+    const uint32_t q = (w >> 2) & 0x3F3F3F3Fu;  // byte b = the row word of draw b
+    add_draw_perm<0>(img, rep_off, q, m, one);
+    add_draw_perm<1>(img, rep_off, q, m, one);
+    add_draw_perm<2>(img, rep_off, q, m, one);
+    add_draw_perm<3>(img, rep_off, q, m, one);
+    return;
+  }
+  const uint32_t lo = (w << 6) & 0x3F003F00u, hi = (w >> 2) & 0x3F003F00u;
   add_draw_byte<0>(img, rep_off, lo, m, one);
   add_draw_byte<1>(img, rep_off, hi, m, one);
   add_draw_byte<2>(img, rep_off, lo, m, one);
