@@ -4,7 +4,7 @@
 Workload = BASELINE.json configs[1]: a 1,000,000-row two-group panel (500k/500k) with 20 numeric
 predictors, two-fold WLS decomposition (builder default reference coefficients GroupA), 10,000
 bootstrap replicates per GPU per step. One step = one full bootstrap run with the panel already
-resident in HBM: OBRS-1 resampling + Gram + solves + OB terms for every replicate (HIP), the
+resident in HBM: OBRS-2 resampling + Gram + solves + OB terms for every replicate (HIP), the
 RCCL all-gather of the per-replicate component columns over xGMI (N > 1), and the SE/p/CI aggregation of
 every reported component on rank 0 (builder.rs:841-930). Replicates are sharded across ranks
 (weak scaling: each rank runs its own 10,000 replicate ids per step).
@@ -225,7 +225,7 @@ def bench_mm(args, world, rank, local, dist):
         "metric": "Machado-Mata bootstrap replicates/sec (configs[4]: 1000 QR draws per group per replicate)",
         "value": value, "unit": "replicates/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "f64", "data": "synthetic (SURVEY.md §8d wage panel, numpy seed 20260424; OBRS-1/MM-1 seed 0x0B5EED)",
+        "dtype": "f64", "data": "synthetic (SURVEY.md §8d wage panel, numpy seed 20260424; OBRS-2/MM-1 seed 0x0B5EED)",
         "config": {"workload": "configs[4]: Machado-Mata, 1000 simulations, quantiles 0.1/0.25/0.5/0.75/0.9",
                    "rows": args.rows, "predictors": args.preds, "simulations": args.sims,
                    "replicates_per_gpu_per_step": R, "parallelism": f"replicates sharded x{world}, RCCL all-gather"},
@@ -405,7 +405,8 @@ def load_traffic(rows, preds, reps, gram_path=1):
 
 def end_to_end(ob, ctx, d, ya, yb, n, ref, stat_cols, dev):
     """One configs[1] run() from a fresh panel, as the reference's published figures are whole runs
-    (README.md:316-317): host -> HBM upload and the Gram panel (ob_panel_create), the digit images
+    (README.md:316-317): host -> HBM upload and the Gram panel (ob_panel_create), the point
+    estimate on the unresampled panel (ob_point_estimate, builder.rs:810-811), the digit images
     and exception rows (prep, first boot of the panel), n replicates, and the aggregation of every
     reported component on the host. Host clock around all of it; prep_ms by HIP events."""
     import torch
@@ -415,6 +416,9 @@ def end_to_end(ob, ctx, d, ya, yb, n, ref, stat_cols, dev):
     panel = ob.Panel(d["xa"], ya, d["xb"], yb, d["wa"], d["wb"], ctx=ctx)
     t_create = time.perf_counter() - t0
     panel.set_gather_columns(list(range(len(stat_cols))))
+    t1 = time.perf_counter()
+    point = panel.point_estimate(ref)  # run_single_pass on the unresampled panel (builder.rs:810-811)
+    t_point = time.perf_counter() - t1
     rows = torch.empty((n, panel.row_len), dtype=torch.float64, device=dev)
     ok = torch.empty(n, dtype=torch.uint8, device=dev)
     panel.boot_sharded_device(0x0B5EED, 0, n, rows.data_ptr(), ok.data_ptr(), ref,
@@ -424,13 +428,67 @@ def end_to_end(ob, ctx, d, ya, yb, n, ref, stat_cols, dev):
     hr = rows[:, : len(stat_cols)].cpu().numpy()
     ob.aggregate(np.ascontiguousarray(hr), ok.cpu().numpy(), stat_cols)
     total_s = time.perf_counter() - t0
+    assert np.isfinite(point[: len(stat_cols)]).all(), "point estimate"
+
     panel.close()
     return {"replicates": n, "ms": total_s * 1e3, "replicates_per_s": n / total_s,
-            "panel_create_ms": t_create * 1e3, "prep_ms": tm["prep_ms"],
+            "panel_create_ms": t_create * 1e3, "point_estimate_ms": t_point * 1e3, "prep_ms": tm["prep_ms"],
             "boot_ms": tm["level1_ms"] + tm["counts_ms"] + tm["gram_ms"] + tm["reduce_ms"] + tm["solve_ms"],
             "oz_exceptions": tm["oz_exceptions"], "oz_bits": tm["oz_bits"],
-            "what": "fresh ob_panel_create (H2D + Gram panel) + digit images/exception rows + one boot of n "
+            "what": "run() as builder.rs:787-983 runs it: fresh ob_panel_create (H2D + Gram panel) + the point "
+                    "estimate (ob_point_estimate, builder.rs:810-811) + digit images/exception rows + one boot of n "
                     "replicates + host aggregation, host clock"}
+
+
+def free_port():
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_cmd(argv, n, port):
+    """The torch.distributed.run command that runs this bench as n ranks on one node (one process
+    per GPU, rendezvous on 127.0.0.1), with the same arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(n),
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def probe_gpu_count():
+    """GPUs visible to a fresh process, counted in a child so that this process never touches the
+    GPU before it starts the launcher (a process that initialised HIP must not exec or fork ranks)."""
+    import subprocess
+
+    code = "import torch; print(torch.cuda.device_count())"
+    try:
+        out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+        return int(out.stdout.strip().splitlines()[-1])
+    except (subprocess.SubprocessError, ValueError, IndexError):
+        return 0
+
+
+def launch_ranks(argv, n):
+    """`bench.py --gpus N` run directly (no WORLD_SIZE): start N ranks under torch.distributed.run
+    as a child, forward rank 0's JSON line to stdout (everything else to stderr) and return the
+    launcher's exit code. Fails loudly, before starting anything, when fewer than N GPUs exist."""
+    import subprocess
+
+    have = probe_gpu_count()
+    if have < n:
+        print(f"bench.py: --gpus {n} needs {n} visible GPUs, this machine has {have}; "
+              f"refusing to print a {have}-GPU line for an {n}-GPU run", file=sys.stderr, flush=True)
+        return 3
+    cmd = launcher_cmd(argv, n, free_port())
+    print("bench.py: launching " + " ".join(cmd), file=sys.stderr, flush=True)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True)
+    for line in proc.stdout:
+        s = line.strip()
+        if s.startswith("{") and '"metric"' in s:
+            print(s, flush=True)
+        else:
+            sys.stderr.write(line)
+    return proc.wait()
 
 
 def main():
@@ -473,9 +531,14 @@ def main():
         if "--reps" not in explicit:
             args.reps = 12
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; the line reports the launched world "
+              f"({world} ranks)", file=sys.stderr, flush=True)
     args.cpu_threads_explicit = args.cpu_threads > 0
     if args.cpu_threads <= 0:
         args.cpu_threads = host_cores()
@@ -508,6 +571,9 @@ def main():
         if dist is not None and world > 1:
             dist.broadcast_object_list(uid, src=0)
         ctx = N.rank_context(local, rank, world, uid[0])
+    rccl_rank, rccl_world = N.ctx_rank(ctx)
+    if (rccl_rank, rccl_world) != (rank, world):
+        raise RuntimeError(f"engine RCCL communicator is rank {rccl_rank} of {rccl_world}, expected {rank} of {world}")
     panel = ob.Panel(d["xa"], ya, d["xb"], yb, d["wa"], d["wb"], ctx=ctx)
     # weak: every rank runs --reps replicates per step; strong (configs[2]): --reps in total
     total = args.reps if args.strong else args.reps * world
@@ -631,6 +697,7 @@ def main():
             "value": value * ny,
             "unit": "replicates/s" if not taus else "replicate-quantiles/s",
             "n_gpus": world,
+            "rccl_world": rccl_world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
@@ -638,7 +705,7 @@ def main():
             "scaling": mode,
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (SURVEY.md §8d wage panel, numpy seed 20260424; OBRS-1 bootstrap seed 0x0B5EED)",
+            "data": "synthetic (SURVEY.md §8d wage panel, numpy seed 20260424; OBRS-2 bootstrap seed 0x0B5EED)",
             "config": {"workload": ("configs[1]: two-fold WLS bootstrap, GroupA reference coefficients" if not args.strong
                                     else f"configs[2]: {total} replicates per step in total, sharded over {world} GPU(s)")
                        if not taus else f"configs[3]: RIF decomposition at tau={taus}, two-fold WLS, GroupA",

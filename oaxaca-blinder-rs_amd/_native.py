@@ -41,6 +41,7 @@ EXPORTED = (
     "ob_get_unique_id", "ob_ctx_create_rank", "ob_ctx_rank", "ob_boot_run_sharded", "ob_boot_run_sharded_device",
     "ob_boot_run_multi", "ob_debug_counts", "ob_prepared_boot_sharded", "ob_debug_gram",
     "ob_debug_gram_exceptions", "ob_panel_set_gather_columns", "ob_debug_shard_sim", "ob_debug_mm_fail",
+    "ob_debug_chunks", "ob_debug_mm_betas",
 )
 
 
@@ -195,6 +196,8 @@ _SIGS = {
                                            C.POINTER(C.c_uint32), C.c_int32]),
     "ob_prepared_boot_sharded": (C.c_int, [_P, C.c_uint64, C.c_uint64, _D, _U8]),
     "ob_debug_counts": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_int, C.POINTER(C.c_uint32), _U8]),
+    "ob_debug_chunks": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_int32, C.POINTER(C.c_int32)]),
+    "ob_debug_mm_betas": (C.c_int, [_P, C.c_uint64, C.c_int32, C.c_uint64, _D, _U8]),
 }
 
 _lib = None
@@ -289,6 +292,14 @@ def rank_context(device: int, rank: int, world: int, uid: bytes) -> C.c_void_p:
         with _lib_lock:
             _rank_ctx_cache[key] = ctx
     return ctx
+
+
+def ctx_rank(ctx) -> tuple:
+    """(rank, world) of the engine's RCCL communicator in ``ctx`` (ob_ctx_rank; (0, 1) for a
+    plain context)."""
+    r, w = C.c_int(0), C.c_int(0)
+    check(lib().ob_ctx_rank(ctx, C.byref(r), C.byref(w)))
+    return r.value, w.value
 
 
 def device_count() -> int:

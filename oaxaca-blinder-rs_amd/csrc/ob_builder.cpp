@@ -868,8 +868,13 @@ int ob_prepared_boot_sharded(ob_prepared* p, uint64_t first_rep, uint64_t n_reps
   std::vector<int32_t> cols;
   for (int c = 0; c < 6 + 2 * kd; ++c) cols.push_back(c);
   for (size_t i = 0; i < p->selection_names.size(); ++i) cols.push_back(sel0 + (int)i);
+  // the narrowing holds for this call only: the panel's own column set is restored afterwards, so a
+  // later ob_boot_run_sharded on ob_prepared_panel(p) gathers what its caller asked for
+  const std::vector<int32_t> saved = p->panel->gather_cols;
   OB_TRY(ob_panel_set_gather_columns(p->panel, cols.data(), (int32_t)cols.size()));
-  return ob_boot_run_sharded(p->panel, p->seed, first_rep, n_reps, p->ref, rows, ok);
+  const int rc = ob_boot_run_sharded(p->panel, p->seed, first_rep, n_reps, p->ref, rows, ok);
+  const int rc2 = ob_panel_set_gather_columns(p->panel, saved.data(), (int32_t)saved.size());
+  return rc != OB_OK ? rc : rc2;
 }
 
 int ob_prepared_boot_device(ob_prepared* p, uint64_t first_rep, uint64_t n_reps, double* d_rows, uint8_t* d_ok,

@@ -1,4 +1,4 @@
-// ob_engine.hip -- the MI355X bootstrap engine: OBRS-1 resampling + X^T diag(c w) X on f64 MFMA
+// ob_engine.hip -- the MI355X bootstrap engine: OBRS-2 resampling + X^T diag(c w) X on f64 MFMA
 // + wave-parallel Cholesky solves + Oaxaca-Blinder algebra, all resident in HBM.
 //
 // Replaces, per replicate, builder.rs:816-839 (polars resample + vstack + run_single_pass):
@@ -82,8 +82,9 @@ struct GramArgs {
 };
 
 // ---------------------------------------------------------------------------------------------
-// Level 1: tile counts m_j for one (replicate, group) by fair-bit splitting (OBRS-1, ob_spec.h;
-// oracle orc_level1_counts). Level l of the dyadic tile tree lives in LDS buffer (D - l) & 1.
+// Level 1: tile counts m_j for one (replicate, group) by binomial splitting (OBRS-2, ob_spec.h:
+// popcounts below 4096 draws, Knuth-Yao samples above; oracle orc_level1_counts). Level l of the
+// dyadic tile tree lives in LDS buffer (D - l) & 1.
 // Levels l < 8 have at most 2^l nodes and give each 256 >> l threads (popcounts summed by LDS
 // atomics); deeper levels give a thread whole nodes. T <= 256 tiles ("small") keeps the tile
 // level and the running counts in LDS; larger T sends the last split straight to m1, the
@@ -433,7 +434,7 @@ __device__ __forceinline__ void stage_dma(const GramArgs& a, const Work& w, uint
                                        (__attribute__((address_space(3))) void*)(lds3 + dst + t * 1024), 16, 0, 0);
 }
 
-// Level-2 draws of `tile` into a u8 count image (OBRS-1, ob_spec.h: full tiles take sixteen
+// Level-2 draws of `tile` into a u8 count image (OBRS-2, ob_spec.h: full tiles take sixteen
 // 8-bit draws per Philox call, the partial last tile two 64-bit ones). Wave wv of nw owns
 // replicates [64 wv / nw, 64 (wv+1) / nw). Full tile: replicate r's draws are floor(m/16) whole
 // calls plus, when m % 16 != 0, one part call (index floor(m/16)). The whole calls of the wave's
@@ -1635,7 +1636,7 @@ int engine_point_estimate(ob_panel* p, int ref_mode, double* row, double* resid_
   return rc;
 }
 
-// OBRS-1 resample counts for replicates [first_rep, first_rep + n_reps) without the Gram: level-1
+// OBRS-2 resample counts for replicates [first_rep, first_rep + n_reps) without the Gram: level-1
 // tile counts into d_m1 ([replicate][tile]) and the level-2 count images into d_counts (the
 // ob_engine.hpp layout, replicate batches of 64). Used by the Machado-Mata driver (ob_mm.hip).
 int engine_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_reps, hipStream_t s,
@@ -1643,7 +1644,7 @@ int engine_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_rep
   HIP_OK(hipSetDevice(p->ctx->device));
   if (n_reps == 0) return OB_OK;
   if (first_rep + n_reps > 0xFFFFFFFFull)
-    return ob::fail(OB_E_INVALID, "replicate ids must stay below 2^32 - 1 (OBRS-1 / MM-1 counter word)");
+    return ob::fail(OB_E_INVALID, "replicate ids must stay below 2^32 - 1 (OBRS-2 / MM-1 counter word)");
   const uint32_t tiles = p->ntiles[0] + p->ntiles[1];
   Plan pl = make_plan(p, n_reps, false);
   OB_TRY(ensure_buf(&p->d_m1, p->cap_m1, (size_t)tiles * pl.rep_pad));
@@ -1673,14 +1674,27 @@ int engine_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_rep
   return OB_OK;
 }
 
+int engine_order(ob_panel* p, hipStream_t s) {
+  if (p->order_stream && p->order_stream != s) HIP_OK(hipStreamWaitEvent(s, p->order_ev, 0));
+  return OB_OK;
+}
+
+int engine_mark(ob_panel* p, hipStream_t s) {
+  if (!p->order_ev) HIP_OK(hipEventCreateWithFlags(&p->order_ev, hipEventDisableTiming));
+  HIP_OK(hipEventRecord(p->order_ev, s));
+  p->order_stream = s;
+  return OB_OK;
+}
+
 int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps, int ref_mode, double* d_rows,
                 uint8_t* d_ok, hipStream_t stream) {
   ob_ctx* ctx = p->ctx;
   HIP_OK(hipSetDevice(ctx->device));
   if (n_reps == 0) return OB_OK;
   if (first_rep + n_reps > 0x100000000ull)
-    return ob::fail(OB_E_INVALID, "replicate ids must stay below 2^32 (OBRS-1 counter word)");
+    return ob::fail(OB_E_INVALID, "replicate ids must stay below 2^32 (OBRS-2 counter word)");
   hipStream_t s = stream ? stream : ctx->stream;
+  OB_TRY(engine_order(p, s));  // a previous call on another stream (the digit images, scratch buffers)
   const uint32_t tiles = p->ntiles[0] + p->ntiles[1];
   // segment: at most kSegReps replicates, and a count-image buffer within kCountBudget
   const uint64_t batch_bytes = (uint64_t)std::max(tiles, 1u) * 4 * kCimgWords * sizeof(uint32_t);
@@ -1828,7 +1842,7 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   }
   p->timing_pending = true;
   p->last_stream = s;
-  return OB_OK;
+  return engine_mark(p, s);
 }
 
 // Synchronize the last boot run, sum its per-segment kernel timings and check the
@@ -1858,8 +1872,11 @@ int engine_collect(ob_panel* p) {
   if (p->timing.gram_path == 2) OB_TRY(ob::oz_collect(p));
   uint32_t flag = 0;
   HIP_OK(hipMemcpy(&flag, p->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost));
-  if (flag & 1u) return ob::fail(OB_E_OVERFLOW, "a resampled row was drawn more than 255 times in one replicate");
-  if (flag & 2u)  // p ~ 1e-215 per row and replicate; the f64 Gram path takes counts up to 255
+  // a count of 256+ wraps its byte (bit 0: byte sums differ from the tile counts); on the i8 path
+  // the bound is 127 either way
+  if ((flag & 1u) && p->timing.gram_path != 2)
+    return ob::fail(OB_E_OVERFLOW, "a resampled row was drawn more than 255 times in one replicate");
+  if (flag & 3u)  // p ~ 1e-215 per row and replicate; the f64 Gram path takes counts up to 255
     return ob::fail(OB_E_OVERFLOW, "a resampled row was drawn more than 127 times in one replicate "
                                    "(the i8 Gram's range; OB_GRAM_PATH=f64 runs the f64 MFMA Gram)");
   return OB_OK;
@@ -2084,6 +2101,7 @@ void ob_panel_destroy(ob_panel* p) {
   ob::oz_free(p);
   (void)hipFree(p->d_mm_fail);
   for (hipEvent_t e : p->seg_events) (void)hipEventDestroy(e);
+  if (p->order_ev) (void)hipEventDestroy(p->order_ev);
   if (p->mm_ws_free) p->mm_ws_free(p->mm_ws);
   delete p;
 }
@@ -2148,7 +2166,16 @@ int ob_boot_run(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   return OB_OK;
 }
 
-// Test hook (include/oaxaca_boot.h): the OBRS-1 counts of replicates [first_rep, first_rep + n)
+// Test hook (include/oaxaca_boot.h): the panel's chunk table, as make_plan builds it.
+int ob_debug_chunks(const ob_panel* p, uint32_t* table, int32_t cap, int32_t* n_chunks) {
+  if (!p || !n_chunks || (cap > 0 && !table)) return ob::fail(OB_E_INVALID, "null pointer");
+  const Plan pl = make_plan(p, 64, false);
+  *n_chunks = pl.n_chunks();
+  for (int32_t i = 0; i < 3 * std::min(cap, *n_chunks); ++i) table[i] = pl.chunks[i];
+  return OB_OK;
+}
+
+// Test hook (include/oaxaca_boot.h): the OBRS-2 counts of replicates [first_rep, first_rep + n)
 // exactly as ob_count_kernel leaves them for the Gram kernel, unpacked on the host.
 int ob_debug_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_reps, int group, uint32_t* level1,
                     uint8_t* row_counts) {

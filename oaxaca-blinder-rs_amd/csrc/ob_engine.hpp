@@ -124,6 +124,11 @@ struct ob_panel {
   bool timing_pending = false;
   hipStream_t last_stream = nullptr;
   int pending_segments = 0;
+  // cross-stream order of the calls on one panel: every boot shares the panel's scratch buffers,
+  // digit images and chunk table, so a boot on another stream than the previous one first waits
+  // for order_ev, recorded after the previous call's last kernel (engine_order / engine_mark)
+  hipEvent_t order_ev = nullptr;
+  hipStream_t order_stream = nullptr;
 };
 
 namespace ob {
@@ -131,6 +136,9 @@ int engine_point_estimate(ob_panel* p, int ref_mode, double* row, double* resid_
 int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps, int ref_mode,
                 double* d_rows, uint8_t* d_ok, hipStream_t stream);
 int engine_collect(ob_panel* p);
+// make stream s wait for the panel's previous call when that ran on another stream / mark s as it
+int engine_order(ob_panel* p, hipStream_t s);
+int engine_mark(ob_panel* p, hipStream_t s);
 int engine_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_reps, hipStream_t s,
                   uint32_t* nb_rep, uint32_t* rep_pad);
 // ob_gram_i8.hip

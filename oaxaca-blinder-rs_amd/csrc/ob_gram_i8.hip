@@ -271,24 +271,28 @@ __device__ __forceinline__ void oz_stage(double* vs, int k1p, const double* cols
 }
 
 // Per (chunk, pair): the largest |P| over the chunk's regular rows, as the raw exponent
-// ex + kExpBias (atomicMax; 2^(ex-1) <= max |P| < 2^ex). Grid: the group's tiles.
+// ex + kExpBias (atomicMax; 2^(ex-1) <= max |P| < 2^ex). Grid: (the group's tiles, pair blocks of
+// kPexpPairs): the per-pair accumulators of a block stay within 18 * kPexpPairs bytes of LDS
+// whatever the panel's width (p <= 120: e <= 7,503 pairs).
+constexpr int kPexpPairs = 1024;
 __global__ __launch_bounds__(256) void oz_pexp_kernel(const double* cols, int64_t ld, uint32_t n, int nxy,
                                                       int weighted, int k1, int e, int npp, const int32_t* tile_chunk,
                                                       const int8_t* dev, const int32_t* meta, int32_t* raw,
                                                       unsigned long long* psum) {
   extern __shared__ __attribute__((aligned(16))) double ozs[];
   const int k1p = k1 | 1, tid = threadIdx.x;
+  const int q0 = (int)blockIdx.y * kPexpPairs, ne = min(kPexpPairs, e - q0);  // this block's pairs
   double* vs = ozs;               // [64][k1p]
-  double* mx = ozs + 64 * k1p;    // [e]
-  int32_t* xs = reinterpret_cast<int32_t*>(mx + e);  // [e] exponent sums of the nonzero |P|
-  int32_t* xc = xs + e;                              // [e] their count
-  uint8_t* pa = reinterpret_cast<uint8_t*>(xc + e);
-  uint8_t* pb = pa + e;
+  double* mx = ozs + 64 * k1p;    // [ne]
+  int32_t* xs = reinterpret_cast<int32_t*>(mx + ne);  // [ne] exponent sums of the nonzero |P|
+  int32_t* xc = xs + ne;                              // [ne] their count
+  uint8_t* pa = reinterpret_cast<uint8_t*>(xc + ne);
+  uint8_t* pb = pa + ne;
   const uint32_t tile = blockIdx.x;
   const int chunk = tile_chunk[tile], bits = meta[0];
-  for (int q = tid; q < e; q += 256) {
+  for (int q = tid; q < ne; q += 256) {
     int a, b;
-    oz_pair_cols(q, k1, &a, &b);
+    oz_pair_cols(q0 + q, k1, &a, &b);
     pa[q] = (uint8_t)a;
     pb[q] = (uint8_t)b;
     mx[q] = 0.0;
@@ -299,7 +303,7 @@ __global__ __launch_bounds__(256) void oz_pexp_kernel(const double* cols, int64_
     __syncthreads();
     oz_stage(vs, k1p, cols, ld, n, nxy, weighted, k1, dev, bits, (size_t)tile * 256 + sub * 64);
     __syncthreads();
-    for (int q = tid; q < e; q += 256) {
+    for (int q = tid; q < ne; q += 256) {
       const int a = pa[q], b = pb[q];
       double m = mx[q];
       int sx = 0, sc = 0;
@@ -319,13 +323,14 @@ __global__ __launch_bounds__(256) void oz_pexp_kernel(const double* cols, int64_
       xc[q] += sc;
     }
   }
-  for (int q = tid; q < e; q += 256)
+  for (int q = tid; q < ne; q += 256)
     if (mx[q] > 0.0) {
       int ex = 0;
       (void)frexp(mx[q], &ex);
-      atomicMax(&raw[(size_t)chunk * npp + q], ex + kExpBias);
-      atomicAdd(&psum[2 * ((size_t)chunk * npp + q)], (unsigned long long)(long long)xs[q]);
-      atomicAdd(&psum[2 * ((size_t)chunk * npp + q) + 1], (unsigned long long)xc[q]);
+      const size_t x = (size_t)chunk * npp + q0 + q;
+      atomicMax(&raw[x], ex + kExpBias);
+      atomicAdd(&psum[2 * x], (unsigned long long)(long long)xs[q]);
+      atomicAdd(&psum[2 * x + 1], (unsigned long long)xc[q]);
     }
 }
 
@@ -986,13 +991,16 @@ int oz_prepare(ob_panel* p, hipStream_t s) {
                      p->d_oz_excp);
   OZ_HIP(hipGetLastError());
   const int k1p = p->k1 | 1;
-  const size_t lds_pexp = sizeof(double) * ((size_t)64 * k1p + p->e) + (2 * sizeof(int32_t) + 2) * (size_t)p->e;
+  const int pexp_pairs = std::min(p->e, kPexpPairs), pexp_blocks = (p->e + kPexpPairs - 1) / kPexpPairs;
+  const size_t lds_pexp =
+      sizeof(double) * ((size_t)64 * k1p + pexp_pairs) + (2 * sizeof(int32_t) + 2) * (size_t)pexp_pairs;
   const size_t lds_dig = sizeof(double) * (size_t)64 * k1p;
   OZ_HIP(hipFuncSetAttribute((const void*)oz_pexp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_pexp));
   OZ_HIP(hipFuncSetAttribute((const void*)oz_digits_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_dig));
   for (int g = 0; g < 2; ++g)
     if (p->ntiles[g]) {
-      hipLaunchKernelGGL(oz_pexp_kernel, dim3(p->ntiles[g]), dim3(256), lds_pexp, s, cols[g], p->ld[g], p->n[g], nxy,
+      hipLaunchKernelGGL(oz_pexp_kernel, dim3(p->ntiles[g], pexp_blocks), dim3(256), lds_pexp, s, cols[g], p->ld[g],
+                         p->n[g], nxy,
                          p->weighted, p->k1, p->e, npp, (const int32_t*)p->d_oz_tile_chunk[g],
                          (const int8_t*)p->d_oz_dev[g], (const int32_t*)p->d_oz_meta, p->d_oz_pexp,
                          reinterpret_cast<unsigned long long*>(p->d_oz_psum));

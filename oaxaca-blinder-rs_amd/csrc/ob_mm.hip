@@ -1810,6 +1810,35 @@ int reduced_round(const MmArgs& a, int K, int round, hipStream_t s, MmStats& st)
   return ipm(a2, K, 3, s, st);
 }
 
+// ob_debug_mm_betas (tests only): the per-fit coefficients of slot 0 of the next batch run, per group
+// in simulation order (NaN where the fit failed), and the fit statuses (1 converged).
+struct MmCapture {
+  bool on = false;
+  double* beta = nullptr;  // [2][S][K]
+  uint8_t* done = nullptr;  // [2][S]
+};
+MmCapture g_capture;
+
+int capture_fits(const MmArgs& a, int K, hipStream_t s) {
+  const size_t nf = (size_t)2 * a.S_pad;  // slot 0: fit_index(a, 0, g, j) = g S_pad + j
+  std::vector<uint32_t> lane(nf), fst(nf);
+  std::vector<double> beta(nf * K);
+  MM_OK(hipStreamSynchronize(s));
+  MM_OK(hipMemcpy(lane.data(), a.lane_of, sizeof(uint32_t) * nf, hipMemcpyDeviceToHost));
+  MM_OK(hipMemcpy(fst.data(), a.fstat, sizeof(uint32_t) * nf, hipMemcpyDeviceToHost));
+  MM_OK(hipMemcpy(beta.data(), a.beta, sizeof(double) * nf * K, hipMemcpyDeviceToHost));
+  for (int g = 0; g < 2; ++g)
+    for (int sm = 0; sm < a.S; ++sm) {
+      const size_t f = (size_t)g * a.S_pad + lane[(size_t)g * a.S_pad + sm];
+      const bool ok = fst[f] == kDone;
+      g_capture.done[(size_t)g * a.S + sm] = ok ? 1 : 0;
+      for (int k = 0; k < K; ++k)
+        g_capture.beta[((size_t)g * a.S + sm) * K + k] = ok ? beta[f * K + k] : __builtin_nan("");
+    }
+  g_capture.on = false;
+  return OB_OK;
+}
+
 // One batch of replicate slots: start, IPM iterations (with the row reduction: phase 1 on the
 // subsample, bands, phase 2 on the reduced lists, verification, phase 3 for flagged fits),
 // finish. Rows/ok -> host.
@@ -1924,6 +1953,7 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, MmS
   MM_OK(hipMemcpyAsync(rows_h, a.rows, sizeof(double) * a.n_rb * 3 * a.n_q, hipMemcpyDeviceToHost, s));
   MM_OK(hipMemcpyAsync(ok_h, a.ok, a.n_rb, hipMemcpyDeviceToHost, s));
   MM_OK(hipStreamSynchronize(s));
+  if (g_capture.on) OB_TRY(capture_fits(a, K, s));
   return OB_OK;
 }
 
@@ -2079,7 +2109,7 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
     OB_TRY(run_batch(pa, K, s, rows, ok, st, rd));
     out = 1;
   }
-  // resamples: OBRS-1 count images per segment, then batches of rb_cap slots
+  // resamples: OBRS-2 count images per segment, then batches of rb_cap slots
   const uint64_t seg_cap = 4096;
   for (uint64_t s0 = 0; s0 < n_reps; s0 += seg_cap) {
     const uint32_t ns = (uint32_t)std::min<uint64_t>(seg_cap, n_reps - s0);
@@ -2121,6 +2151,23 @@ extern "C" int ob_mm_run(ob_panel* panel, uint64_t seed, int32_t simulations, co
   if (!panel || !quantiles || !rows || !ok) return ob::fail(OB_E_INVALID, "null pointer");
   return ob::mm_run(panel, seed, simulations, quantiles, n_quantiles, first_rep, n_reps, with_point != 0, rows, ok,
                     nullptr);
+}
+
+// Test hook (include/oaxaca_boot.h): one MM pass (rep = OB_MM_POINT_REP for the point pass) and
+// the coefficients of its 2 x sims quantile regressions.
+extern "C" int ob_debug_mm_betas(ob_panel* p, uint64_t seed, int32_t simulations, uint64_t rep, double* betas,
+                                 uint8_t* done) {
+  if (!p || !betas || !done) return ob::fail(OB_E_INVALID, "null pointer");
+  const double q = 0.5;
+  double row[3];
+  uint8_t ok = 0;
+  g_capture.on = true;
+  g_capture.beta = betas;
+  g_capture.done = done;
+  const bool point = rep == OB_MM_POINT_REP;
+  const int rc = ob::mm_run(p, seed, simulations, &q, 1, point ? 0 : rep, point ? 0 : 1, point, row, &ok, nullptr);
+  g_capture.on = false;
+  return rc;
 }
 
 extern "C" int ob_debug_mm_fail(ob_panel* p, const uint8_t* mask, int32_t sims) {

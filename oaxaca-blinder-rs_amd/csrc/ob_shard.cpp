@@ -1,7 +1,7 @@
 // ob_shard.cpp -- replicates sharded over GPUs with one RCCL all-gather of the per-replicate rows
 // (replaces the Rayon `into_par_iter` of builder.rs:816-839 across devices).
 //
-// A replicate's row is a pure function of (seed, replicate id) and the panel (OBRS-1 counters are
+// A replicate's row is a pure function of (seed, replicate id) and the panel (OBRS-2 counters are
 // global replicate ids; the chunking depends on the panel only), so rank r simply runs replicate
 // ids [first + r*per, first + (r+1)*per) on its own GPU and the gathered rows equal a one-GPU run
 // bit for bit. The only collective is ncclAllGather over xGMI: (n_y x per x row_len) f64 plus
@@ -140,6 +140,7 @@ int shard_compute(ob_panel* p, uint64_t seed, const Shard& sh, int world, int re
   const size_t rl = (size_t)p->row_len, ny = (size_t)p->n_y;
   const int nc = n_gather_cols(p);
   SH_HIP(hipSetDevice(p->ctx->device));
+  OB_TRY(ob::engine_order(p, s));  // the previous call's gather buffers, on another stream
   OB_TRY(ensure_gather_map(p));
   const size_t slots = ny * std::max<uint64_t>(sh.per, 1);
   OB_TRY(ensure_dev(&p->d_shard_rows, &p->cap_shard, slots * rl));
@@ -204,7 +205,7 @@ int shard_deliver(ob_panel* p, const Shard& sh, int world, uint64_t n_reps, doub
     SH_HIP(hipMemcpyAsync(rows, drows, sizeof(double) * ny * n_reps * rl, hipMemcpyDeviceToHost, s));
     SH_HIP(hipMemcpyAsync(ok, dok, ny * n_reps, hipMemcpyDeviceToHost, s));
   }
-  return OB_OK;
+  return ob::engine_mark(p, s);
 }
 
 bool valid_ref(int m) { return m >= OB_REF_GROUP_A && m <= OB_REF_NEUMARK; }

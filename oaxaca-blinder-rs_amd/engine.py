@@ -114,6 +114,15 @@ class Panel:
                                   n_reps, int(bool(with_point)), _dp(rows), ok.ctypes.data_as(C.POINTER(C.c_uint8))))
         return rows, ok
 
+    def debug_mm_betas(self, seed: int, simulations: int, rep: int):
+        """ob_debug_mm_betas: the 2 x simulations QR coefficient vectors of one MM pass (rep =
+        OB_MM_POINT_REP = 2^32 - 1 for the point pass): (betas [2, S, K], converged [2, S])."""
+        b = np.empty((2, int(simulations), self.k))
+        done = np.zeros((2, int(simulations)), dtype=np.uint8)
+        N.check(N.lib().ob_debug_mm_betas(self._h, seed & ((1 << 64) - 1), int(simulations), int(rep), _dp(b),
+                                          done.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return b, done
+
     def debug_mm_fail(self, mask=None):
         """ob_debug_mm_fail: mask[g][s] bit (rep & 7) forces fit (g, s) of pass rep to fail."""
         m = np.ascontiguousarray(np.zeros((2, 0)) if mask is None else mask, dtype=np.uint8)
@@ -140,7 +149,7 @@ class Panel:
                                                    C.c_void_p(rows_ptr), C.c_void_p(ok_ptr), C.c_void_p(stream or 0)))
 
     def debug_counts(self, seed: int, first_rep: int, n_reps: int, group: int):
-        """OBRS-1 counts as the Gram kernel consumes them (ob_debug_counts): (level-1 tile counts
+        """OBRS-2 counts as the Gram kernel consumes them (ob_debug_counts): (level-1 tile counts
         [n_reps, tiles], per-row counts [n_reps, n_g] uint8)."""
         ng = self.n_a if group == 0 else self.n_b
         tiles = -(-ng // 256)
@@ -158,6 +167,14 @@ class Panel:
         g = np.empty((n_reps, 2, e_pad))
         N.check(N.lib().ob_debug_gram(self._h, int(path), seed & ((1 << 64) - 1), first_rep, n_reps, _dp(g)))
         return g
+
+    def debug_chunks(self):
+        """The panel's row chunking (ob_debug_chunks): [(group, first tile, end tile), ...]."""
+        n = C.c_int32(0)
+        N.check(N.lib().ob_debug_chunks(self._h, None, 0, C.byref(n)))
+        t = np.zeros(3 * n.value, dtype=np.uint32)
+        N.check(N.lib().ob_debug_chunks(self._h, t.ctypes.data_as(C.POINTER(C.c_uint32)), n.value, C.byref(n)))
+        return [tuple(int(v) for v in t[3 * c: 3 * c + 3]) for c in range(n.value)]
 
     def set_gather_columns(self, cols=None):
         """Row columns the sharded entry points gather (ob_panel_set_gather_columns); None = all."""

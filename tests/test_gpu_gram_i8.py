@@ -1,7 +1,7 @@
 """The exact integer-sliced Gram (ob_gram_i8.hip) against the f64 MFMA Gram (ob_gram_kernel).
 
 Both compute G_r = sum_i c_ri v_i v_i^T (v = sqrt(w) [1, x, y], ols.rs:68-78) for the same
-OBRS-1 counts. The i8 path's only approximation is the 54-bit fixed-point split of each pair
+OBRS-2 counts. The i8 path's only approximation is the 54-bit fixed-point split of each pair
 product relative to its chunk's power of two (rounding <= 2^-55 of the chunk's largest regular
 |P| per row); rows whose magnitude dwarfs their chunk's ("exception rows": some |v_c| >= 2^B x
 the chunk's geometric-mean scale of column c, or non-finite) are summed in f64 instead
@@ -113,33 +113,44 @@ def test_i8_rows_equal_f64_rows(ob, O):
         panel.close()
 
 
+def test_i8_gram_widest_panel(ob, O):
+    """p = 120 predictors (k1 = 122, 7,503 pairs: the engine's widest panel) on the default i8
+    path: the digit preparation's per-pair LDS is tiled over pair blocks, so the panel
+    runs the i8 Gram instead of failing, and agrees with the f64 Gram to 1e-12 of sqrt(G_aa G_bb)."""
+    d = O.synthetic_panel(3000, 120, True, seed=120)
+    panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"], d["wa"], d["wb"])
+    try:
+        g8 = panel.debug_gram(SEED, 0, 64, path=0)
+        assert panel.timing()["gram_path"] == 2
+        g64 = panel.debug_gram(SEED, 0, 64, path=1)
+        assert _check_gram(g8, g64, 122) < 1e-12
+    finally:
+        panel.close()
+
+
 # ---- exception rows: sentinels, heavy tails, non-finite values ---------------------------------
-def _chunks(na, nb):
-    """ob_engine.hip make_plan: ~64 balanced chunks of whole 256-row tiles per panel."""
+def _halve(chunks):
+    """Each chunk split in two: the chunking a 2x chunk target would give (64 instead of 32)."""
     out = []
-    ta, tb = -(-na // 256), -(-nb // 256)
-    tt = ta + tb
-    for g, tg in ((0, ta), (1, tb)):
-        if tg == 0:
-            continue
-        want = max(1, (64 * tg + tt // 2) // max(tt, 1))
-        nc = min(tg, max(want, -(-tg // 4096)))
-        out += [(g, tg * c // nc, tg * (c + 1) // nc) for c in range(nc)]
+    for g, t0, t1 in chunks:
+        m = (t0 + t1) // 2
+        out += [(g, t0, m), (g, m, t1)] if t1 - t0 > 1 else [(g, t0, t1)]
     return out
 
 
-def _exception_rule(xa, ya, wa, xb, yb, wb, bits_min=8, cap=4096):
-    """numpy restatement of oz_scale/oz_dev/oz_choose/oz_collect (ob_gram_i8.hip): per (chunk,
-    column) s_c = floor(mean frexp exponent of the nonzero finite v_c + 0.5); per row d = max_c
-    min(ex - s_c, 126) (127 if some v_c is not finite); B = the smallest bits >= 8 leaving <= 4096
-    rows with d > B. Returns (B, sorted [(group, row)])."""
+def _exception_rule(xa, ya, wa, xb, yb, wb, chunks, bits_min=8, cap=4096):
+    """numpy restatement of oz_scale/oz_dev/oz_choose/oz_collect (ob_gram_i8.hip) over the chunk
+    table `chunks` [(group, first tile, end tile)] (the engine's, from ob_debug_chunks): per
+    (chunk, column) s_c = floor(mean frexp exponent of the nonzero finite v_c + 0.5); per row d =
+    max_c min(ex - s_c, 126) (127 if some v_c is not finite); B = the smallest bits >= 8 leaving
+    <= 4096 rows with d > B. Returns (B, sorted [(group, row)])."""
     def vmat(x, y, w):
         one = np.ones((x.shape[0], 1))
         v = np.hstack([one, x, y.reshape(len(y), -1)])
         return v * np.sqrt(w)[:, None] if w is not None else v
     vs = [vmat(xa, ya, wa), vmat(xb, yb, wb)]
     devs = [np.full(v.shape[0], -128, dtype=np.int64) for v in vs]
-    for g, t0, t1 in _chunks(len(ya), len(yb)):
+    for g, t0, t1 in chunks:
         v = vs[g][t0 * 256: t1 * 256]
         with np.errstate(invalid="ignore"):
             ex = np.frexp(np.where(np.isfinite(v), v, 0.0))[1].astype(np.int64)
@@ -176,12 +187,42 @@ def test_exception_rows_follow_the_rule(ob, O):
     try:
         panel.debug_gram(SEED, 0, 64, path=2)
         bits, rows = panel.debug_gram_exceptions()
-        b_ref, rows_ref = _exception_rule(xa, ya, wa, xb, yb, wb)
+        b_ref, rows_ref = _exception_rule(xa, ya, wa, xb, yb, wb, panel.debug_chunks())
         assert bits == b_ref == 8 and rows == rows_ref, (bits, rows[:10], rows_ref[:10])
         assert {(0, 1000), (0, 1001), (0, 1002), (1, 4000), (1, 9000)} <= set(rows)
         assert panel.timing()["oz_exceptions"] == len(rows)
     finally:
         panel.close()
+
+
+def test_exception_rule_depends_on_the_chunking(ob, O):
+    """A block of rows scaled by 2^16 that fills a little over half of a chunk at the engine's
+    chunking (and all of the first chunk after halving): the exception list the engine returns is
+    the rule's over the engine's own chunk table, and the rule over the halved table gives a
+    different list -- so the restatement above cannot pass on a stale chunking."""
+    d = O.synthetic_panel(120_000, 4, True, seed=21)
+    xa = d["xa"].copy()
+    chunks = None
+    panel = None
+    try:
+        panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"], d["wa"], d["wb"])
+        chunks = panel.debug_chunks()
+        panel.close()
+        g, t0, t1 = chunks[0]
+        assert g == 0 and t1 - t0 >= 4
+        hi = (t0 + t1) // 2 * 256  # rows [0, hi) of the first chunk of A: the first half-chunk
+        xa[:hi, 1] *= 2.0 ** 16
+        panel = ob.Panel(xa, d["ya"], d["xb"], d["yb"], d["wa"], d["wb"])
+        assert panel.debug_chunks() == chunks
+        panel.debug_gram(SEED, 0, 64, path=2)
+        bits, rows = panel.debug_gram_exceptions()
+    finally:
+        if panel is not None:
+            panel.close()
+    want = _exception_rule(xa, d["ya"], d["wa"], d["xb"], d["yb"], d["wb"], chunks)
+    assert (bits, rows) == want, (bits, len(rows), want[0], len(want[1]))
+    stale = _exception_rule(xa, d["ya"], d["wa"], d["xb"], d["yb"], d["wb"], _halve(chunks))
+    assert stale != want, "the panel does not discriminate the chunking"
 
 
 def test_sentinels_gram_exact_for_replicates_missing_them(ob, O):
@@ -244,7 +285,7 @@ def test_heavy_tailed_covariate_matches_oracle(ob, O):
     try:
         rows, ok = panel.boot(SEED, 0, 128, 0)
         bits, exc = panel.debug_gram_exceptions()
-        assert (bits, exc) == _exception_rule(xa, d["ya"], wa, xb, d["yb"], wb)
+        assert (bits, exc) == _exception_rule(xa, d["ya"], wa, xb, d["yb"], wb, panel.debug_chunks())
     finally:
         panel.close()
     cfg = O.PassConfig(6, 5, 0, True)

@@ -268,3 +268,77 @@ def test_mm_point_pass_failure(ob, O, N):
     assert list(ok) == list(wok) == [0, 1, 1]
     good, worst = close_mm(rows, want, len(QS))
     assert good, worst
+
+
+def _golden_mm():
+    import json
+    import os
+
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "mm_sims.json")) as f:
+        return json.load(f)["cases"]
+
+
+@pytest.mark.parametrize("case", range(2))
+def test_mm_many_simulations_match_golden(ob, case):
+    """configs[4]'s simulation count (1000) and 2500: the finish kernel's LDS bitonic sort then
+    holds several fitted values per thread (256 threads, sort width 1024 / 4096). Rows vs the
+    oracle's (HiGHS-exact fits, MM-1 draws) committed by tests/golden/make_mm_sims.py."""
+    c = _golden_mm()[case]
+    d = mm_data(c["rows"], c["predictors"], seed=c["data_seed"])
+    panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"])
+    try:
+        rows, ok = panel.mm(c["seed"], c["simulations"], c["quantiles"], 0, c["replicates"])
+    finally:
+        panel.close()
+    assert list(ok) == c["ok"] == [1] * (1 + c["replicates"])
+    good, worst = close_mm(rows, np.array(c["pass_rows"]), len(c["quantiles"]))
+    assert good, worst
+
+
+def _qr_objective(x, y, c, beta, tau):
+    r = y - x @ beta
+    return float(np.sum(c * np.where(r >= 0, tau * r, (tau - 1.0) * r)))
+
+
+def test_mm_degenerate_lp_reaches_the_optimum(ob, O):
+    """Integer-valued covariates (years of education, whole years of experience) and an outcome
+    on a 0.5 grid: many rows tie, the QR LP is degenerate and its optimal face is not a point.
+    HiGHS (the oracle) returns a vertex of that face, Clarabel (the reference, an IPM) and the
+    engine's IPM a point inside it, so the coefficients need not agree. What every optimum shares
+    is the objective sum_i c_i rho_tau(y_i - x_i beta) (quantile_regression.rs:22-129): the
+    engine's must equal HiGHS's for every fit, point pass and a resample, to the IPM's stopping
+    rule (1e-9 relative)."""
+    rng = np.random.default_rng(8)
+    d = {}
+    for g, ng in (("a", 400), ("b", 360)):
+        edu = rng.integers(8, 21, ng).astype(float)
+        exp_ = rng.integers(0, 41, ng).astype(float)
+        y = np.round(2.0 * (1.0 + 0.08 * edu + 0.02 * exp_ + rng.standard_t(4, ng) * 0.4)) / 2.0
+        d["x" + g], d["y" + g] = np.column_stack([edu, exp_]), y
+    sims = 24
+    panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"])
+    try:
+        fits = {rep: panel.debug_mm_betas(SEED, sims, rep) for rep in (O.MM_POINT_REP, 3)}
+    finally:
+        panel.close()
+    xs = [O.with_intercept(d["xa"]), O.with_intercept(d["xb"])]
+    ys = [d["ya"], d["yb"]]
+    ties = 0
+    for rep, (betas, done) in fits.items():
+        assert done.all(), (rep, done)
+        for g in (0, 1):
+            n = len(ys[g])
+            c = np.ones(n) if rep == O.MM_POINT_REP else np.bincount(O.resample_indices(SEED, rep, g, n), minlength=n)
+            for s in range(sims):
+                tau = O.mm_tau(SEED, rep, s)
+                bh = O.qr_exact(xs[g], ys[g], c.astype(np.int64), tau)
+                fh = _qr_objective(xs[g], ys[g], c, bh, tau)
+                fe = _qr_objective(xs[g], ys[g], c, betas[g, s], tau)
+                assert abs(fe - fh) <= 1e-9 * (1.0 + abs(fh)), (rep, g, s, tau, fe, fh)
+                # residual signs: no row of positive count lies strictly beyond the optimum's
+                # balance -- the share of the count below the fit is at most tau
+                r = ys[g] - xs[g] @ betas[g, s]
+                tol = 1e-7 * (1.0 + np.abs(ys[g]))
+                assert c[r < -tol].sum() <= tau * c.sum() + 1e-9 and c[r > tol].sum() <= (1 - tau) * c.sum() + 1e-9
+                ties += int(np.abs(bh - betas[g, s]).max() > 1e-6)
+    print(f"degenerate fits whose engine coefficients differ from the HiGHS vertex: {ties} of {4 * sims}")
