@@ -79,6 +79,7 @@ struct GramArgs {
   uint32_t tiles_total;
   int diag;  // OB_GRAM_DIAG bits: 2 no MFMAs, 4 no sub-tile DMA (tools/gram_ablate.py), 8 raw Heckman
              // statuses; count kernel timing ablations (wrong counts): 32 no LDS atomics, 64 no Philox
+  int dbl;   // ob_gram_kernel: 1 = two staged sub-tile buffers (prefetch), 0 = one (k1 > kGramDblMaxK1)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -858,11 +859,12 @@ __global__ __launch_bounds__(kBlock, 2) void ob_gram_kernel(const GramArgs a) {
                                          16, 0, 0);
   };
 
+  const bool dbl = a.dbl != 0;
   if (w.t0 < w.t1) {
     if (a.c_first == 1)
       for (int i = tid; i < kColStride; i += kBlock) {
         xt[i] = 1.0;
-        xt[buf_dbl + i] = 1.0;
+        if (dbl) xt[buf_dbl + i] = 1.0;
       }
     stage_dma(a, w, kXtOff, (size_t)w.t0 * OB_TILE_ROWS, wave, 0, 4, lane, lds3);
     stage_counts(0, w.t0, 0);
@@ -902,13 +904,14 @@ __global__ __launch_bounds__(kBlock, 2) void ob_gram_kernel(const GramArgs a) {
       const bool has_next = !last_sub || tile + 1 < w.t1;
       const uint32_t ntile = last_sub ? tile + 1 : tile, nsub = last_sub ? 0u : s + 1;
       gbase = (size_t)tile * OB_TILE_ROWS + s * 64;
-      if (has_next && dma) {
+      if (has_next && dma && dbl) {
         stage_dma(a, w, kXtOff + (cur ^ 1) * buf_dbl * 8, (size_t)ntile * OB_TILE_ROWS + nsub * 64, wave, 0, 4, lane,
                   lds3);
         stage_counts(cur ^ 1, ntile, nsub);
       }
-      const uint32_t* cw = cimg + cur * kCimgWords + (lane & 15) * kCimgStride;
-      const double* xb = xt + cur * buf_dbl;
+      const int cb_ = dbl ? cur : 0;
+      const uint32_t* cw = cimg + cb_ * kCimgWords + (lane & 15) * kCimgStride;
+      const double* xb = xt + cb_ * buf_dbl;
       if (mma) {
         {
           double va[CB], vb[CB];
@@ -940,6 +943,11 @@ __global__ __launch_bounds__(kBlock, 2) void ob_gram_kernel(const GramArgs a) {
           }
           __builtin_amdgcn_sched_barrier(0);
         }
+      }
+      if (!dbl && has_next && dma) {  // one buffer: every read of this sub-tile done, then refill it
+        lds_barrier();
+        stage_dma(a, w, kXtOff, (size_t)ntile * OB_TILE_ROWS + nsub * 64, wave, 0, 4, lane, lds3);
+        stage_counts(0, ntile, nsub);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next sub-tile has landed
       lds_barrier();
@@ -1305,7 +1313,13 @@ int diag_mode() {
   return m;
 }
 
-size_t gram_lds_bytes(const ob_panel* p) { return (size_t)kXtOff + 2 * (size_t)p->k1 * kColStride * 8; }
+// Two staged sub-tiles (the next one's DMA under this one's MFMAs) while they fit in the 160 KB of
+// LDS (k1 <= 101); wider panels (p up to 120) stage one at a time.
+constexpr size_t kLdsMax = 160 * 1024;
+bool gram_dbl(const ob_panel* p) { return (size_t)kXtOff + 2 * (size_t)p->k1 * kColStride * 8 <= kLdsMax; }
+size_t gram_lds_bytes(const ob_panel* p) {
+  return (size_t)kXtOff + (gram_dbl(p) ? 2 : 1) * (size_t)p->k1 * kColStride * 8;
+}
 
 // The chunking is a function of the panel only (never of the replicate count or the launch),
 // so a replicate's Gram -- summed over chunks in a fixed order -- is bitwise the same however
@@ -1454,6 +1468,7 @@ GramArgs gram_args(const ob_panel* p, const Plan& pl) {
   ga.rep_pad = pl.rep_pad;
   ga.e_pad = p->e_pad;
   ga.flags = p->d_flags;
+  ga.dbl = gram_dbl(p) ? 1 : 0;
   return ga;
 }
 

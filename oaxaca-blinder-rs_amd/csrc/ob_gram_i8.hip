@@ -602,7 +602,11 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   // then A of s + 3 into the register slot s frees. Issue order per sub-tile t: B(t + 4) after
   // B_t, A(t + 3) at the end of step t, so at B_s the loads newer than those of s + 1 are
   // B(s + 3), A(s + 2) (after step s - 1) and B(s + 2) is older than A(s + 1): the wait leaves
-  // PER in flight while two or more sub-tiles follow.
+  // PER in flight. Every step issues the same loads (past the end: the last sub-tile again, into a
+  // stage nobody reads, and a dead A slot), so every step waits the same count and the wait
+  // pattern is a property of the code, not of the chunk length (tools/isa_vmem_check.py checks it
+  // on the built ISA: no DMA older than two barriers at a barrier, no register of an un-waited load
+  // touched).
   auto step = [&](uint32_t s, auto J) {
     constexpr int j = decltype(J)::value;
     const int buf = (int)((s - s0) & (kNbuf - 1));
@@ -612,12 +616,11 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
       if constexpr (!(DIAG & 2)) oz_mfmas<NQ>(acc, 0, ar[j], fb0);
       __builtin_amdgcn_sched_barrier(0);
     }
-    const uint32_t ahead = (DIAG & 4) ? 0u : s1 - 1 - s;  // sub-tiles after s
-    if (ahead >= 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (DIAG & 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
     if constexpr (DIAG & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // timing only: no barrier
     else oz_barrier();
-    if (!(DIAG & 4) && s + kNbuf < s1) dma(buf, s + kNbuf);
+    if constexpr (!(DIAG & 4)) dma(buf, min(s + kNbuf, s1 - 1));
     if constexpr (LIVE) {
       read((buf + 1) & (kNbuf - 1), 0, fb0);
       __builtin_amdgcn_sched_barrier(0);
@@ -658,6 +661,7 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
         v[m][h][i] = ldexp((double)part, shift);
       }
     }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing DMAs (past the end) have landed
   __syncthreads();  // every wave is done with the ring: the exchange overlays it
   double* xch = reinterpret_cast<double*>(smem);  // [batch in tile][64 reps][32 pairs]
   if (grp) {

@@ -122,10 +122,17 @@ def test_i8_gram_widest_panel(ob, O):
     try:
         g8 = panel.debug_gram(SEED, 0, 64, path=0)
         assert panel.timing()["gram_path"] == 2
-        g64 = panel.debug_gram(SEED, 0, 64, path=1)
+        g64 = panel.debug_gram(SEED, 0, 64, path=1)  # f64 MFMA Gram: one staged sub-tile at k1 > 101
         assert _check_gram(g8, g64, 122) < 1e-12
+        row = panel.point_estimate(0)  # the unit Gram (ob_gram_kernel<.., true>) at the same width
     finally:
         panel.close()
+    cfg = O.PassConfig(121, 120, 0, True)
+    rc, orow = O.single_pass(cfg, O.with_intercept(d["xa"]), d["ya"], d["wa"], O.with_intercept(d["xb"]), d["yb"],
+                             d["wb"])
+    assert rc == 0
+    scale = np.maximum(np.abs(orow), abs(orow[5]))
+    assert np.all(np.abs(row - orow) <= 1e-6 * scale)
 
 
 # ---- exception rows: sentinels, heavy tails, non-finite values ---------------------------------
