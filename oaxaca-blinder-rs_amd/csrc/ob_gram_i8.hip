@@ -916,7 +916,9 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
 // LDS exchange). Same ring, half-steps, issue order and uniform waits as oz_gram_body.
 constexpr int kWaves1 = 4;
 
-template <int NS, int NB, bool LIVE>
+// IL: the DMA pieces of the step are issued between groups of (s, 1)'s MFMAs instead of in one run
+// after the barrier (a wave alone on its SIMD has no partner to fill the matrix pipe meanwhile).
+template <int NS, int NB, bool LIVE, bool IL>
 __device__ __forceinline__ void oz_gram1_body(const OzArgs& a, unsigned char* smem, int wave) {
   constexpr int PER = NB + (LIVE ? 4 : 0);
   const ob_v4i* bs = reinterpret_cast<const ob_v4i*>(smem);  // [kNbuf][kSubUnits]
@@ -933,13 +935,14 @@ __device__ __forceinline__ void oz_gram1_body(const OzArgs& a, unsigned char* sm
   const uint32_t s1 = min(a.chunks[3 * chunk + 2] * 4u, (n + 63u) >> 6);
   const ob_v4i* Bg = g ? a.B1 : a.B0;
   const uint32_t batch = rt * 4u + (uint32_t)wave;
-  auto dma = [&](int buf, uint32_t s) {
+  auto dma_piece = [&](int buf, uint32_t s, int t) {
     const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct) * kSubUnits;
+    const int piece = t * kWaves1 + wave;
+    oz_dma16(src + piece * 64 + lane, (uint32_t)(buf * kSubUnits + piece * 64) * 16u);
+  };
+  auto dma = [&](int buf, uint32_t s) {
 #pragma unroll
-    for (int t = 0; t < NB; ++t) {
-      const int piece = t * kWaves1 + wave;
-      oz_dma16(src + piece * 64 + lane, (uint32_t)(buf * kSubUnits + piece * 64) * 16u);
-    }
+    for (int t = 0; t < NB; ++t) dma_piece(buf, s, t);
   };
   ob_v4i ar[3][4];
   auto aload = [&](ob_v4i (&dst)[4], uint32_t s) {
@@ -958,6 +961,14 @@ __device__ __forceinline__ void oz_gram1_body(const OzArgs& a, unsigned char* sm
 #pragma unroll
       for (int m = 0; m < 4; ++m)
         acc[m][q][h] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[m], bf[q], acc[m][q][h], 0, 0, 0);
+  };
+  // MFMAs i in [LO, HI) of a half-step, i = 4 q + m
+  auto mfma_range = [&](ob_v4i (&acc)[4][NS][2], int h, const ob_v4i (&af)[4], const ob_v4i (&bf)[NS], auto LO,
+                        auto HI) {
+    constexpr int lo = decltype(LO)::value, hi = decltype(HI)::value;
+#pragma unroll
+    for (int i = lo; i < hi; ++i)
+      acc[i & 3][i >> 2][h] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[i & 3], bf[i >> 2], acc[i & 3][i >> 2][h], 0, 0, 0);
   };
 
   ob_v4i acc[4][NS][2];
@@ -988,13 +999,42 @@ __device__ __forceinline__ void oz_gram1_body(const OzArgs& a, unsigned char* sm
     }
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
     oz_barrier();
-    dma(buf, min(s + kNbuf, s1 - 1));
-    if constexpr (LIVE) {
+    const uint32_t sd = min(s + kNbuf, s1 - 1);
+    if constexpr (LIVE && IL) {
+      // (s, 1)'s 4 NS MFMAs in NB + 1 groups, one DMA piece after each of the first NB
+      constexpr int G = 4 * NS / (NB + 1);
       read((buf + 1) & (kNbuf - 1), 0, fb0);
       __builtin_amdgcn_sched_barrier(0);
-      mfmas(acc, 1, ar[j], fb1);
+      mfma_range(acc, 1, ar[j], fb1, IC<0>{}, IC<G>{});
+      __builtin_amdgcn_sched_barrier(0);
+      dma_piece(buf, sd, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_range(acc, 1, ar[j], fb1, IC<G>{}, IC<2 * G>{});
+      __builtin_amdgcn_sched_barrier(0);
+      dma_piece(buf, sd, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mfma_range(acc, 1, ar[j], fb1, IC<2 * G>{}, IC<3 * G>{});
+      __builtin_amdgcn_sched_barrier(0);
+      dma_piece(buf, sd, 2);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (NB == 4) {
+        mfma_range(acc, 1, ar[j], fb1, IC<3 * G>{}, IC<4 * G>{});
+        __builtin_amdgcn_sched_barrier(0);
+        dma_piece(buf, sd, 3);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      mfma_range(acc, 1, ar[j], fb1, IC<NB * G>{}, IC<4 * NS>{});
       __builtin_amdgcn_sched_barrier(0);
       aload(ar[j], min(s + 3, s1 - 1));
+    } else {
+      dma(buf, sd);
+      if constexpr (LIVE) {
+        read((buf + 1) & (kNbuf - 1), 0, fb0);
+        __builtin_amdgcn_sched_barrier(0);
+        mfmas(acc, 1, ar[j], fb1);
+        __builtin_amdgcn_sched_barrier(0);
+        aload(ar[j], min(s + 3, s1 - 1));
+      }
     }
   };
   uint32_t s = s0;
@@ -1032,6 +1072,7 @@ __device__ __forceinline__ void oz_gram1_body(const OzArgs& a, unsigned char* sm
   }
 }
 
+template <bool IL>
 __global__ __launch_bounds__(kWaves1 * 64, 1) void oz_gram1_kernel(const OzArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1043,14 +1084,14 @@ __global__ __launch_bounds__(kWaves1 * 64, 1) void oz_gram1_kernel(const OzArgs 
   const bool six = a.nsl[chunk * (uint32_t)a.n_ct + wi % (uint32_t)a.n_ct] == 6;
   // B pieces of a sub-tile: six slices 12 (3 per wave), seven 14 (4 on waves 0-1, 3 on waves 2-3)
   if (six) {
-    if (live) oz_gram1_body<6, 3, true>(a, smem, wave);
-    else oz_gram1_body<6, 3, false>(a, smem, wave);
+    if (live) oz_gram1_body<6, 3, true, IL>(a, smem, wave);
+    else oz_gram1_body<6, 3, false, IL>(a, smem, wave);
   } else if (wave < 2) {
-    if (live) oz_gram1_body<7, 4, true>(a, smem, wave);
-    else oz_gram1_body<7, 4, false>(a, smem, wave);
+    if (live) oz_gram1_body<7, 4, true, IL>(a, smem, wave);
+    else oz_gram1_body<7, 4, false, IL>(a, smem, wave);
   } else {
-    if (live) oz_gram1_body<7, 3, true>(a, smem, wave);
-    else oz_gram1_body<7, 3, false>(a, smem, wave);
+    if (live) oz_gram1_body<7, 3, true, IL>(a, smem, wave);
+    else oz_gram1_body<7, 3, false, IL>(a, smem, wave);
   }
 }
 
@@ -1290,13 +1331,15 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
     else OZ_HIP(launch_la(oz_gram_la_kernel<0>));
     return OB_OK;
   }
-  static const int waves = [] {  // OB_OZ_WAVES=4: one wave per SIMD (oz_gram1_kernel), else 8
-    const char* e = getenv("OB_OZ_WAVES");
-    return e && atoi(e) == 4 ? 4 : 8;
+  static const int waves = [] {  // OB_OZ_WAVES=4: one wave per SIMD (oz_gram1_kernel), 41: its
+    const char* e = getenv("OB_OZ_WAVES");  // DMA-interleaved form; else the 8-wave kernel
+    return e ? atoi(e) : 8;
   }();
-  if (waves == 4 && diag == 0) {
-    OZ_HIP(hipFuncSetAttribute((const void*)oz_gram1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsB));
-    hipLaunchKernelGGL(oz_gram1_kernel, dim3(blocks), dim3(kWaves1 * 64), kLdsB, s, a);
+  if ((waves == 4 || waves == 41) && diag == 0) {
+    const void* k1 = waves == 41 ? (const void*)oz_gram1_kernel<true> : (const void*)oz_gram1_kernel<false>;
+    OZ_HIP(hipFuncSetAttribute(k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsB));
+    if (waves == 41) hipLaunchKernelGGL(oz_gram1_kernel<true>, dim3(blocks), dim3(kWaves1 * 64), kLdsB, s, a);
+    else hipLaunchKernelGGL(oz_gram1_kernel<false>, dim3(blocks), dim3(kWaves1 * 64), kLdsB, s, a);
     OZ_HIP(hipGetLastError());
     return OB_OK;
   }
