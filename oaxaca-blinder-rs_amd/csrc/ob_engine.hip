@@ -2081,6 +2081,7 @@ int ob_panel_create(ob_ctx* ctx, const ob_panel_desc* d, ob_panel** out) {
     hipError_t e = hipMalloc(&p->d_norm, sizeof(int32_t) * packed.size());
     if (e == hipSuccess) e = hipMemcpy(p->d_norm, packed.data(), sizeof(int32_t) * packed.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&p->d_flags, sizeof(uint32_t) * 4);
+    if (e == hipSuccess) e = hipMemset(p->d_flags, 0, sizeof(uint32_t) * 4);  // read by calls that draw nothing
     if (e != hipSuccess) bad(e, __LINE__);
   }
   if (rc != OB_OK) {

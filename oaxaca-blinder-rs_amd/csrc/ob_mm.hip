@@ -2036,6 +2036,8 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   MM_OK(b.reserve(need));
   MM_OK(hipMemcpy(b.quant, quantiles, sizeof(double) * n_q, hipMemcpyHostToDevice));
 
+  // the overflow flag of this call's count images (a point-pass-only call draws none)
+  MM_OK(hipMemsetAsync(p->d_flags, 0, sizeof(uint32_t), s));
   MmArgs a{};
   for (int g = 0; g < 2; ++g) {
     a.cols[g] = p->d_cols[g];

@@ -73,6 +73,21 @@ def test_mm_rows_match_oracle(ob, O, n, p, sims):
     assert good, worst
 
 
+def test_mm_point_pass_only_on_a_fresh_panel(ob, O):
+    """The point pass alone (no bootstrap replicate: no count images drawn) on a panel that never
+    ran a boot: the overflow flag the call checks is its own, not the allocation's garbage."""
+    d = mm_data(900, 2, seed=13)
+    panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"])
+    try:
+        rows, ok = panel.mm(SEED, 16, QS, 0, 0)
+    finally:
+        panel.close()
+    want = oracle_rows(O, d, 16, QS, 0)
+    assert list(ok) == [1]
+    good, worst = close_mm(rows, want, len(QS))
+    assert good, worst
+
+
 def mm_frame(n, seed=4):
     rng = np.random.default_rng(seed)
     g = np.where(rng.random(n) < 0.5, "M", "F")
