@@ -531,7 +531,9 @@ __device__ __forceinline__ void oz_mfmas(ob_v4i (&acc)[4][kSlo][2], int h, const
 // an A fragment holds replicate 16 m + (l & 15), rows 16 (l >> 4) + j of the sub-tile; lane l of a B
 // fragment pair 16 h + (l & 15) of the column tile, the same rows; D: pair 16 h + (l & 15),
 // replicates 16 m + 4 (l >> 4) + i.
-template <int NQ, int SLO, int NB, bool LIVE, int DIAG>
+// PS: B DMA piece t of this wave is piece t * PS + (PS == kWaves ? wave : wave & 3) -- all 8 waves
+// share the pieces (PS = 8), or only the slice-group-1 waves carry them (PS = 4, NB = 0 on group 0).
+template <int NQ, int SLO, int NB, bool LIVE, int DIAG, int PS = kWaves>
 __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* smem, int wave) {
   constexpr int PER = NB + (LIVE ? 4 : 0);  // this wave's vector-memory ops per sub-tile
   const ob_v4i* bs = reinterpret_cast<const ob_v4i*>(smem);  // [kNbuf][kSubUnits]
@@ -556,7 +558,7 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
     const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct) * kSubUnits;  // B: 14 KB
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
-      const int piece = t * kWaves + wave;
+      const int piece = t * PS + (PS == kWaves ? wave : (wave & 3));
       oz_dma16(src + piece * 64 + lane, (uint32_t)(buf * kSubUnits + piece * 64) * 16u);
     }
   };
@@ -873,7 +875,7 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_la_kernel(const OzArgs
   }
 }
 
-template <int DIAG>
+template <int DIAG, bool DG1 = false>
 __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -884,6 +886,30 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
   const uint32_t tq = wi / (uint32_t)a.n_ct, rt = tq % a.n_rt, chunk = tq / a.n_rt;
   const bool live = rt * 4u + (uint32_t)(wave & 3) < a.nb_rep;
   const bool six = a.nsl[chunk * (uint32_t)a.n_ct + wi % (uint32_t)a.n_ct] == 6;
+  // DG1 (OB_OZ_DMA_G1=1): the B pieces ride on the slice-group-1 waves only (fewer MFMAs per step),
+  // so the group-0 waves go from the barrier straight to their MFMAs: six slices 3 pieces each on
+  // waves 4-7; seven 4 on waves 4-5 and 3 on waves 6-7.
+  if constexpr (DG1) {
+    if (six) {
+      if (wave < 4) {
+        if (live) oz_gram_body<kSix0, 0, 0, true, DIAG, 4>(a, smem, wave);
+        else oz_gram_body<kSix0, 0, 0, false, DIAG, 4>(a, smem, wave);
+      } else {
+        if (live) oz_gram_body<6 - kSix0, kSix0, 3, true, DIAG, 4>(a, smem, wave);
+        else oz_gram_body<6 - kSix0, kSix0, 3, false, DIAG, 4>(a, smem, wave);
+      }
+    } else if (wave < 4) {
+      if (live) oz_gram_body<kSlo, 0, 0, true, DIAG, 4>(a, smem, wave);
+      else oz_gram_body<kSlo, 0, 0, false, DIAG, 4>(a, smem, wave);
+    } else if (wave < 6) {
+      if (live) oz_gram_body<kS - kSlo, kSlo, 4, true, DIAG, 4>(a, smem, wave);
+      else oz_gram_body<kS - kSlo, kSlo, 4, false, DIAG, 4>(a, smem, wave);
+    } else {
+      if (live) oz_gram_body<kS - kSlo, kSlo, 3, true, DIAG, 4>(a, smem, wave);
+      else oz_gram_body<kS - kSlo, kSlo, 3, false, DIAG, 4>(a, smem, wave);
+    }
+    return;
+  }
   // waves 0-3: slices 0-3, two B pieces; 4-5: slices 4-6, two B pieces; 6-7: slices 4-6, one piece.
   // Six slices: waves 0-3 take slices 0 .. kSix0 - 1, waves 4-7 the rest of 0-5, one piece each;
   // pieces 12-13 (slice 6) are not loaded.
@@ -904,194 +930,6 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
   } else {
     if (live) oz_gram_body<kS - kSlo, kSlo, 1, true, DIAG>(a, smem, wave);
     else oz_gram_body<kS - kSlo, kSlo, 1, false, DIAG>(a, smem, wave);
-  }
-}
-
-// ---- one wave per SIMD: a wave owns a replicate batch and every slice (OB_OZ_WAVES=4) ------------
-// Block: (chunk, replicate tile of 4 batches, column tile) as above, but 4 waves, wave w = batch w
-// of the tile x all 32 pairs x all NS slices (NS = 6 or 7): 4 NS x 2 accumulators of 16 x 16 i32
-// (192 or 224 registers, one wave per SIMD with the 512-register file). Each batch's A fragments are
-// loaded once per block instead of once per slice group, so a sub-tile step moves 16 KB of A and 12
-// or 14 KB of B from L2 per block instead of 32 KB + B; the slices meet in the wave's registers (no
-// LDS exchange). Same ring, half-steps, issue order and uniform waits as oz_gram_body.
-constexpr int kWaves1 = 4;
-
-// IL: the DMA pieces of the step are issued between groups of (s, 1)'s MFMAs instead of in one run
-// after the barrier (a wave alone on its SIMD has no partner to fill the matrix pipe meanwhile).
-template <int NS, int NB, bool LIVE, bool IL>
-__device__ __forceinline__ void oz_gram1_body(const OzArgs& a, unsigned char* smem, int wave) {
-  constexpr int PER = NB + (LIVE ? 4 : 0);
-  const ob_v4i* bs = reinterpret_cast<const ob_v4i*>(smem);  // [kNbuf][kSubUnits]
-  const int lane = threadIdx.x & 63;
-  const uint32_t nwg = gridDim.x, bid = blockIdx.x;
-  const uint32_t xcd = bid & 7u, slot = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7u;
-  const uint32_t wi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
-  const int ct = (int)(wi % (uint32_t)a.n_ct);
-  const uint32_t tq = wi / (uint32_t)a.n_ct;
-  const uint32_t rt = tq % a.n_rt, chunk = tq / a.n_rt;
-  const uint32_t g = a.chunks[3 * chunk];
-  const uint32_t n = g ? a.n1 : a.n0, tg0 = g ? a.tiles0 : 0u;
-  const uint32_t s0 = a.chunks[3 * chunk + 1] * 4u;
-  const uint32_t s1 = min(a.chunks[3 * chunk + 2] * 4u, (n + 63u) >> 6);
-  const ob_v4i* Bg = g ? a.B1 : a.B0;
-  const uint32_t batch = rt * 4u + (uint32_t)wave;
-  auto dma_piece = [&](int buf, uint32_t s, int t) {
-    const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct) * kSubUnits;
-    const int piece = t * kWaves1 + wave;
-    oz_dma16(src + piece * 64 + lane, (uint32_t)(buf * kSubUnits + piece * 64) * 16u);
-  };
-  auto dma = [&](int buf, uint32_t s) {
-#pragma unroll
-    for (int t = 0; t < NB; ++t) dma_piece(buf, s, t);
-  };
-  ob_v4i ar[3][4];
-  auto aload = [&](ob_v4i (&dst)[4], uint32_t s) {
-    const ob_v4i* src_a = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256 + lane;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) dst[m] = src_a[m * 64];
-  };
-  auto read = [&](int buf, int h, ob_v4i (&bf)[NS]) {
-    const ob_v4i* bb = bs + buf * kSubUnits + h * 64 + lane;
-#pragma unroll
-    for (int q = 0; q < NS; ++q) bf[q] = bb[q * 128];
-  };
-  auto mfmas = [&](ob_v4i (&acc)[4][NS][2], int h, const ob_v4i (&af)[4], const ob_v4i (&bf)[NS]) {
-#pragma unroll
-    for (int q = 0; q < NS; ++q)
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-        acc[m][q][h] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[m], bf[q], acc[m][q][h], 0, 0, 0);
-  };
-  // MFMAs i in [LO, HI) of a half-step, i = 4 q + m
-  auto mfma_range = [&](ob_v4i (&acc)[4][NS][2], int h, const ob_v4i (&af)[4], const ob_v4i (&bf)[NS], auto LO,
-                        auto HI) {
-    constexpr int lo = decltype(LO)::value, hi = decltype(HI)::value;
-#pragma unroll
-    for (int i = lo; i < hi; ++i)
-      acc[i & 3][i >> 2][h] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[i & 3], bf[i >> 2], acc[i & 3][i >> 2][h], 0, 0, 0);
-  };
-
-  ob_v4i acc[4][NS][2];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int q = 0; q < NS; ++q) acc[m][q][0] = acc[m][q][1] = (ob_v4i){};
-  if constexpr (LIVE) {
-    aload(ar[0], s0);
-    aload(ar[1], min(s0 + 1, s1 - 1));
-    aload(ar[2], min(s0 + 2, s1 - 1));
-  }
-#pragma unroll
-  for (int j = 0; j < kNbuf; ++j)
-    if (s0 + j < s1) dma(j, s0 + j);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  ob_v4i fb0[NS], fb1[NS];
-  if constexpr (LIVE) read(0, 0, fb0);
-  auto step = [&](uint32_t s, auto J) {
-    constexpr int j = decltype(J)::value;
-    const int buf = (int)((s - s0) & (kNbuf - 1));
-    if constexpr (LIVE) {
-      read(buf, 1, fb1);
-      __builtin_amdgcn_sched_barrier(0);
-      mfmas(acc, 0, ar[j], fb0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
-    oz_barrier();
-    const uint32_t sd = min(s + kNbuf, s1 - 1);
-    if constexpr (LIVE && IL) {
-      // (s, 1)'s 4 NS MFMAs in NB + 1 groups, one DMA piece after each of the first NB
-      constexpr int G = 4 * NS / (NB + 1);
-      read((buf + 1) & (kNbuf - 1), 0, fb0);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_range(acc, 1, ar[j], fb1, IC<0>{}, IC<G>{});
-      __builtin_amdgcn_sched_barrier(0);
-      dma_piece(buf, sd, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_range(acc, 1, ar[j], fb1, IC<G>{}, IC<2 * G>{});
-      __builtin_amdgcn_sched_barrier(0);
-      dma_piece(buf, sd, 1);
-      __builtin_amdgcn_sched_barrier(0);
-      mfma_range(acc, 1, ar[j], fb1, IC<2 * G>{}, IC<3 * G>{});
-      __builtin_amdgcn_sched_barrier(0);
-      dma_piece(buf, sd, 2);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (NB == 4) {
-        mfma_range(acc, 1, ar[j], fb1, IC<3 * G>{}, IC<4 * G>{});
-        __builtin_amdgcn_sched_barrier(0);
-        dma_piece(buf, sd, 3);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      mfma_range(acc, 1, ar[j], fb1, IC<NB * G>{}, IC<4 * NS>{});
-      __builtin_amdgcn_sched_barrier(0);
-      aload(ar[j], min(s + 3, s1 - 1));
-    } else {
-      dma(buf, sd);
-      if constexpr (LIVE) {
-        read((buf + 1) & (kNbuf - 1), 0, fb0);
-        __builtin_amdgcn_sched_barrier(0);
-        mfmas(acc, 1, ar[j], fb1);
-        __builtin_amdgcn_sched_barrier(0);
-        aload(ar[j], min(s + 3, s1 - 1));
-      }
-    }
-  };
-  uint32_t s = s0;
-  for (; s + 3 <= s1; s += 3) {
-    step(s, IC<0>{});
-    step(s + 1, IC<1>{});
-    step(s + 2, IC<2>{});
-  }
-  if (s < s1) step(s, IC<0>{});
-  if (s + 1 < s1) step(s + 1, IC<1>{});
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing DMAs (past the end) have landed
-  if constexpr (!LIVE) return;
-  // slices -> f64 as oz_gram_body: slices [0, S0) and [S0, NS) meet exactly in int64 (|part| < 2^63
-  // for either group), one ldexp each, then one f64 add -- the same roundings in the same order
-  constexpr int S0 = NS == 6 ? kSix0 : kSlo;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int pair = ct * kPairsPerTile + 16 * h + (lane & 15);
-    const int E = a.pexp[chunk * a.n_pairs_pad + min(pair, a.n_pairs_pad - 1)];
-    const int sh0 = E - kFracBits + 8 * (kS - S0), sh1 = E - kFracBits + 8 * (kS - NS);
-    if (pair >= a.e_pad) continue;
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        long long p0 = 0, p1 = 0;
-#pragma unroll
-        for (int q = 0; q < S0; ++q) p0 = p0 * 256 + acc[m][q][h][i];
-#pragma unroll
-        for (int q = S0; q < NS; ++q) p1 = p1 * 256 + acc[m][q][h][i];
-        const double val = ldexp((double)p0, sh0) + ldexp((double)p1, sh1);
-        const uint32_t rep = batch * 64u + (uint32_t)(16 * m + 4 * (lane >> 4) + i);
-        if (rep < a.n_reps) a.partial[((size_t)chunk * a.rep_pad + rep) * a.e_pad + pair] = val;
-      }
-  }
-}
-
-template <bool IL>
-__global__ __launch_bounds__(kWaves1 * 64, 1) void oz_gram1_kernel(const OzArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t nwg = gridDim.x, bid = blockIdx.x;
-  const uint32_t xcd = bid & 7u, slot = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7u;
-  const uint32_t wi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
-  const uint32_t tq = wi / (uint32_t)a.n_ct, rt = tq % a.n_rt, chunk = tq / a.n_rt;
-  const bool live = rt * 4u + (uint32_t)wave < a.nb_rep;
-  const bool six = a.nsl[chunk * (uint32_t)a.n_ct + wi % (uint32_t)a.n_ct] == 6;
-  // B pieces of a sub-tile: six slices 12 (3 per wave), seven 14 (4 on waves 0-1, 3 on waves 2-3)
-  if (six) {
-    if (live) oz_gram1_body<6, 3, true, IL>(a, smem, wave);
-    else oz_gram1_body<6, 3, false, IL>(a, smem, wave);
-  } else if (wave < 2) {
-    if (live) oz_gram1_body<7, 4, true, IL>(a, smem, wave);
-    else oz_gram1_body<7, 4, false, IL>(a, smem, wave);
-  } else {
-    if (live) oz_gram1_body<7, 3, true, IL>(a, smem, wave);
-    else oz_gram1_body<7, 3, false, IL>(a, smem, wave);
   }
 }
 
@@ -1331,16 +1169,12 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
     else OZ_HIP(launch_la(oz_gram_la_kernel<0>));
     return OB_OK;
   }
-  static const int waves = [] {  // OB_OZ_WAVES=4: one wave per SIMD (oz_gram1_kernel), 41: its
-    const char* e = getenv("OB_OZ_WAVES");  // DMA-interleaved form; else the 8-wave kernel
-    return e ? atoi(e) : 8;
+  static const bool dg1 = [] {
+    const char* e = getenv("OB_OZ_DMA_G1");
+    return e && atoi(e) == 1;
   }();
-  if ((waves == 4 || waves == 41) && diag == 0) {
-    const void* k1 = waves == 41 ? (const void*)oz_gram1_kernel<true> : (const void*)oz_gram1_kernel<false>;
-    OZ_HIP(hipFuncSetAttribute(k1, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsB));
-    if (waves == 41) hipLaunchKernelGGL(oz_gram1_kernel<true>, dim3(blocks), dim3(kWaves1 * 64), kLdsB, s, a);
-    else hipLaunchKernelGGL(oz_gram1_kernel<false>, dim3(blocks), dim3(kWaves1 * 64), kLdsB, s, a);
-    OZ_HIP(hipGetLastError());
+  if (dg1 && diag == 0) {
+    OZ_HIP(launch(oz_gram_kernel<0, true>));
     return OB_OK;
   }
   switch (diag) {

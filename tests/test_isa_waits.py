@@ -19,7 +19,8 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 import isa_vmem_check as C  # noqa: E402
 
 SO = os.path.join(ROOT, "oaxaca-blinder-rs_amd", "liboaxaca_boot.so")
-GRAM = "_ZN12_GLOBAL__N_114oz_gram_kernelILi0EEEvNS_6OzArgsE"
+GRAM = "_ZN12_GLOBAL__N_114oz_gram_kernelILi0ELb0EEEvNS_6OzArgsE"  # oz_gram_kernel<0, false>: the default
+GRAM_DG1 = "_ZN12_GLOBAL__N_114oz_gram_kernelILi0ELb1EEEvNS_6OzArgsE"  # B pieces on slice group 1 only
 
 
 @pytest.fixture(scope="module")
@@ -34,6 +35,14 @@ def test_shipped_gram_kernel_waits_are_clean(gram_isa):
     dma = sum(1 for i in insns if i.mnem.startswith("global_load_lds"))
     bars = sum(1 for i in insns if i.mnem == "s_barrier")
     assert dma >= 64 and bars >= 40, (len(insns), dma, bars)  # the loop bodies were parsed
+    assert C.check(insns) == []
+
+
+def test_group1_dma_variant_waits_are_clean():
+    if not os.path.exists(SO):
+        pytest.skip("engine library missing")
+    insns = C.parse(C.disassemble_symbol(SO, GRAM_DG1), GRAM_DG1)
+    assert sum(1 for i in insns if i.mnem.startswith("global_load_lds")) >= 64
     assert C.check(insns) == []
 
 
