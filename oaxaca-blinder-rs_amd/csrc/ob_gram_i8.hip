@@ -531,9 +531,9 @@ __device__ __forceinline__ void oz_mfmas(ob_v4i (&acc)[4][kSlo][2], int h, const
 // an A fragment holds replicate 16 m + (l & 15), rows 16 (l >> 4) + j of the sub-tile; lane l of a B
 // fragment pair 16 h + (l & 15) of the column tile, the same rows; D: pair 16 h + (l & 15),
 // replicates 16 m + 4 (l >> 4) + i.
-// PS: B DMA piece t of this wave is piece t * PS + (PS == kWaves ? wave : wave & 3) -- all 8 waves
-// share the pieces (PS = 8), or only the slice-group-1 waves carry them (PS = 4, NB = 0 on group 0).
-template <int NQ, int SLO, int NB, bool LIVE, int DIAG, int PS = kWaves>
+// PS, PB: B DMA piece t of this wave is piece PB + t * PS + (PS == kWaves ? wave : wave & 3) -- all 8
+// waves share the pieces (PS = 8), or the 4 waves of a slice group take pieces PB, PB + 4, ... (PS = 4).
+template <int NQ, int SLO, int NB, bool LIVE, int DIAG, int PS = kWaves, int PB = 0>
 __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* smem, int wave) {
   constexpr int PER = NB + (LIVE ? 4 : 0);  // this wave's vector-memory ops per sub-tile
   const ob_v4i* bs = reinterpret_cast<const ob_v4i*>(smem);  // [kNbuf][kSubUnits]
@@ -558,7 +558,7 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
     const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct) * kSubUnits;  // B: 14 KB
 #pragma unroll
     for (int t = 0; t < NB; ++t) {
-      const int piece = t * PS + (PS == kWaves ? wave : (wave & 3));
+      const int piece = PB + t * PS + (PS == kWaves ? wave : (wave & 3));
       oz_dma16(src + piece * 64 + lane, (uint32_t)(buf * kSubUnits + piece * 64) * 16u);
     }
   };
@@ -875,7 +875,7 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_la_kernel(const OzArgs
   }
 }
 
-template <int DIAG, bool DG1 = false>
+template <int DIAG, int DG = 0>
 __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -889,7 +889,29 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
   // DG1 (OB_OZ_DMA_G1=1): the B pieces ride on the slice-group-1 waves only (fewer MFMAs per step),
   // so the group-0 waves go from the barrier straight to their MFMAs: six slices 3 pieces each on
   // waves 4-7; seven 4 on waves 4-5 and 3 on waves 6-7.
-  if constexpr (DG1) {
+  if constexpr (DG == 2) {
+    // DG 2 (OB_OZ_DMA_G1=2): one piece on each group-0 wave (pieces 0-3), the rest on group 1
+    if (six) {
+      if (wave < 4) {
+        if (live) oz_gram_body<kSix0, 0, 1, true, DIAG, 4, 0>(a, smem, wave);
+        else oz_gram_body<kSix0, 0, 1, false, DIAG, 4, 0>(a, smem, wave);
+      } else {
+        if (live) oz_gram_body<6 - kSix0, kSix0, 2, true, DIAG, 4, 4>(a, smem, wave);
+        else oz_gram_body<6 - kSix0, kSix0, 2, false, DIAG, 4, 4>(a, smem, wave);
+      }
+    } else if (wave < 4) {
+      if (live) oz_gram_body<kSlo, 0, 1, true, DIAG, 4, 0>(a, smem, wave);
+      else oz_gram_body<kSlo, 0, 1, false, DIAG, 4, 0>(a, smem, wave);
+    } else if (wave < 6) {
+      if (live) oz_gram_body<kS - kSlo, kSlo, 3, true, DIAG, 4, 4>(a, smem, wave);
+      else oz_gram_body<kS - kSlo, kSlo, 3, false, DIAG, 4, 4>(a, smem, wave);
+    } else {
+      if (live) oz_gram_body<kS - kSlo, kSlo, 2, true, DIAG, 4, 4>(a, smem, wave);
+      else oz_gram_body<kS - kSlo, kSlo, 2, false, DIAG, 4, 4>(a, smem, wave);
+    }
+    return;
+  }
+  if constexpr (DG == 1) {
     if (six) {
       if (wave < 4) {
         if (live) oz_gram_body<kSix0, 0, 0, true, DIAG, 4>(a, smem, wave);
@@ -1169,12 +1191,16 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
     else OZ_HIP(launch_la(oz_gram_la_kernel<0>));
     return OB_OK;
   }
-  static const bool dg1 = [] {
+  static const int dg = [] {
     const char* e = getenv("OB_OZ_DMA_G1");
-    return e && atoi(e) == 1;
+    return e ? atoi(e) : 0;
   }();
-  if (dg1 && diag == 0) {
-    OZ_HIP(launch(oz_gram_kernel<0, true>));
+  if (dg == 1 && diag == 0) {
+    OZ_HIP(launch(oz_gram_kernel<0, 1>));
+    return OB_OK;
+  }
+  if (dg == 2 && diag == 0) {
+    OZ_HIP(launch(oz_gram_kernel<0, 2>));
     return OB_OK;
   }
   switch (diag) {

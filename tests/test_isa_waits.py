@@ -19,8 +19,9 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 import isa_vmem_check as C  # noqa: E402
 
 SO = os.path.join(ROOT, "oaxaca-blinder-rs_amd", "liboaxaca_boot.so")
-GRAM = "_ZN12_GLOBAL__N_114oz_gram_kernelILi0ELb0EEEvNS_6OzArgsE"  # oz_gram_kernel<0, false>: the default
-GRAM_DG1 = "_ZN12_GLOBAL__N_114oz_gram_kernelILi0ELb1EEEvNS_6OzArgsE"  # B pieces on slice group 1 only
+GRAM = "_ZN12_GLOBAL__N_114oz_gram_kernelILi0ELi0EEEvNS_6OzArgsE"  # oz_gram_kernel<0, 0>: the default
+GRAM_DG = ["_ZN12_GLOBAL__N_114oz_gram_kernelILi0ELi1EEEvNS_6OzArgsE",  # B pieces on slice group 1 only
+           "_ZN12_GLOBAL__N_114oz_gram_kernelILi0ELi2EEEvNS_6OzArgsE"]  # 1 piece per group-0 wave
 
 
 @pytest.fixture(scope="module")
@@ -38,10 +39,11 @@ def test_shipped_gram_kernel_waits_are_clean(gram_isa):
     assert C.check(insns) == []
 
 
-def test_group1_dma_variant_waits_are_clean():
+@pytest.mark.parametrize("sym", GRAM_DG)
+def test_dma_split_variants_waits_are_clean(sym):
     if not os.path.exists(SO):
         pytest.skip("engine library missing")
-    insns = C.parse(C.disassemble_symbol(SO, GRAM_DG1), GRAM_DG1)
+    insns = C.parse(C.disassemble_symbol(SO, sym), sym)
     assert sum(1 for i in insns if i.mnem.startswith("global_load_lds")) >= 64
     assert C.check(insns) == []
 
