@@ -509,6 +509,32 @@ struct IC {
   static constexpr int value = N;
 };
 
+// Manual A fragments (MA): the four A units of a sub-tile batch (1 KB apart) by 16-byte loads the
+// compiler does not track (SGPR base + lane offset), waited for by oz_wait_a. The compiler's own
+// waits count only the loads it tracks, so with the B LDS-DMA (untracked) interleaved they forced
+// every DMA issued between two A loads to complete as well: A(s + 1) and B(s + 2) at the start of
+// step s, one step of latency budget. Counted by hand, A(s) is waited for at step s only (2.5 steps
+// after its issue). Round 3's version of this faulted because the last loads' registers were dead
+// and the compiler gave them away while the loads were in flight; every slot is now kept live to a
+// final wait, and tools/isa_vmem_check.py checks the built ISA for any touch of an in-flight
+// load's registers (tests/test_isa_waits.py).
+__device__ __forceinline__ void oz_load_a4(ob_v4i (&d)[4], const ob_v4i* base, uint32_t lane_off) {
+  asm volatile(
+      "global_load_dwordx4 %0, %4, %5\n\t"
+      "global_load_dwordx4 %1, %4, %5 offset:1024\n\t"
+      "global_load_dwordx4 %2, %4, %5 offset:2048\n\t"
+      "global_load_dwordx4 %3, %4, %5 offset:3072"
+      : "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3])
+      : "v"(lane_off), "s"(base)
+      : "memory");
+}
+
+// s_waitcnt vmcnt(N) that the four A registers depend on: no instruction reading them moves above it.
+template <int N>
+__device__ __forceinline__ void oz_wait_a(ob_v4i (&a)[4]) {
+  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]) : "n"(N) : "memory");
+}
+
 // Half-step h of a sub-tile: pair block h (16 pairs) of every slice q < NQ against the four
 // 16-replicate blocks: 4 NQ v_mfma_i32_16x16x64_i8, K = the whole 64-row sub-tile.
 template <int NQ>
@@ -533,7 +559,7 @@ __device__ __forceinline__ void oz_mfmas(ob_v4i (&acc)[4][kSlo][2], int h, const
 // replicates 16 m + 4 (l >> 4) + i.
 // PS, PB: B DMA piece t of this wave is piece PB + t * PS + (PS == kWaves ? wave : wave & 3) -- all 8
 // waves share the pieces (PS = 8), or the 4 waves of a slice group take pieces PB, PB + 4, ... (PS = 4).
-template <int NQ, int SLO, int NB, bool LIVE, int DIAG, int PS = kWaves, int PB = 0>
+template <int NQ, int SLO, int NB, bool LIVE, int DIAG, int PS = kWaves, int PB = 0, bool MA = false>
 __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* smem, int wave) {
   constexpr int PER = NB + (LIVE ? 4 : 0);  // this wave's vector-memory ops per sub-tile
   const ob_v4i* bs = reinterpret_cast<const ob_v4i*>(smem);  // [kNbuf][kSubUnits]
@@ -566,9 +592,14 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   // sub-tile s is 4 x 1 KB, [replicate block][lane]
   ob_v4i ar[3][4];
   auto aload = [&](ob_v4i (&dst)[4], uint32_t s) {
-    const ob_v4i* src_a = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256 + lane;
+    const ob_v4i* blk = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256;
+    if constexpr (MA) {
+      oz_load_a4(dst, blk, (uint32_t)lane * 16u);
+    } else {
+      const ob_v4i* src_a = blk + lane;
 #pragma unroll
-    for (int m = 0; m < 4; ++m) dst[m] = OB_OZ_A_NT ? __builtin_nontemporal_load(src_a + m * 64) : src_a[m * 64];
+      for (int m = 0; m < 4; ++m) dst[m] = OB_OZ_A_NT ? __builtin_nontemporal_load(src_a + m * 64) : src_a[m * 64];
+    }
   };
   // B fragments of half-step h (sub-tile in ring stage buf)
   auto read = [&](int buf, int h, ob_v4i (&bf)[kSlo]) {
@@ -609,16 +640,22 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   // pattern is a property of the code, not of the chunk length (tools/isa_vmem_check.py checks it
   // on the built ISA: no DMA older than two barriers at a barrier, no register of an un-waited load
   // touched).
+  // MA: at step s the loads newer than A(s) (end of step s - 3) are B(s + 2), A(s + 1), B(s + 3),
+  // A(s + 2): A(s) has landed at vmcnt(8 + 2 NB), and with it B(s + 1) (issued before it), so the
+  // barrier needs no wait of its own on a live wave; a wave without A loads waits vmcnt(2 NB).
   auto step = [&](uint32_t s, auto J) {
     constexpr int j = decltype(J)::value;
     const int buf = (int)((s - s0) & (kNbuf - 1));
+    if constexpr (LIVE && MA && !(DIAG & 4)) oz_wait_a<8 + 2 * NB>(ar[j]);
     if constexpr (LIVE) {
       read(buf, 1, fb1);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!(DIAG & 2)) oz_mfmas<NQ>(acc, 0, ar[j], fb0);
+      if (!(DIAG & 2) && s < s1) oz_mfmas<NQ>(acc, 0, ar[j], fb0);
       __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (DIAG & 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if constexpr (MA && LIVE) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + 2 * NB) : "memory");
+    else if constexpr (MA) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NB) : "memory");
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
     if constexpr (DIAG & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // timing only: no barrier
     else oz_barrier();
@@ -626,21 +663,26 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
     if constexpr (LIVE) {
       read((buf + 1) & (kNbuf - 1), 0, fb0);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!(DIAG & 2)) oz_mfmas<NQ>(acc, 1, ar[j], fb1);
+      if (!(DIAG & 2) && s < s1) oz_mfmas<NQ>(acc, 1, ar[j], fb1);
       __builtin_amdgcn_sched_barrier(0);
       // unconditional (past the end: a re-read of the last sub-tile, never used), so the compiler's
       // count of outstanding A loads is exact at every MFMA
       if constexpr (!(DIAG & 4)) aload(ar[j], min(s + 3, s1 - 1));
     }
   };
-  uint32_t s = s0;
-  for (; s + 3 <= s1; s += 3) {
+  // whole groups of three steps: the last group's steps past s1 are ghosts that issue the same loads
+  // (clamped), waits and barriers but no MFMAs, so no path through the loop issues or waits
+  // differently from another (at most two ghost steps per block of ~490 at configs[1])
+  for (uint32_t s = s0; s < s1; s += 3) {
     step(s, IC<0>{});
     step(s + 1, IC<1>{});
     step(s + 2, IC<2>{});
   }
-  if (s < s1) step(s, IC<0>{});
-  if (s + 1 < s1) step(s + 1, IC<1>{});
+  if constexpr (LIVE && MA) {  // the trailing A loads (past the end) land before their registers go
+    oz_wait_a<0>(ar[0]);
+    oz_wait_a<0>(ar[1]);
+    oz_wait_a<0>(ar[2]);
+  }
   // slices -> f64: this wave's digits meet exactly in int64, one ldexp each; group 1 goes through
   // LDS to its group-0 partner, which adds (one rounding) and stores.
   int E[2];
@@ -889,6 +931,27 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
   // DG1 (OB_OZ_DMA_G1=1): the B pieces ride on the slice-group-1 waves only (fewer MFMAs per step),
   // so the group-0 waves go from the barrier straight to their MFMAs: six slices 3 pieces each on
   // waves 4-7; seven 4 on waves 4-5 and 3 on waves 6-7.
+  if constexpr (DG == 3) {  // OB_OZ_DMA_G1=3: manual A waits, the default DMA split
+    if (six) {
+      if (wave < 4) {
+        if (live) oz_gram_body<kSix0, 0, 2, true, DIAG, kWaves, 0, true>(a, smem, wave);
+        else oz_gram_body<kSix0, 0, 2, false, DIAG, kWaves, 0, true>(a, smem, wave);
+      } else {
+        if (live) oz_gram_body<6 - kSix0, kSix0, 1, true, DIAG, kWaves, 0, true>(a, smem, wave);
+        else oz_gram_body<6 - kSix0, kSix0, 1, false, DIAG, kWaves, 0, true>(a, smem, wave);
+      }
+    } else if (wave < 4) {
+      if (live) oz_gram_body<kSlo, 0, 2, true, DIAG, kWaves, 0, true>(a, smem, wave);
+      else oz_gram_body<kSlo, 0, 2, false, DIAG, kWaves, 0, true>(a, smem, wave);
+    } else if (wave < 6) {
+      if (live) oz_gram_body<kS - kSlo, kSlo, 2, true, DIAG, kWaves, 0, true>(a, smem, wave);
+      else oz_gram_body<kS - kSlo, kSlo, 2, false, DIAG, kWaves, 0, true>(a, smem, wave);
+    } else {
+      if (live) oz_gram_body<kS - kSlo, kSlo, 1, true, DIAG, kWaves, 0, true>(a, smem, wave);
+      else oz_gram_body<kS - kSlo, kSlo, 1, false, DIAG, kWaves, 0, true>(a, smem, wave);
+    }
+    return;
+  }
   if constexpr (DG == 2) {
     // DG 2 (OB_OZ_DMA_G1=2): one piece on each group-0 wave (pieces 0-3), the rest on group 1
     if (six) {
@@ -1201,6 +1264,10 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
   }
   if (dg == 2 && diag == 0) {
     OZ_HIP(launch(oz_gram_kernel<0, 2>));
+    return OB_OK;
+  }
+  if (dg == 3 && diag == 0) {
+    OZ_HIP(launch(oz_gram_kernel<0, 3>));
     return OB_OK;
   }
   switch (diag) {
