@@ -559,7 +559,7 @@ __device__ __forceinline__ void oz_mfmas(ob_v4i (&acc)[4][kSlo][2], int h, const
 // replicates 16 m + 4 (l >> 4) + i.
 // PS, PB: B DMA piece t of this wave is piece PB + t * PS + (PS == kWaves ? wave : wave & 3) -- all 8
 // waves share the pieces (PS = 8), or the 4 waves of a slice group take pieces PB, PB + 4, ... (PS = 4).
-template <int NQ, int SLO, int NB, bool LIVE, int DIAG, int PS = kWaves, int PB = 0, bool MA = false>
+template <int NQ, int SLO, int NB, bool LIVE, int DIAG, int PS = kWaves, int PB = 0, bool MA = false, int PRIO = 0>
 __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* smem, int wave) {
   constexpr int PER = NB + (LIVE ? 4 : 0);  // this wave's vector-memory ops per sub-tile
   const ob_v4i* bs = reinterpret_cast<const ob_v4i*>(smem);  // [kNbuf][kSubUnits]
@@ -628,6 +628,7 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   __syncthreads();
   ob_v4i fb0[kSlo], fb1[kSlo];
   if constexpr (LIVE) read(0, 0, fb0);
+  if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);  // static priority (A/B variants)
 
   // Half-step (s, 0): read (s, 1); MFMAs on (s, 0). Barrier B_s: sub-tile s + 1 landed (own loads,
   // then everyone's), every read of sub-tile s done. Refill stage s with B of s + 4. Half-step
@@ -931,24 +932,25 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
   // DG1 (OB_OZ_DMA_G1=1): the B pieces ride on the slice-group-1 waves only (fewer MFMAs per step),
   // so the group-0 waves go from the barrier straight to their MFMAs: six slices 3 pieces each on
   // waves 4-7; seven 4 on waves 4-5 and 3 on waves 6-7.
-  if constexpr (DG == 3) {  // OB_OZ_DMA_G1=3: manual A waits, the default DMA split
+  if constexpr (DG >= 3) {  // OB_OZ_DMA_G1=3: manual A waits, the default DMA split; 4 / 5: with
+    constexpr int P0 = DG == 5 ? 1 : 0, P1 = DG == 4 ? 1 : 0;  // s_setprio 1 on group 1 / group 0
     if (six) {
       if (wave < 4) {
-        if (live) oz_gram_body<kSix0, 0, 2, true, DIAG, kWaves, 0, true>(a, smem, wave);
-        else oz_gram_body<kSix0, 0, 2, false, DIAG, kWaves, 0, true>(a, smem, wave);
+        if (live) oz_gram_body<kSix0, 0, 2, true, DIAG, kWaves, 0, true, P0>(a, smem, wave);
+        else oz_gram_body<kSix0, 0, 2, false, DIAG, kWaves, 0, true, P0>(a, smem, wave);
       } else {
-        if (live) oz_gram_body<6 - kSix0, kSix0, 1, true, DIAG, kWaves, 0, true>(a, smem, wave);
-        else oz_gram_body<6 - kSix0, kSix0, 1, false, DIAG, kWaves, 0, true>(a, smem, wave);
+        if (live) oz_gram_body<6 - kSix0, kSix0, 1, true, DIAG, kWaves, 0, true, P1>(a, smem, wave);
+        else oz_gram_body<6 - kSix0, kSix0, 1, false, DIAG, kWaves, 0, true, P1>(a, smem, wave);
       }
     } else if (wave < 4) {
-      if (live) oz_gram_body<kSlo, 0, 2, true, DIAG, kWaves, 0, true>(a, smem, wave);
-      else oz_gram_body<kSlo, 0, 2, false, DIAG, kWaves, 0, true>(a, smem, wave);
+      if (live) oz_gram_body<kSlo, 0, 2, true, DIAG, kWaves, 0, true, P0>(a, smem, wave);
+      else oz_gram_body<kSlo, 0, 2, false, DIAG, kWaves, 0, true, P0>(a, smem, wave);
     } else if (wave < 6) {
-      if (live) oz_gram_body<kS - kSlo, kSlo, 2, true, DIAG, kWaves, 0, true>(a, smem, wave);
-      else oz_gram_body<kS - kSlo, kSlo, 2, false, DIAG, kWaves, 0, true>(a, smem, wave);
+      if (live) oz_gram_body<kS - kSlo, kSlo, 2, true, DIAG, kWaves, 0, true, P1>(a, smem, wave);
+      else oz_gram_body<kS - kSlo, kSlo, 2, false, DIAG, kWaves, 0, true, P1>(a, smem, wave);
     } else {
-      if (live) oz_gram_body<kS - kSlo, kSlo, 1, true, DIAG, kWaves, 0, true>(a, smem, wave);
-      else oz_gram_body<kS - kSlo, kSlo, 1, false, DIAG, kWaves, 0, true>(a, smem, wave);
+      if (live) oz_gram_body<kS - kSlo, kSlo, 1, true, DIAG, kWaves, 0, true, P1>(a, smem, wave);
+      else oz_gram_body<kS - kSlo, kSlo, 1, false, DIAG, kWaves, 0, true, P1>(a, smem, wave);
     }
     return;
   }
@@ -1268,6 +1270,14 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
   }
   if (dg == 3 && diag == 0) {
     OZ_HIP(launch(oz_gram_kernel<0, 3>));
+    return OB_OK;
+  }
+  if (dg == 4 && diag == 0) {
+    OZ_HIP(launch(oz_gram_kernel<0, 4>));
+    return OB_OK;
+  }
+  if (dg == 5 && diag == 0) {
+    OZ_HIP(launch(oz_gram_kernel<0, 5>));
     return OB_OK;
   }
   switch (diag) {
