@@ -559,7 +559,19 @@ __device__ __forceinline__ void oz_mfmas(ob_v4i (&acc)[4][kSlo][2], int h, const
 // replicates 16 m + 4 (l >> 4) + i.
 // PS, PB: B DMA piece t of this wave is piece PB + t * PS + (PS == kWaves ? wave : wave & 3) -- all 8
 // waves share the pieces (PS = 8), or the 4 waves of a slice group take pieces PB, PB + 4, ... (PS = 4).
-template <int NQ, int SLO, int NB, bool LIVE, int DIAG, int PS = kWaves, int PB = 0, bool MA = false, int PRIO = 0>
+// MFMAs i in [LO, HI) of a half-step (i = 4 q + m), for the DMA-interleaved variant
+template <int LO, int HI>
+__device__ __forceinline__ void oz_mfma_range(ob_v4i (&acc)[4][kSlo][2], int h, const ob_v4i (&af)[4],
+                                              const ob_v4i (&bf)[kSlo]) {
+#pragma unroll
+  for (int i = LO; i < HI; ++i)
+    acc[i & 3][i >> 2][h] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[i & 3], bf[i >> 2], acc[i & 3][i >> 2][h], 0, 0, 0);
+}
+
+// IL: the step's DMA pieces go between groups of (s, 1)'s MFMAs instead of in one run right after
+// the barrier, so the matrix pipe restarts as soon as the barrier releases.
+template <int NQ, int SLO, int NB, bool LIVE, int DIAG, int PS = kWaves, int PB = 0, bool MA = false, int PRIO = 0,
+          bool IL = false>
 __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* smem, int wave) {
   constexpr int PER = NB + (LIVE ? 4 : 0);  // this wave's vector-memory ops per sub-tile
   const ob_v4i* bs = reinterpret_cast<const ob_v4i*>(smem);  // [kNbuf][kSubUnits]
@@ -580,13 +592,14 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   const uint32_t s1 = min(a.chunks[3 * chunk + 2] * 4u, (n + 63u) >> 6);
   const ob_v4i* Bg = g ? a.B1 : a.B0;
   const uint32_t batch = rt * 4u + (uint32_t)wb;
-  auto dma = [&](int buf, uint32_t s) {
+  auto dma_piece = [&](int buf, uint32_t s, int t) {
     const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct) * kSubUnits;  // B: 14 KB
+    const int piece = PB + t * PS + (PS == kWaves ? wave : (wave & 3));
+    oz_dma16(src + piece * 64 + lane, (uint32_t)(buf * kSubUnits + piece * 64) * 16u);
+  };
+  auto dma = [&](int buf, uint32_t s) {
 #pragma unroll
-    for (int t = 0; t < NB; ++t) {
-      const int piece = PB + t * PS + (PS == kWaves ? wave : (wave & 3));
-      oz_dma16(src + piece * 64 + lane, (uint32_t)(buf * kSubUnits + piece * 64) * 16u);
-    }
+    for (int t = 0; t < NB; ++t) dma_piece(buf, s, t);
   };
   // A fragments in registers: three slots, sub-tile s in slot (s - s0) % 3; this wave's batch of
   // sub-tile s is 4 x 1 KB, [replicate block][lane]
@@ -660,15 +673,43 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
     if constexpr (DIAG & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // timing only: no barrier
     else oz_barrier();
-    if constexpr (!(DIAG & 4)) dma(buf, min(s + kNbuf, s1 - 1));
-    if constexpr (LIVE) {
+    if constexpr (IL && LIVE && !(DIAG & 6) && NB > 0) {
+      // (s, 1)'s 4 NQ MFMAs in NB + 1 groups, DMA piece t after group t
+      constexpr int G = 4 * NQ / (NB + 1);
+      const uint32_t sd = min(s + kNbuf, s1 - 1);
+      const bool real = s < s1;
       read((buf + 1) & (kNbuf - 1), 0, fb0);
       __builtin_amdgcn_sched_barrier(0);
-      if (!(DIAG & 2) && s < s1) oz_mfmas<NQ>(acc, 1, ar[j], fb1);
+      if (real) oz_mfma_range<0, G>(acc, 1, ar[j], fb1);
       __builtin_amdgcn_sched_barrier(0);
-      // unconditional (past the end: a re-read of the last sub-tile, never used), so the compiler's
-      // count of outstanding A loads is exact at every MFMA
-      if constexpr (!(DIAG & 4)) aload(ar[j], min(s + 3, s1 - 1));
+      dma_piece(buf, sd, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (NB >= 2) {
+        if (real) oz_mfma_range<G, 2 * G>(acc, 1, ar[j], fb1);
+        __builtin_amdgcn_sched_barrier(0);
+        dma_piece(buf, sd, 1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (NB >= 3) {
+        if (real) oz_mfma_range<2 * G, 3 * G>(acc, 1, ar[j], fb1);
+        __builtin_amdgcn_sched_barrier(0);
+        dma_piece(buf, sd, 2);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (real) oz_mfma_range<NB * G, 4 * NQ>(acc, 1, ar[j], fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      aload(ar[j], min(s + 3, s1 - 1));
+    } else {
+      if constexpr (!(DIAG & 4)) dma(buf, min(s + kNbuf, s1 - 1));
+      if constexpr (LIVE) {
+        read((buf + 1) & (kNbuf - 1), 0, fb0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (!(DIAG & 2) && s < s1) oz_mfmas<NQ>(acc, 1, ar[j], fb1);
+        __builtin_amdgcn_sched_barrier(0);
+        // unconditional (past the end: a re-read of the last sub-tile, never used), so the compiler's
+        // count of outstanding A loads is exact at every MFMA
+        if constexpr (!(DIAG & 4)) aload(ar[j], min(s + 3, s1 - 1));
+      }
     }
   };
   // whole groups of three steps: the last group's steps past s1 are ghosts that issue the same loads
@@ -933,24 +974,25 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
   // so the group-0 waves go from the barrier straight to their MFMAs: six slices 3 pieces each on
   // waves 4-7; seven 4 on waves 4-5 and 3 on waves 6-7.
   if constexpr (DG >= 3) {  // OB_OZ_DMA_G1=3: manual A waits, the default DMA split; 4 / 5: with
-    constexpr int P0 = DG == 5 ? 1 : 0, P1 = DG == 4 ? 1 : 0;  // s_setprio 1 on group 1 / group 0
+    constexpr int P0 = DG == 5 ? 1 : 0, P1 = DG == 4 ? 1 : 0;  // s_setprio 1 on group 1 / group 0;
+    constexpr bool IL = DG == 6;                                 // 6: DMA between the MFMAs
     if (six) {
       if (wave < 4) {
-        if (live) oz_gram_body<kSix0, 0, 2, true, DIAG, kWaves, 0, true, P0>(a, smem, wave);
-        else oz_gram_body<kSix0, 0, 2, false, DIAG, kWaves, 0, true, P0>(a, smem, wave);
+        if (live) oz_gram_body<kSix0, 0, 2, true, DIAG, kWaves, 0, true, P0, IL>(a, smem, wave);
+        else oz_gram_body<kSix0, 0, 2, false, DIAG, kWaves, 0, true, P0, IL>(a, smem, wave);
       } else {
-        if (live) oz_gram_body<6 - kSix0, kSix0, 1, true, DIAG, kWaves, 0, true, P1>(a, smem, wave);
-        else oz_gram_body<6 - kSix0, kSix0, 1, false, DIAG, kWaves, 0, true, P1>(a, smem, wave);
+        if (live) oz_gram_body<6 - kSix0, kSix0, 1, true, DIAG, kWaves, 0, true, P1, IL>(a, smem, wave);
+        else oz_gram_body<6 - kSix0, kSix0, 1, false, DIAG, kWaves, 0, true, P1, IL>(a, smem, wave);
       }
     } else if (wave < 4) {
-      if (live) oz_gram_body<kSlo, 0, 2, true, DIAG, kWaves, 0, true, P0>(a, smem, wave);
-      else oz_gram_body<kSlo, 0, 2, false, DIAG, kWaves, 0, true, P0>(a, smem, wave);
+      if (live) oz_gram_body<kSlo, 0, 2, true, DIAG, kWaves, 0, true, P0, IL>(a, smem, wave);
+      else oz_gram_body<kSlo, 0, 2, false, DIAG, kWaves, 0, true, P0, IL>(a, smem, wave);
     } else if (wave < 6) {
-      if (live) oz_gram_body<kS - kSlo, kSlo, 2, true, DIAG, kWaves, 0, true, P1>(a, smem, wave);
-      else oz_gram_body<kS - kSlo, kSlo, 2, false, DIAG, kWaves, 0, true, P1>(a, smem, wave);
+      if (live) oz_gram_body<kS - kSlo, kSlo, 2, true, DIAG, kWaves, 0, true, P1, IL>(a, smem, wave);
+      else oz_gram_body<kS - kSlo, kSlo, 2, false, DIAG, kWaves, 0, true, P1, IL>(a, smem, wave);
     } else {
-      if (live) oz_gram_body<kS - kSlo, kSlo, 1, true, DIAG, kWaves, 0, true, P1>(a, smem, wave);
-      else oz_gram_body<kS - kSlo, kSlo, 1, false, DIAG, kWaves, 0, true, P1>(a, smem, wave);
+      if (live) oz_gram_body<kS - kSlo, kSlo, 1, true, DIAG, kWaves, 0, true, P1, IL>(a, smem, wave);
+      else oz_gram_body<kS - kSlo, kSlo, 1, false, DIAG, kWaves, 0, true, P1, IL>(a, smem, wave);
     }
     return;
   }
@@ -1278,6 +1320,10 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
   }
   if (dg == 5 && diag == 0) {
     OZ_HIP(launch(oz_gram_kernel<0, 5>));
+    return OB_OK;
+  }
+  if (dg == 6 && diag == 0) {
+    OZ_HIP(launch(oz_gram_kernel<0, 6>));
     return OB_OK;
   }
   switch (diag) {

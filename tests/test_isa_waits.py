@@ -22,7 +22,8 @@ SO = os.path.join(ROOT, "oaxaca-blinder-rs_amd", "liboaxaca_boot.so")
 GRAM = "_ZN12_GLOBAL__N_114oz_gram_kernelILi0ELi0EEEvNS_6OzArgsE"  # oz_gram_kernel<0, 0>: the default
 GRAM_DG = ["_ZN12_GLOBAL__N_114oz_gram_kernelILi0ELi1EEEvNS_6OzArgsE",  # B pieces on slice group 1 only
            "_ZN12_GLOBAL__N_114oz_gram_kernelILi0ELi2EEEvNS_6OzArgsE",  # 1 piece per group-0 wave
-           "_ZN12_GLOBAL__N_114oz_gram_kernelILi0ELi3EEEvNS_6OzArgsE"]  # A loads with manual waits
+           "_ZN12_GLOBAL__N_114oz_gram_kernelILi0ELi3EEEvNS_6OzArgsE",  # A loads with manual waits
+           "_ZN12_GLOBAL__N_114oz_gram_kernelILi0ELi6EEEvNS_6OzArgsE"]  # ... and DMA between the MFMAs
 
 
 @pytest.fixture(scope="module")
