@@ -509,32 +509,6 @@ struct IC {
   static constexpr int value = N;
 };
 
-// Manual A fragments (MA): the four A units of a sub-tile batch (1 KB apart) by 16-byte loads the
-// compiler does not track (SGPR base + lane offset), waited for by oz_wait_a. The compiler's own
-// waits count only the loads it tracks, so with the B LDS-DMA (untracked) interleaved they forced
-// every DMA issued between two A loads to complete as well: A(s + 1) and B(s + 2) at the start of
-// step s, one step of latency budget. Counted by hand, A(s) is waited for at step s only (2.5 steps
-// after its issue). Round 3's version of this faulted because the last loads' registers were dead
-// and the compiler gave them away while the loads were in flight; every slot is now kept live to a
-// final wait, and tools/isa_vmem_check.py checks the built ISA for any touch of an in-flight
-// load's registers (tests/test_isa_waits.py).
-__device__ __forceinline__ void oz_load_a4(ob_v4i (&d)[4], const ob_v4i* base, uint32_t lane_off) {
-  asm volatile(
-      "global_load_dwordx4 %0, %4, %5\n\t"
-      "global_load_dwordx4 %1, %4, %5 offset:1024\n\t"
-      "global_load_dwordx4 %2, %4, %5 offset:2048\n\t"
-      "global_load_dwordx4 %3, %4, %5 offset:3072"
-      : "=&v"(d[0]), "=&v"(d[1]), "=&v"(d[2]), "=&v"(d[3])
-      : "v"(lane_off), "s"(base)
-      : "memory");
-}
-
-// s_waitcnt vmcnt(N) that the four A registers depend on: no instruction reading them moves above it.
-template <int N>
-__device__ __forceinline__ void oz_wait_a(ob_v4i (&a)[4]) {
-  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]) : "n"(N) : "memory");
-}
-
 // Half-step h of a sub-tile: pair block h (16 pairs) of every slice q < NQ against the four
 // 16-replicate blocks: 4 NQ v_mfma_i32_16x16x64_i8, K = the whole 64-row sub-tile.
 template <int NQ>
@@ -557,21 +531,7 @@ __device__ __forceinline__ void oz_mfmas(ob_v4i (&acc)[4][kSlo][2], int h, const
 // an A fragment holds replicate 16 m + (l & 15), rows 16 (l >> 4) + j of the sub-tile; lane l of a B
 // fragment pair 16 h + (l & 15) of the column tile, the same rows; D: pair 16 h + (l & 15),
 // replicates 16 m + 4 (l >> 4) + i.
-// PS, PB: B DMA piece t of this wave is piece PB + t * PS + (PS == kWaves ? wave : wave & 3) -- all 8
-// waves share the pieces (PS = 8), or the 4 waves of a slice group take pieces PB, PB + 4, ... (PS = 4).
-// MFMAs i in [LO, HI) of a half-step (i = 4 q + m), for the DMA-interleaved variant
-template <int LO, int HI>
-__device__ __forceinline__ void oz_mfma_range(ob_v4i (&acc)[4][kSlo][2], int h, const ob_v4i (&af)[4],
-                                              const ob_v4i (&bf)[kSlo]) {
-#pragma unroll
-  for (int i = LO; i < HI; ++i)
-    acc[i & 3][i >> 2][h] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[i & 3], bf[i >> 2], acc[i & 3][i >> 2][h], 0, 0, 0);
-}
-
-// IL: the step's DMA pieces go between groups of (s, 1)'s MFMAs instead of in one run right after
-// the barrier, so the matrix pipe restarts as soon as the barrier releases.
-template <int NQ, int SLO, int NB, bool LIVE, int DIAG, int PS = kWaves, int PB = 0, bool MA = false, int PRIO = 0,
-          bool IL = false>
+template <int NQ, int SLO, int NB, bool LIVE, int DIAG>
 __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* smem, int wave) {
   constexpr int PER = NB + (LIVE ? 4 : 0);  // this wave's vector-memory ops per sub-tile
   const ob_v4i* bs = reinterpret_cast<const ob_v4i*>(smem);  // [kNbuf][kSubUnits]
@@ -592,27 +552,21 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   const uint32_t s1 = min(a.chunks[3 * chunk + 2] * 4u, (n + 63u) >> 6);
   const ob_v4i* Bg = g ? a.B1 : a.B0;
   const uint32_t batch = rt * 4u + (uint32_t)wb;
-  auto dma_piece = [&](int buf, uint32_t s, int t) {
-    const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct) * kSubUnits;  // B: 14 KB
-    const int piece = PB + t * PS + (PS == kWaves ? wave : (wave & 3));
-    oz_dma16(src + piece * 64 + lane, (uint32_t)(buf * kSubUnits + piece * 64) * 16u);
-  };
   auto dma = [&](int buf, uint32_t s) {
+    const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct) * kSubUnits;  // B: 14 KB
 #pragma unroll
-    for (int t = 0; t < NB; ++t) dma_piece(buf, s, t);
+    for (int t = 0; t < NB; ++t) {
+      const int piece = t * kWaves + wave;
+      oz_dma16(src + piece * 64 + lane, (uint32_t)(buf * kSubUnits + piece * 64) * 16u);
+    }
   };
   // A fragments in registers: three slots, sub-tile s in slot (s - s0) % 3; this wave's batch of
   // sub-tile s is 4 x 1 KB, [replicate block][lane]
   ob_v4i ar[3][4];
   auto aload = [&](ob_v4i (&dst)[4], uint32_t s) {
-    const ob_v4i* blk = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256;
-    if constexpr (MA) {
-      oz_load_a4(dst, blk, (uint32_t)lane * 16u);
-    } else {
-      const ob_v4i* src_a = blk + lane;
+    const ob_v4i* src_a = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256 + lane;
 #pragma unroll
-      for (int m = 0; m < 4; ++m) dst[m] = OB_OZ_A_NT ? __builtin_nontemporal_load(src_a + m * 64) : src_a[m * 64];
-    }
+    for (int m = 0; m < 4; ++m) dst[m] = OB_OZ_A_NT ? __builtin_nontemporal_load(src_a + m * 64) : src_a[m * 64];
   };
   // B fragments of half-step h (sub-tile in ring stage buf)
   auto read = [&](int buf, int h, ob_v4i (&bf)[kSlo]) {
@@ -641,7 +595,6 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   __syncthreads();
   ob_v4i fb0[kSlo], fb1[kSlo];
   if constexpr (LIVE) read(0, 0, fb0);
-  if constexpr (PRIO > 0) __builtin_amdgcn_s_setprio(PRIO);  // static priority (A/B variants)
 
   // Half-step (s, 0): read (s, 1); MFMAs on (s, 0). Barrier B_s: sub-tile s + 1 landed (own loads,
   // then everyone's), every read of sub-tile s done. Refill stage s with B of s + 4. Half-step
@@ -653,14 +606,10 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   // stage nobody reads, and a dead A slot), so every step waits the same count and the wait
   // pattern is a property of the code, not of the chunk length (tools/isa_vmem_check.py checks it
   // on the built ISA: no DMA older than two barriers at a barrier, no register of an un-waited load
-  // touched).
-  // MA: at step s the loads newer than A(s) (end of step s - 3) are B(s + 2), A(s + 1), B(s + 3),
-  // A(s + 2): A(s) has landed at vmcnt(8 + 2 NB), and with it B(s + 1) (issued before it), so the
-  // barrier needs no wait of its own on a live wave; a wave without A loads waits vmcnt(2 NB).
+  // touched). Round 4 measured the alternatives to this schedule and kept none.
   auto step = [&](uint32_t s, auto J) {
     constexpr int j = decltype(J)::value;
     const int buf = (int)((s - s0) & (kNbuf - 1));
-    if constexpr (LIVE && MA && !(DIAG & 4)) oz_wait_a<8 + 2 * NB>(ar[j]);
     if constexpr (LIVE) {
       read(buf, 1, fb1);
       __builtin_amdgcn_sched_barrier(0);
@@ -668,48 +617,18 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
       __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (DIAG & 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else if constexpr (MA && LIVE) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(8 + 2 * NB) : "memory");
-    else if constexpr (MA) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NB) : "memory");
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
     if constexpr (DIAG & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // timing only: no barrier
     else oz_barrier();
-    if constexpr (IL && LIVE && !(DIAG & 6) && NB > 0) {
-      // (s, 1)'s 4 NQ MFMAs in NB + 1 groups, DMA piece t after group t
-      constexpr int G = 4 * NQ / (NB + 1);
-      const uint32_t sd = min(s + kNbuf, s1 - 1);
-      const bool real = s < s1;
+    if constexpr (!(DIAG & 4)) dma(buf, min(s + kNbuf, s1 - 1));
+    if constexpr (LIVE) {
       read((buf + 1) & (kNbuf - 1), 0, fb0);
       __builtin_amdgcn_sched_barrier(0);
-      if (real) oz_mfma_range<0, G>(acc, 1, ar[j], fb1);
+      if (!(DIAG & 2) && s < s1) oz_mfmas<NQ>(acc, 1, ar[j], fb1);
       __builtin_amdgcn_sched_barrier(0);
-      dma_piece(buf, sd, 0);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (NB >= 2) {
-        if (real) oz_mfma_range<G, 2 * G>(acc, 1, ar[j], fb1);
-        __builtin_amdgcn_sched_barrier(0);
-        dma_piece(buf, sd, 1);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if constexpr (NB >= 3) {
-        if (real) oz_mfma_range<2 * G, 3 * G>(acc, 1, ar[j], fb1);
-        __builtin_amdgcn_sched_barrier(0);
-        dma_piece(buf, sd, 2);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      if (real) oz_mfma_range<NB * G, 4 * NQ>(acc, 1, ar[j], fb1);
-      __builtin_amdgcn_sched_barrier(0);
-      aload(ar[j], min(s + 3, s1 - 1));
-    } else {
-      if constexpr (!(DIAG & 4)) dma(buf, min(s + kNbuf, s1 - 1));
-      if constexpr (LIVE) {
-        read((buf + 1) & (kNbuf - 1), 0, fb0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (!(DIAG & 2) && s < s1) oz_mfmas<NQ>(acc, 1, ar[j], fb1);
-        __builtin_amdgcn_sched_barrier(0);
-        // unconditional (past the end: a re-read of the last sub-tile, never used), so the compiler's
-        // count of outstanding A loads is exact at every MFMA
-        if constexpr (!(DIAG & 4)) aload(ar[j], min(s + 3, s1 - 1));
-      }
+      // unconditional (past the end: a re-read of the last sub-tile, never used), so the compiler's
+      // count of outstanding A loads is exact at every MFMA
+      if constexpr (!(DIAG & 4)) aload(ar[j], min(s + 3, s1 - 1));
     }
   };
   // whole groups of three steps: the last group's steps past s1 are ghosts that issue the same loads
@@ -719,11 +638,6 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
     step(s, IC<0>{});
     step(s + 1, IC<1>{});
     step(s + 2, IC<2>{});
-  }
-  if constexpr (LIVE && MA) {  // the trailing A loads (past the end) land before their registers go
-    oz_wait_a<0>(ar[0]);
-    oz_wait_a<0>(ar[1]);
-    oz_wait_a<0>(ar[2]);
   }
   // slices -> f64: this wave's digits meet exactly in int64, one ldexp each; group 1 goes through
   // LDS to its group-0 partner, which adds (one rounding) and stores.
@@ -959,7 +873,7 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_la_kernel(const OzArgs
   }
 }
 
-template <int DIAG, int DG = 0>
+template <int DIAG>
 __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -970,76 +884,7 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
   const uint32_t tq = wi / (uint32_t)a.n_ct, rt = tq % a.n_rt, chunk = tq / a.n_rt;
   const bool live = rt * 4u + (uint32_t)(wave & 3) < a.nb_rep;
   const bool six = a.nsl[chunk * (uint32_t)a.n_ct + wi % (uint32_t)a.n_ct] == 6;
-  // DG1 (OB_OZ_DMA_G1=1): the B pieces ride on the slice-group-1 waves only (fewer MFMAs per step),
-  // so the group-0 waves go from the barrier straight to their MFMAs: six slices 3 pieces each on
-  // waves 4-7; seven 4 on waves 4-5 and 3 on waves 6-7.
-  if constexpr (DG >= 3) {  // OB_OZ_DMA_G1=3: manual A waits, the default DMA split; 4 / 5: with
-    constexpr int P0 = DG == 5 ? 1 : 0, P1 = DG == 4 ? 1 : 0;  // s_setprio 1 on group 1 / group 0;
-    constexpr bool IL = DG == 6;                                 // 6: DMA between the MFMAs
-    if (six) {
-      if (wave < 4) {
-        if (live) oz_gram_body<kSix0, 0, 2, true, DIAG, kWaves, 0, true, P0, IL>(a, smem, wave);
-        else oz_gram_body<kSix0, 0, 2, false, DIAG, kWaves, 0, true, P0, IL>(a, smem, wave);
-      } else {
-        if (live) oz_gram_body<6 - kSix0, kSix0, 1, true, DIAG, kWaves, 0, true, P1, IL>(a, smem, wave);
-        else oz_gram_body<6 - kSix0, kSix0, 1, false, DIAG, kWaves, 0, true, P1, IL>(a, smem, wave);
-      }
-    } else if (wave < 4) {
-      if (live) oz_gram_body<kSlo, 0, 2, true, DIAG, kWaves, 0, true, P0, IL>(a, smem, wave);
-      else oz_gram_body<kSlo, 0, 2, false, DIAG, kWaves, 0, true, P0, IL>(a, smem, wave);
-    } else if (wave < 6) {
-      if (live) oz_gram_body<kS - kSlo, kSlo, 2, true, DIAG, kWaves, 0, true, P1, IL>(a, smem, wave);
-      else oz_gram_body<kS - kSlo, kSlo, 2, false, DIAG, kWaves, 0, true, P1, IL>(a, smem, wave);
-    } else {
-      if (live) oz_gram_body<kS - kSlo, kSlo, 1, true, DIAG, kWaves, 0, true, P1, IL>(a, smem, wave);
-      else oz_gram_body<kS - kSlo, kSlo, 1, false, DIAG, kWaves, 0, true, P1, IL>(a, smem, wave);
-    }
-    return;
-  }
-  if constexpr (DG == 2) {
-    // DG 2 (OB_OZ_DMA_G1=2): one piece on each group-0 wave (pieces 0-3), the rest on group 1
-    if (six) {
-      if (wave < 4) {
-        if (live) oz_gram_body<kSix0, 0, 1, true, DIAG, 4, 0>(a, smem, wave);
-        else oz_gram_body<kSix0, 0, 1, false, DIAG, 4, 0>(a, smem, wave);
-      } else {
-        if (live) oz_gram_body<6 - kSix0, kSix0, 2, true, DIAG, 4, 4>(a, smem, wave);
-        else oz_gram_body<6 - kSix0, kSix0, 2, false, DIAG, 4, 4>(a, smem, wave);
-      }
-    } else if (wave < 4) {
-      if (live) oz_gram_body<kSlo, 0, 1, true, DIAG, 4, 0>(a, smem, wave);
-      else oz_gram_body<kSlo, 0, 1, false, DIAG, 4, 0>(a, smem, wave);
-    } else if (wave < 6) {
-      if (live) oz_gram_body<kS - kSlo, kSlo, 3, true, DIAG, 4, 4>(a, smem, wave);
-      else oz_gram_body<kS - kSlo, kSlo, 3, false, DIAG, 4, 4>(a, smem, wave);
-    } else {
-      if (live) oz_gram_body<kS - kSlo, kSlo, 2, true, DIAG, 4, 4>(a, smem, wave);
-      else oz_gram_body<kS - kSlo, kSlo, 2, false, DIAG, 4, 4>(a, smem, wave);
-    }
-    return;
-  }
-  if constexpr (DG == 1) {
-    if (six) {
-      if (wave < 4) {
-        if (live) oz_gram_body<kSix0, 0, 0, true, DIAG, 4>(a, smem, wave);
-        else oz_gram_body<kSix0, 0, 0, false, DIAG, 4>(a, smem, wave);
-      } else {
-        if (live) oz_gram_body<6 - kSix0, kSix0, 3, true, DIAG, 4>(a, smem, wave);
-        else oz_gram_body<6 - kSix0, kSix0, 3, false, DIAG, 4>(a, smem, wave);
-      }
-    } else if (wave < 4) {
-      if (live) oz_gram_body<kSlo, 0, 0, true, DIAG, 4>(a, smem, wave);
-      else oz_gram_body<kSlo, 0, 0, false, DIAG, 4>(a, smem, wave);
-    } else if (wave < 6) {
-      if (live) oz_gram_body<kS - kSlo, kSlo, 4, true, DIAG, 4>(a, smem, wave);
-      else oz_gram_body<kS - kSlo, kSlo, 4, false, DIAG, 4>(a, smem, wave);
-    } else {
-      if (live) oz_gram_body<kS - kSlo, kSlo, 3, true, DIAG, 4>(a, smem, wave);
-      else oz_gram_body<kS - kSlo, kSlo, 3, false, DIAG, 4>(a, smem, wave);
-    }
-    return;
-  }
-  // waves 0-3: slices 0-3, two B pieces; 4-5: slices 4-6, two B pieces; 6-7: slices 4-6, one piece.
+  // B piece t of wave w is 8 t + w. Waves 0-3: slices 0-3, two B pieces; 4-5: slices 4-6, two B pieces; 6-7: slices 4-6, one piece.
   // Six slices: waves 0-3 take slices 0 .. kSix0 - 1, waves 4-7 the rest of 0-5, one piece each;
   // pieces 12-13 (slice 6) are not loaded.
   if (six) {
@@ -1296,34 +1141,6 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
     };
     if (diag == 2) OZ_HIP(launch_la(oz_gram_la_kernel<2>));
     else OZ_HIP(launch_la(oz_gram_la_kernel<0>));
-    return OB_OK;
-  }
-  static const int dg = [] {
-    const char* e = getenv("OB_OZ_DMA_G1");
-    return e ? atoi(e) : 0;
-  }();
-  if (dg == 1 && diag == 0) {
-    OZ_HIP(launch(oz_gram_kernel<0, 1>));
-    return OB_OK;
-  }
-  if (dg == 2 && diag == 0) {
-    OZ_HIP(launch(oz_gram_kernel<0, 2>));
-    return OB_OK;
-  }
-  if (dg == 3 && diag == 0) {
-    OZ_HIP(launch(oz_gram_kernel<0, 3>));
-    return OB_OK;
-  }
-  if (dg == 4 && diag == 0) {
-    OZ_HIP(launch(oz_gram_kernel<0, 4>));
-    return OB_OK;
-  }
-  if (dg == 5 && diag == 0) {
-    OZ_HIP(launch(oz_gram_kernel<0, 5>));
-    return OB_OK;
-  }
-  if (dg == 6 && diag == 0) {
-    OZ_HIP(launch(oz_gram_kernel<0, 6>));
     return OB_OK;
   }
   switch (diag) {
