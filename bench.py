@@ -440,6 +440,21 @@ def end_to_end(ob, ctx, d, ya, yb, n, ref, stat_cols, dev):
                     "replicates + host aggregation, host clock"}
 
 
+def workload_label(strong, taus, total, world, per_rank):
+    """config.workload of the default bench line. A non-strong run at a replicate count other than
+    configs[1]'s 10,000 per GPU is named for what it is: 1,250 is configs[2]'s per-GPU share at 8 GPUs."""
+    if taus:
+        return f"configs[3]: RIF decomposition at tau={taus}, two-fold WLS, GroupA"
+    if strong:
+        return f"configs[2]: {total} replicates per step in total, sharded over {world} GPU(s)"
+    if per_rank == 10000:
+        return "configs[1]: two-fold WLS bootstrap, GroupA reference coefficients"
+    if 10000 % per_rank == 0 and 10000 // per_rank > 1:
+        return (f"configs[2]'s per-GPU share at {10000 // per_rank} GPUs: configs[1]'s panel at {per_rank} "
+                "replicates per GPU per step")
+    return f"configs[1]'s panel at {per_rank} replicates per GPU per step (not a BASELINE config)"
+
+
 def free_port():
     import socket
 
@@ -706,9 +721,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (SURVEY.md §8d wage panel, numpy seed 20260424; OBRS-2 bootstrap seed 0x0B5EED)",
-            "config": {"workload": ("configs[1]: two-fold WLS bootstrap, GroupA reference coefficients" if not args.strong
-                                    else f"configs[2]: {total} replicates per step in total, sharded over {world} GPU(s)")
-                       if not taus else f"configs[3]: RIF decomposition at tau={taus}, two-fold WLS, GroupA",
+            "config": {"workload": workload_label(args.strong, taus, total, world, per_rank),
                        "rows": args.rows, "predictors": args.preds, "weighted": weighted,
                        "replicates_per_step": total, "replicates_per_gpu_per_step": per_rank,
                        "parallelism": f"replicates sharded x{world}, engine RCCL all-gather (ob_boot_run_sharded_device)"},

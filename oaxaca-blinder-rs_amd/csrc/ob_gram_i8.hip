@@ -525,7 +525,9 @@ __device__ __forceinline__ void oz_mfmas(ob_v4i (&acc)[4][kSlo][2], int h, const
 // its B DMA pieces per sub-tile, LIVE = its replicate batch exists. All are wave-uniform template
 // constants, so the loop has no divergent control flow and the compiler's LDS-counter bookkeeping
 // stays exact (a wait only for the fragments an MFMA consumes). DIAG (OB_GRAM_DIAG, timing
-// ablations only, wrong results): 2 no MFMAs, 4 no sub-tile loads after the prologue, 8 no barrier.
+// ablations only, wrong results): 2 no MFMAs, 4 no sub-tile loads after the prologue, 8 no barrier,
+// 16 the MFMAs on zeroed B fragments (same instructions and traffic, no multiplier toggling: the
+// power the data costs).
 // MFMA shape: v_mfma_i32_16x16x64_i8 (the 16x16 forms hold a higher clock than the 32x32 forms on
 // random operands at equal cycles per op, MI355X_MICROARCH.md 'DVFS give-back' item 7). Lane l of
 // an A fragment holds replicate 16 m + (l & 15), rows 16 (l >> 4) + j of the sub-tile; lane l of a B
@@ -573,6 +575,12 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
     const ob_v4i* bb = bs + buf * kSubUnits + (slo * 2 + h) * 64 + lane;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) bf[q] = bb[q * 128];
+    if constexpr (DIAG & 16) {
+      int z;
+      asm volatile("v_mov_b32 %0, 0" : "=v"(z));  // opaque zero: the reads and MFMAs stay
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) bf[q] &= z;
+    }
   };
 
   ob_v4i acc[4][kSlo][2];
@@ -1123,7 +1131,7 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
   a.n_pairs_pad = p->oz_n_ct * kPairsPerTile;
   static const int diag = [] {
     const char* e = getenv("OB_GRAM_DIAG");
-    return e ? atoi(e) & 14 : 0;
+    return e ? atoi(e) & 30 : 0;
   }();
   const uint32_t blocks = (uint32_t)n_chunks * a.n_rt * (uint32_t)a.n_ct;
   auto launch = [&](auto kern) -> hipError_t {
@@ -1148,6 +1156,7 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
     case 4: OZ_HIP(launch(oz_gram_kernel<4>)); break;
     case 6: OZ_HIP(launch(oz_gram_kernel<6>)); break;
     case 8: OZ_HIP(launch(oz_gram_kernel<8>)); break;
+    case 16: OZ_HIP(launch(oz_gram_kernel<16>)); break;
     default: OZ_HIP(launch(oz_gram_kernel<0>)); break;
   }
   return OB_OK;

@@ -344,6 +344,24 @@ __device__ __forceinline__ double mm_rcp(double v) {
   return fma(fma(-v, r, 1.0), r, r);
 }
 
+// One Newton step: enough for a step-length bound, which the step scales by kEta = 0.99995 anyway.
+__device__ __forceinline__ double mm_rcp1(double v) {
+  const double r = __builtin_amdgcn_rcp(v);
+  return fma(fma(-v, r, 1.0), r, r);
+}
+
+// Step-length bounds of one (fit, row) direction (dx, dz, dw) from (x, s = c - x, z, w): the
+// minimum over the components that move toward their bound of distance / |speed|. Every ratio is
+// computed on a safe denominator and selected, so the bounds add no branches to the row's code.
+__device__ __forceinline__ void mm_bounds(double xv, double sv, double zv, double wv, double dx, double dz,
+                                          double dw, double& bp, double& bd) {
+  const double rx = (dx < 0.0 ? -xv : sv) * mm_rcp1(dx != 0.0 ? dx : 1.0);
+  const double rz = -zv * mm_rcp1(dz < 0.0 ? dz : -1.0);
+  const double rw = -wv * mm_rcp1(dw < 0.0 ? dw : -1.0);
+  bp = fmin(bp, dx != 0.0 ? rx : 1e300);
+  bd = fmin(bd, fmin(dz < 0.0 ? rz : 1e300, dw < 0.0 ? rw : 1e300));
+}
+
 // Per-row affine direction from the current state (shared by mm_affine, mm_final and the step
 // replay of mm_assemble).
 struct Affine {
@@ -609,7 +627,7 @@ __device__ __forceinline__ void state_walk(const MmArgs& a, const Blk& b, const 
 }
 
 // [0] primal step bound, [1] dual step bound, [2..4] mu_aff terms, then X'q rho0, X'q rho1.
-template <int K>
+template <int K, bool BB>
 __global__ __launch_bounds__(256, K <= 16 ? 3 : 2) void mm_affine_kernel(const MmArgs a) {
   constexpr int NV = 5 + 2 * K;
   constexpr int NXB = Xs<K>::NXB;
@@ -630,9 +648,13 @@ __global__ __launch_bounds__(256, K <= 16 ? 3 : 2) void mm_affine_kernel(const M
     double q0 = 0.0, q1 = 0.0;
     if (valid) {
       const Affine f = affine_row(xv, zv, wv, c, xr[Xs<K>::Y], dv[0], dv[1]);
-      if (f.dxa != 0.0) acc[0] = fmin(acc[0], (f.dxa < 0.0 ? -f.xv : f.sv) * mm_rcp(f.dxa));
-      if (f.dza < 0.0) acc[1] = fmin(acc[1], -f.zv * mm_rcp(f.dza));
-      if (f.dwa < 0.0) acc[1] = fmin(acc[1], -f.wv * mm_rcp(f.dwa));
+      if constexpr (BB) {
+        mm_bounds(f.xv, f.sv, f.zv, f.wv, f.dxa, f.dza, f.dwa, acc[0], acc[1]);
+      } else {
+        if (f.dxa != 0.0) acc[0] = fmin(acc[0], (f.dxa < 0.0 ? -f.xv : f.sv) * mm_rcp(f.dxa));
+        if (f.dza < 0.0) acc[1] = fmin(acc[1], -f.zv * mm_rcp(f.dza));
+        if (f.dwa < 0.0) acc[1] = fmin(acc[1], -f.wv * mm_rcp(f.dwa));
+      }
       acc[2] += f.xv * f.dza + f.sv * f.dwa;
       acc[3] += f.zv * f.dxa - f.wv * f.dxa;
       acc[4] += f.dxa * f.dza - f.dxa * f.dwa;
@@ -667,7 +689,7 @@ __global__ __launch_bounds__(256, K <= 16 ? 3 : 2) void mm_affine_kernel(const M
 }
 
 // Step-length bounds of the corrector direction (the next assemble replays the direction).
-template <int K>
+template <int K, bool BB>
 __global__ __launch_bounds__(256, 2) void mm_final_kernel(const MmArgs a) {
   __shared__ __attribute__((aligned(16))) double xs[2][kSub * Xs<K>::S];
   __shared__ uint32_t lst[kCap];
@@ -685,10 +707,13 @@ __global__ __launch_bounds__(256, 2) void mm_final_kernel(const MmArgs a) {
     if (!valid) return;
     const Affine f = affine_row(xv, zv, wv, c, xr[Xs<K>::Y], dv[0], dv[1]);
     const Corrector d = corrector_row(f, dv[2], sigmu);
-    const double dx = d.dx, dz = d.dz, dw = d.dw;
-    if (dx != 0.0) acc[0] = fmin(acc[0], (dx < 0.0 ? -f.xv : f.sv) * mm_rcp(dx));
-    if (dz < 0.0) acc[1] = fmin(acc[1], -f.zv * mm_rcp(dz));
-    if (dw < 0.0) acc[1] = fmin(acc[1], -f.wv * mm_rcp(dw));
+    if constexpr (BB) {
+      mm_bounds(f.xv, f.sv, f.zv, f.wv, d.dx, d.dz, d.dw, acc[0], acc[1]);
+    } else {
+      if (d.dx != 0.0) acc[0] = fmin(acc[0], (d.dx < 0.0 ? -f.xv : f.sv) * mm_rcp(d.dx));
+      if (d.dz < 0.0) acc[1] = fmin(acc[1], -f.zv * mm_rcp(d.dz));
+      if (d.dw < 0.0) acc[1] = fmin(acc[1], -f.wv * mm_rcp(d.dw));
+    }
   });
   acc[0] = rows_min(acc[0]);
   acc[1] = rows_min(acc[1]);
@@ -1547,11 +1572,22 @@ struct Kernels {
     else
       hipLaunchKernelGGL((mm_assemble_mfma_kernel<K, false>), grid, dim3(256), 0, s, a, mode);
   }
+  // OB_MM_BB (A/B at K = 16 only): bit 0 branch-free bounds in mm_affine, bit 1 in mm_final
+  static int bb() {
+    static const int v = getenv("OB_MM_BB") ? atoi(getenv("OB_MM_BB")) : 3;
+    return v;
+  }
   static void affine(const MmArgs& a, dim3 grid, hipStream_t s) {
-    hipLaunchKernelGGL(mm_affine_kernel<K>, grid, dim3(256), 0, s, a);
+    if (K != 16 || (bb() & 1))
+      hipLaunchKernelGGL((mm_affine_kernel<K, true>), grid, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((mm_affine_kernel<K, K != 16>), grid, dim3(256), 0, s, a);
   }
   static void final_(const MmArgs& a, dim3 grid, hipStream_t s) {
-    hipLaunchKernelGGL(mm_final_kernel<K>, grid, dim3(256), 0, s, a);
+    if (K != 16 || (bb() & 2))
+      hipLaunchKernelGGL((mm_final_kernel<K, true>), grid, dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL((mm_final_kernel<K, K != 16>), grid, dim3(256), 0, s, a);
   }
   static void classify(const MmArgs& a, dim3 grid, bool verify, hipStream_t s) {
     if (verify)

@@ -50,3 +50,11 @@ def test_gpus_2_without_two_gpus_exits_nonzero():
     assert r.returncode != 0
     assert r.stdout.strip() == "", "no JSON line may be printed for a world the machine cannot run"
     assert "--gpus 2 needs 2 visible GPUs" in r.stderr
+
+
+def test_share_runs_are_labelled_as_configs2_shares():
+    """a 1,250-replicate run is configs[2]'s per-GPU share, not configs[1]."""
+    assert _bench().workload_label(False, None, 10000, 1, 10000).startswith("configs[1]:")
+    assert _bench().workload_label(False, None, 1250, 1, 1250).startswith("configs[2]'s per-GPU share at 8 GPUs")
+    assert _bench().workload_label(True, None, 10000, 8, 1250).startswith("configs[2]:")
+    assert "not a BASELINE config" in _bench().workload_label(False, None, 3000, 1, 3000)
