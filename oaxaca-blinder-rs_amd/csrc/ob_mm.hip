@@ -64,6 +64,10 @@ constexpr int kFitStrideMin = 64;    // ... when a group has at least 64 simulat
 constexpr double kBandKappa = 4.0;   // band half-width in rank units: kappa sqrt(tau (1 - tau) K / m) + 0.01
                                      // (OB_MM_KAPPA overrides it: a tuning knob; results do not depend on it)
 constexpr int kBandSamples = 4096;   // residuals per fit behind its band quantiles
+constexpr double kDelta1 = 3.0;      // phase 1 starts with 3x the shifted start's z/w offset (48 -> 36
+                                     // iterations at configs[4]) ...
+constexpr double kDelta2 = 2.0;      // ... phases 2/3 with twice phase 1's: all fits converge 3 iterations
+                                     // sooner (sweeps: profiles/r04_mm_delta.txt)
 
 enum { FS_TAU, FS_GAP, FS_OBJ, FS_MU, FS_SIGMU, FS_AP, FS_AD, FS_NACT, FS_DELTA, FS_LO, FS_HI, FS_EXT, FS_OBJFIX, kFs };
 
@@ -132,7 +136,13 @@ struct MmArgs {
   // fail_mask[g * fail_sims + s] is set -- the reference's dropped Clarabel fits, on demand
   const uint8_t* fail_mask;
   int fail_sims;
+  double dscale;  // scale of the start's z/w offset (0: 1): phase 1 OB_MM_DELTA1, phases 2/3 kDelta2
+  int list_stat;  // OB_MM_TRACE: the classify pass counts block-list entries against each wave's own needs
 };
+
+// OB_MM_TRACE statistics of the classify pass: [0] (wave, block-list entry) pairs, [1] those whose
+// entry some fit of the wave keeps itself (what per-wave lists would walk)
+__device__ unsigned long long g_mm_list_stat[2];
 
 __device__ __forceinline__ size_t fit_index(const MmArgs& a, uint32_t slot, uint32_t g, int s) {
   return ((size_t)slot * 2 + g) * a.S_pad + s;
@@ -344,24 +354,6 @@ __device__ __forceinline__ double mm_rcp(double v) {
   return fma(fma(-v, r, 1.0), r, r);
 }
 
-// One Newton step: enough for a step-length bound, which the step scales by kEta = 0.99995 anyway.
-__device__ __forceinline__ double mm_rcp1(double v) {
-  const double r = __builtin_amdgcn_rcp(v);
-  return fma(fma(-v, r, 1.0), r, r);
-}
-
-// Step-length bounds of one (fit, row) direction (dx, dz, dw) from (x, s = c - x, z, w): the
-// minimum over the components that move toward their bound of distance / |speed|. Every ratio is
-// computed on a safe denominator and selected, so the bounds add no branches to the row's code.
-__device__ __forceinline__ void mm_bounds(double xv, double sv, double zv, double wv, double dx, double dz,
-                                          double dw, double& bp, double& bd) {
-  const double rx = (dx < 0.0 ? -xv : sv) * mm_rcp1(dx != 0.0 ? dx : 1.0);
-  const double rz = -zv * mm_rcp1(dz < 0.0 ? dz : -1.0);
-  const double rw = -wv * mm_rcp1(dw < 0.0 ? dw : -1.0);
-  bp = fmin(bp, dx != 0.0 ? rx : 1e300);
-  bd = fmin(bd, fmin(dz < 0.0 ? rz : 1e300, dw < 0.0 ? rw : 1e300));
-}
-
 // Per-row affine direction from the current state (shared by mm_affine, mm_final and the step
 // replay of mm_assemble).
 struct Affine {
@@ -436,7 +428,7 @@ __global__ __launch_bounds__(256, K <= 16 ? 2 : 1) void mm_assemble_mfma_kernel(
     tau = a.fs[b.F * kFs + FS_TAU];
     ap = a.fs[b.F * kFs + FS_AP];
     ad = a.fs[b.F * kFs + FS_AD];
-    delta = a.fs[b.F * kFs + FS_DELTA];
+    delta = a.fs[b.F * kFs + FS_DELTA] * (a.dscale > 0.0 ? a.dscale : 1.0);
     sigmu = a.fs[b.F * kFs + FS_SIGMU];
   }
   // B-operand columns (i, j) of this lane (n = fl) per pair block, packed i | j << 8; the zero
@@ -627,7 +619,7 @@ __device__ __forceinline__ void state_walk(const MmArgs& a, const Blk& b, const 
 }
 
 // [0] primal step bound, [1] dual step bound, [2..4] mu_aff terms, then X'q rho0, X'q rho1.
-template <int K, bool BB>
+template <int K>
 __global__ __launch_bounds__(256, K <= 16 ? 3 : 2) void mm_affine_kernel(const MmArgs a) {
   constexpr int NV = 5 + 2 * K;
   constexpr int NXB = Xs<K>::NXB;
@@ -648,13 +640,9 @@ __global__ __launch_bounds__(256, K <= 16 ? 3 : 2) void mm_affine_kernel(const M
     double q0 = 0.0, q1 = 0.0;
     if (valid) {
       const Affine f = affine_row(xv, zv, wv, c, xr[Xs<K>::Y], dv[0], dv[1]);
-      if constexpr (BB) {
-        mm_bounds(f.xv, f.sv, f.zv, f.wv, f.dxa, f.dza, f.dwa, acc[0], acc[1]);
-      } else {
-        if (f.dxa != 0.0) acc[0] = fmin(acc[0], (f.dxa < 0.0 ? -f.xv : f.sv) * mm_rcp(f.dxa));
-        if (f.dza < 0.0) acc[1] = fmin(acc[1], -f.zv * mm_rcp(f.dza));
-        if (f.dwa < 0.0) acc[1] = fmin(acc[1], -f.wv * mm_rcp(f.dwa));
-      }
+      if (f.dxa != 0.0) acc[0] = fmin(acc[0], (f.dxa < 0.0 ? -f.xv : f.sv) * mm_rcp(f.dxa));
+      if (f.dza < 0.0) acc[1] = fmin(acc[1], -f.zv * mm_rcp(f.dza));
+      if (f.dwa < 0.0) acc[1] = fmin(acc[1], -f.wv * mm_rcp(f.dwa));
       acc[2] += f.xv * f.dza + f.sv * f.dwa;
       acc[3] += f.zv * f.dxa - f.wv * f.dxa;
       acc[4] += f.dxa * f.dza - f.dxa * f.dwa;
@@ -689,7 +677,7 @@ __global__ __launch_bounds__(256, K <= 16 ? 3 : 2) void mm_affine_kernel(const M
 }
 
 // Step-length bounds of the corrector direction (the next assemble replays the direction).
-template <int K, bool BB>
+template <int K>
 __global__ __launch_bounds__(256, 2) void mm_final_kernel(const MmArgs a) {
   __shared__ __attribute__((aligned(16))) double xs[2][kSub * Xs<K>::S];
   __shared__ uint32_t lst[kCap];
@@ -707,13 +695,10 @@ __global__ __launch_bounds__(256, 2) void mm_final_kernel(const MmArgs a) {
     if (!valid) return;
     const Affine f = affine_row(xv, zv, wv, c, xr[Xs<K>::Y], dv[0], dv[1]);
     const Corrector d = corrector_row(f, dv[2], sigmu);
-    if constexpr (BB) {
-      mm_bounds(f.xv, f.sv, f.zv, f.wv, d.dx, d.dz, d.dw, acc[0], acc[1]);
-    } else {
-      if (d.dx != 0.0) acc[0] = fmin(acc[0], (d.dx < 0.0 ? -f.xv : f.sv) * mm_rcp(d.dx));
-      if (d.dz < 0.0) acc[1] = fmin(acc[1], -f.zv * mm_rcp(d.dz));
-      if (d.dw < 0.0) acc[1] = fmin(acc[1], -f.wv * mm_rcp(d.dw));
-    }
+    const double dx = d.dx, dz = d.dz, dw = d.dw;
+    if (dx != 0.0) acc[0] = fmin(acc[0], (dx < 0.0 ? -f.xv : f.sv) * mm_rcp(dx));
+    if (dz < 0.0) acc[1] = fmin(acc[1], -f.zv * mm_rcp(dz));
+    if (dw < 0.0) acc[1] = fmin(acc[1], -f.wv * mm_rcp(dw));
   });
   acc[0] = rows_min(acc[0]);
   acc[1] = rows_min(acc[1]);
@@ -1275,6 +1260,7 @@ __global__ __launch_bounds__(256, 2) void mm_classify_kernel(const MmArgs a) {
     return;
   }
   const uint32_t nsub = (b.n_ent + kSub - 1) / kSub;
+  uint32_t st_need = 0, st_all = 0;  // a.list_stat
   double stg[Xs<K>::Stage], lv = 0.0;
   uint32_t xb1 = 0u;
   auto side_load = [&](uint32_t t) {  // threads < 64: row t * kSub + tid's leverage and added bit
@@ -1318,6 +1304,11 @@ __global__ __launch_bounds__(256, 2) void mm_classify_kernel(const MmArgs a) {
       // rows added after an earlier verification are in the list too (a row flagged in this pass
       // is set after the barrier below, so within a sub-tile the bits read here are the old ones)
       if (in || (e < b.n_ent && XB[4 * j + b.rl])) kp[4 * j + b.rl] = 1u;
+      if (!VERIFY && a.list_stat) {
+        const unsigned long long m = __ballot(in || (valid && XB[4 * j + b.rl]));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st_need += ((m >> (16 * r)) & 0xffffull) != 0ull ? 1u : 0u;
+      }
       if (VERIFY) {
         const double rv = y - dots[ND - 1][j & 3], eps = 1e-9 * (1.0 + fabs(y));
         const uint32_t sd = in ? 1u : (rh > hi + x ? 2u : 0u);
@@ -1331,6 +1322,11 @@ __global__ __launch_bounds__(256, 2) void mm_classify_kernel(const MmArgs a) {
       const bool valid = part && e < b.n_ent;
       const bool kept = kp[4 * j + b.rl] != 0u;
       const uint32_t sd = (side >> (2 * j)) & 3u;
+      if (!VERIFY && a.list_stat) {  // entries of the block's list
+        const unsigned long long m = __ballot(kept && e < b.n_ent);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) st_all += ((m >> (16 * r)) & 0xffffull) != 0ull ? 1u : 0u;
+      }
       const double* xr = X + (4 * j + b.rl) * S;
       const double y = xr[Xs<K>::Y];
       if (!VERIFY) {
@@ -1359,6 +1355,11 @@ __global__ __launch_bounds__(256, 2) void mm_classify_kernel(const MmArgs a) {
     xs_store<K>(xs[(t + 1) & 1], stg);  // the other buffers were last read before the previous barrier
     side_store((t + 1) & 1);
     __syncthreads();
+  }
+  const bool wpart = __ballot(part) != 0ull;  // the wave has a fit in this round
+  if (!VERIFY && a.list_stat && b.lane == 0 && wpart) {
+    atomicAdd(&g_mm_list_stat[0], (unsigned long long)st_all);
+    atomicAdd(&g_mm_list_stat[1], (unsigned long long)st_need);
   }
   if (!VERIFY) {
     if (threadIdx.x == 0) {
@@ -1572,22 +1573,11 @@ struct Kernels {
     else
       hipLaunchKernelGGL((mm_assemble_mfma_kernel<K, false>), grid, dim3(256), 0, s, a, mode);
   }
-  // OB_MM_BB (A/B at K = 16 only): bit 0 branch-free bounds in mm_affine, bit 1 in mm_final
-  static int bb() {
-    static const int v = getenv("OB_MM_BB") ? atoi(getenv("OB_MM_BB")) : 3;
-    return v;
-  }
   static void affine(const MmArgs& a, dim3 grid, hipStream_t s) {
-    if (K != 16 || (bb() & 1))
-      hipLaunchKernelGGL((mm_affine_kernel<K, true>), grid, dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL((mm_affine_kernel<K, K != 16>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(mm_affine_kernel<K>, grid, dim3(256), 0, s, a);
   }
   static void final_(const MmArgs& a, dim3 grid, hipStream_t s) {
-    if (K != 16 || (bb() & 2))
-      hipLaunchKernelGGL((mm_final_kernel<K, true>), grid, dim3(256), 0, s, a);
-    else
-      hipLaunchKernelGGL((mm_final_kernel<K, K != 16>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(mm_final_kernel<K>, grid, dim3(256), 0, s, a);
   }
   static void classify(const MmArgs& a, dim3 grid, bool verify, hipStream_t s) {
     if (verify)
@@ -1833,8 +1823,21 @@ int reduced_round(const MmArgs& a, int K, int round, hipStream_t s, MmStats& st)
   const dim3 grid(nch, a.S_pad / 64, a.n_rb);
   const unsigned fit_blocks = (unsigned)((n_fits + 255) / 256);
   MM_OK(hipMemsetAsync(a.active_rows, 0, sizeof(unsigned long long), s));
-  pass(K, 3, a, grid, 0, s);  // classify: block lists + fixed-row sums
+  MmArgs ac = a;
+  ac.list_stat = trace() && round == 0;
+  if (ac.list_stat) {
+    const unsigned long long z[2] = {0ull, 0ull};
+    MM_OK(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_mm_list_stat), z, sizeof(z), 0, hipMemcpyHostToDevice, s));
+  }
+  pass(K, 3, ac, grid, 0, s);  // classify: block lists + fixed-row sums
   MM_OK(hipGetLastError());
+  if (ac.list_stat) {
+    unsigned long long v[2];
+    MM_OK(hipMemcpyFromSymbolAsync(v, HIP_SYMBOL(g_mm_list_stat), sizeof(v), 0, hipMemcpyDeviceToHost, s));
+    MM_OK(hipStreamSynchronize(s));
+    fprintf(stderr, "[mm] block lists: %llu (wave, entry) pairs, %llu (%.1f %%) needed by a fit of the wave\n", v[0],
+            v[1], v[0] ? 100.0 * (double)v[1] / (double)v[0] : 0.0);
+  }
   MM_OK(reduce_partials(a, nv_cls(K), 0, 0, s));
   hipLaunchKernelGGL(mm_bvec_kernel, dim3(fit_blocks), dim3(256), 0, s, a, K, n_fits, round == 0 ? 1 : 0);
   MM_OK(hipGetLastError());
@@ -1843,6 +1846,12 @@ int reduced_round(const MmArgs& a, int K, int round, hipStream_t s, MmStats& st)
   a2.rowlist = a.blist;
   a2.nrows = a.bnrows;
   a2.rp = 1;
+  static const double d2 = [] {  // OB_MM_DELTA2: tuning knob (results do not depend on it)
+    const char* e = getenv("OB_MM_DELTA2");
+    const double v = e ? atof(e) : 0.0;
+    return v > 0.0 ? v : kDelta2;
+  }();
+  a2.dscale = d2;
   return ipm(a2, K, 3, s, st);
 }
 
@@ -1899,6 +1908,12 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, MmS
     a1.nrows = rd.nrows1;
     a1.tol = kPhase1Tol;
     a1.gchol = rd.gchol;
+    static const double d1 = [] {  // OB_MM_DELTA1: tuning knob (results do not depend on it)
+      const char* e = getenv("OB_MM_DELTA1");
+      const double v = e ? atof(e) : 0.0;
+      return v > 0.0 ? v : kDelta1;
+    }();
+    a1.dscale = d1;
     // phase 1 solves S1 of the S quantiles (their own fit arrays); the others interpolate
     static const int fstride = [] {  // OB_MM_FIT_STRIDE: tuning knob (results do not depend on it)
       const char* e = getenv("OB_MM_FIT_STRIDE");
