@@ -61,7 +61,8 @@ static_assert(kRc <= kCap && kRcF <= kCap && kRc1 / kSubStride <= kCap, "lists f
 constexpr double kPhase1Tol = 1e-6;  // phase-1 relative gap (beta_hat only centres the bands)
 constexpr int kFitStride = 16;       // phase 1 solves every 16th quantile (tau order) and the last ...
 constexpr int kFitStrideMin = 64;    // ... when a group has at least 64 simulations; the rest interpolate
-constexpr double kBandKappa = 4.0;   // band half-width in rank units: kappa sqrt(tau (1 - tau) K / m) + 0.01
+constexpr double kBandKappa = 3.5;   // band half-width in rank units: kappa sqrt(tau (1 - tau) K / m) + kBand0
+constexpr double kBand0 = 0.01;
                                      // (OB_MM_KAPPA overrides it: a tuning knob; results do not depend on it)
 constexpr int kBandSamples = 4096;   // residuals per fit behind its band quantiles
 constexpr double kDelta1 = 3.0;      // phase 1 starts with 3x the shifted start's z/w offset (48 -> 36
@@ -1099,7 +1100,7 @@ __global__ __launch_bounds__(256) void mm_lev_kernel(const MmArgs a, int K) {
 // [lo, hi] = the count-weighted tau -/+ delta quantiles of the sampled residuals at beta_hat, with
 // delta = kappa sqrt(tau (1 - tau) K / m) + 0.01 (m = the phase-1 sample's rows). A fit whose
 // phase 1 failed keeps every row (band = the real line); padding fits keep none.
-__global__ __launch_bounds__(256) void mm_band_kernel(const MmArgs a, int K, double kappa) {
+__global__ __launch_bounds__(256) void mm_band_kernel(const MmArgs a, int K, double kappa, double band0) {
   __shared__ double key[kBandSamples];
   __shared__ double wt[kBandSamples];
   __shared__ double beta[ob::kMmMaxK];
@@ -1129,7 +1130,7 @@ __global__ __launch_bounds__(256) void mm_band_kernel(const MmArgs a, int K, dou
     a.bhat[F * K + t] = beta[t];
   }
   const double tau = f[FS_TAU];
-  const double delta = kappa * sqrt(tau * (1.0 - tau) * K / fmax(f[FS_NACT], 1.0)) + 0.01;
+  const double delta = kappa * sqrt(tau * (1.0 - tau) * K / fmax(f[FS_NACT], 1.0)) + band0;
   if ((a.fstat[F] & kFailed) || (tau - delta <= 0.0 && tau + delta >= 1.0)) {
     if (t == 0) {
       f[FS_LO] = -INFINITY;
@@ -1951,7 +1952,11 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, MmS
       const double v = e ? atof(e) : 0.0;
       return v > 0.0 ? v : kBandKappa;
     }();
-    hipLaunchKernelGGL(mm_band_kernel, dim3((unsigned)n_fits), dim3(256), 0, s, a, K, kappa);
+    static const double band0 = [] {  // OB_MM_BAND0: the same kind of knob, the bands' constant term
+      const char* e = getenv("OB_MM_BAND0");
+      return e ? atof(e) : kBand0;
+    }();
+    hipLaunchKernelGGL(mm_band_kernel, dim3((unsigned)n_fits), dim3(256), 0, s, a, K, kappa, band0);
     MM_OK(hipGetLastError());
     MM_OK(hipMemsetAsync(a.xmask, 0, sizeof(uint32_t) * (size_t)a.n_rb * nch * (a.S_pad / 64) * (a.cap / 32), s));
     // round 0: the bands; round 1: flagged fits, their bands plus the wrong-signed rows; round 2:
