@@ -67,7 +67,8 @@ constexpr int kSix0 = OB_OZ_SIX0;      // six-slice blocks: slices of group 0 (g
 #ifndef OB_OZ_A_LDS
 // 1: A fragments by LDS-DMA beside B (oz_gram_la_kernel); 0: from L2 into registers (oz_gram_kernel,
 // the default). The LDS variant measured 14.42 ms per Gram launch against 13.62 ms at configs[1]
-// (profiles/r03_ab_gram.txt): the 120 KB ring allows one block per CU instead of two.
+// (profiles/r03_ab_gram.txt), and 12.87-12.94 against 12.41-12.45 ms in round 4 with uniform steps
+// and six slices (profiles/r04_ab_gram_alds.txt). OB_OZ_A_LDS=0/1 in the environment overrides it.
 #define OB_OZ_A_LDS 0
 #endif
 
@@ -491,6 +492,7 @@ constexpr size_t kLdsX = 4 * 64 * (size_t)kPairsPerTile * 8;  // slice-group exc
 constexpr size_t kLdsBytes = kLdsB > kLdsX ? kLdsB : kLdsX;
 static_assert(kBDma == 2 && kBDmaTotal == 14, "B DMA split below assumes 14 instructions over 8 waves");
 
+
 // One 16-byte-per-lane LDS-DMA (global_load_lds_dwordx4: lane l lands at lds + 16 l). Issued from
 // inline asm so the compiler does not track it: its wait model counts LDS-DMA against the LDS
 // counter and would then drain every fragment read (lgkmcnt(0)) before the next MFMAs. The
@@ -784,30 +786,27 @@ __device__ __forceinline__ void oz_gram_body_la(const OzArgs& a, unsigned char* 
     if constexpr (LIVE) {
       read_b(buf, 1, fb1);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!(DIAG & 2)) oz_mfmas<NQ>(acc, 0, ar[j], fb0);
+      if (!(DIAG & 2) && s < s1) oz_mfmas<NQ>(acc, 0, ar[j], fb0);
       __builtin_amdgcn_sched_barrier(0);
     }
-    const int nd = (s + 2 < s1 ? 1 : 0) + (s + 3 < s1 ? 1 : 0);
-    if (nd == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NP) : "memory");
-    else if (nd == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NP) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // uniform steps, as oz_gram_body: every step refills (past the end, the last sub-tile again into
+    // the stage just freed) and waits the same count
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NP) : "memory");
     oz_barrier();
-    if (s + kNbuf < s1) dma(buf, s + kNbuf);
+    dma(buf, min(s + kNbuf, s1 - 1));
     if constexpr (LIVE) {
       const int nb = (buf + 1) & (kNbuf - 1);
       read_b(nb, 0, fb0);
       read_a(nb, ar[j ^ 1]);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!(DIAG & 2)) oz_mfmas<NQ>(acc, 1, ar[j], fb1);
+      if (!(DIAG & 2) && s < s1) oz_mfmas<NQ>(acc, 1, ar[j], fb1);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
-  uint32_t s = s0;
-  for (; s + 2 <= s1; s += 2) {
+  for (uint32_t s = s0; s < s1; s += 2) {  // whole pairs of steps (a ghost step past the end)
     step(s, IC<0>{});
     step(s + 1, IC<1>{});
   }
-  if (s < s1) step(s, IC<0>{});
   // slices -> f64 (as oz_gram_body)
   int E[2];
 #pragma unroll
@@ -866,10 +865,19 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_la_kernel(const OzArgs
   const uint32_t nwg = gridDim.x, bid = blockIdx.x;
   const uint32_t xcd = bid & 7u, slot = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7u;
   const uint32_t wi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
-  const uint32_t rt = (wi / (uint32_t)a.n_ct) % a.n_rt;
+  const uint32_t tq = wi / (uint32_t)a.n_ct, rt = tq % a.n_rt, chunk = tq / a.n_rt;
   const bool live = rt * 4u + (uint32_t)(wave & 3) < a.nb_rep;
   // waves 0-3: slices 0-3; 4-7: slices 4-6; DMA pieces: 4 on waves 0-5, 3 on waves 6-7
-  if (wave < 4) {
+  const bool six = a.nsl[chunk * (uint32_t)a.n_ct + wi % (uint32_t)a.n_ct] == 6;
+  if (six && wave >= 4) {  // six slices: group 1 runs slices 4-5 (its DMA pieces are unchanged)
+    if (wave < 6) {
+      if (live) oz_gram_body_la<6 - kSlo, 4, true, DIAG>(a, smem, wave);
+      else oz_gram_body_la<6 - kSlo, 4, false, DIAG>(a, smem, wave);
+    } else {
+      if (live) oz_gram_body_la<6 - kSlo, 3, true, DIAG>(a, smem, wave);
+      else oz_gram_body_la<6 - kSlo, 3, false, DIAG>(a, smem, wave);
+    }
+  } else if (wave < 4) {
     if (live) oz_gram_body_la<kSlo, 4, true, DIAG>(a, smem, wave);
     else oz_gram_body_la<kSlo, 4, false, DIAG>(a, smem, wave);
   } else if (wave < 6) {
@@ -1140,7 +1148,11 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(kWaves * 64), kLdsBytes, s, a);
     return hipGetLastError();
   };
-  if (OB_OZ_A_LDS && (diag == 0 || diag == 2)) {
+  static const bool a_lds = [] {  // OB_OZ_A_LDS=0/1 at run time overrides the build default (A/B)
+    const char* e = getenv("OB_OZ_A_LDS");
+    return e ? atoi(e) != 0 : OB_OZ_A_LDS != 0;
+  }();
+  if (a_lds && (diag == 0 || diag == 2)) {
     auto launch_la = [&](auto kern) -> hipError_t {
       hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytesLA);
       if (e != hipSuccess) return e;
