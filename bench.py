@@ -382,7 +382,11 @@ def load_probit_pmc(rows, preds, reps, ks):
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_probit.json")) as f:
             j = json.load(f)
-        if (j.get("rows"), j.get("preds"), j.get("reps"), j.get("ks")) == (rows, preds, reps, ks):
+        # the counts belong to one build of the kernel: the normal pdf/cdf path must match
+        # (ob_heckman.hip: npdf_ncdf unless OB_HK_ERFC=0)
+        variant = "library_erfc" if os.environ.get("OB_HK_ERFC", "").strip() == "0" else "npdf_ncdf"
+        if ((j.get("rows"), j.get("preds"), j.get("reps"), j.get("ks")) == (rows, preds, reps, ks)
+                and j.get("erfc", "library_erfc") == variant):
             return j
     except (OSError, ValueError):
         pass

@@ -22,6 +22,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <type_traits>
 
 #include "ob_device.hpp"
 #include "ob_engine.hpp"
@@ -45,6 +47,71 @@ constexpr uint32_t kDone = 1u, kFailed = 2u;
 // (The constant divisions are multiplications by the reciprocals: a last-bit difference.)
 __device__ __forceinline__ double npdf(double z) { return exp(-0.5 * z * z) * 0.3989422804014327; }
 __device__ __forceinline__ double ncdf(double z) { return 0.5 * erfc(-z * 0.7071067811865476); }
+
+// pdf and cdf together from one exp(-z^2 / 2) (OB_HK_ERFC=1): erfc(x), x = -z / sqrt 2, by W. J.
+// Cody's rational Chebyshev approximations (Math. Comp. 23 (1969), the CALERF regions |x| < 0.46875,
+// <= 4, > 4), whose two outer regions are exp(-x^2) times a rational function -- exp(-x^2) is the
+// pdf's exp(-z^2 / 2). Checked against scipy's erfc on z in [-12, 12]: at most 3e-14 relative (the
+// rounding of z^2 inside the shared exp, amplified at large |z|; about 1e-15 where the clamped
+// probabilities are used).
+__device__ __forceinline__ void npdf_ncdf(double z, double& pdf, double& cdf) {
+  const double x = -z * 0.7071067811865476, y = fabs(x);
+  const double e = exp(-0.5 * z * z);
+  pdf = e * 0.3989422804014327;
+  double r;
+  if (y <= 0.46875) {
+    const double ysq = y * y;
+    double xn = 1.85777706184603153e-1 * ysq, xd = ysq;
+    xn = (xn + 3.16112374387056560e00) * ysq;
+    xd = (xd + 2.36012909523441209e01) * ysq;
+    xn = (xn + 1.13864154151050156e02) * ysq;
+    xd = (xd + 2.44024637934444173e02) * ysq;
+    xn = (xn + 3.77485237685302021e02) * ysq;
+    xd = (xd + 1.28261652607737228e03) * ysq;
+    cdf = 0.5 * (1.0 - x * (xn + 3.20937758913846947e03) / (xd + 2.84423683343917062e03));
+    return;
+  }
+  if (y <= 4.0) {
+    double xn = 2.15311535474403846e-8 * y, xd = y;
+    xn = (xn + 5.64188496988670089e-1) * y;
+    xd = (xd + 1.57449261107098347e01) * y;
+    xn = (xn + 8.88314979438837594e00) * y;
+    xd = (xd + 1.17693950891312499e02) * y;
+    xn = (xn + 6.61191906371416295e01) * y;
+    xd = (xd + 5.37181101862009858e02) * y;
+    xn = (xn + 2.98635138197400131e02) * y;
+    xd = (xd + 1.62138957456669019e03) * y;
+    xn = (xn + 8.81952221241769090e02) * y;
+    xd = (xd + 3.29079923573345963e03) * y;
+    xn = (xn + 1.71204761263407058e03) * y;
+    xd = (xd + 4.36261909014324716e03) * y;
+    xn = (xn + 2.05107837782607147e03) * y;
+    xd = (xd + 3.43936767414372164e03) * y;
+    r = (xn + 1.23033935479799725e03) / (xd + 1.23033935480374942e03) * e;
+  } else {
+    const double ysq = 1.0 / (y * y);
+    double xn = 1.63153871373020978e-2 * ysq, xd = ysq;
+    xn = (xn + 3.05326634961232344e-1) * ysq;
+    xd = (xd + 2.56852019228982242e00) * ysq;
+    xn = (xn + 3.60344899949804439e-1) * ysq;
+    xd = (xd + 1.87295284992346725e00) * ysq;
+    xn = (xn + 1.25781726111229246e-1) * ysq;
+    xd = (xd + 5.27905102951428412e-1) * ysq;
+    xn = (xn + 1.60837851487422766e-2) * ysq;
+    xd = (xd + 6.05183413124413191e-2) * ysq;
+    r = ysq * (xn + 6.58749161529837803e-4) / (xd + 2.33520497626869185e-3);
+    r = (5.6418958354775628695e-1 - r) / y * e;
+  }
+  cdf = 0.5 * (x >= 0.0 ? r : 2.0 - r);
+}
+
+// The probit and sums kernels take pdf and cdf from npdf_ncdf (one exp per row; probit launch 11.8
+// -> 9.0 ms at configs[1] + selection, profiles/r04_ab_heckman_erfc.txt) unless OB_HK_ERFC=0, which
+// keeps the library's erfc beside a second exp.
+inline bool hk_cody() {
+  static const bool v = !(getenv("OB_HK_ERFC") && atoi(getenv("OB_HK_ERFC")) == 0);
+  return v;
+}
 
 // 1/v within ~1 ulp: v_rcp_f64 and two Newton steps instead of the IEEE division sequence (the
 // operands are normal numbers: clamped probabilities).
@@ -122,7 +189,7 @@ __device__ __forceinline__ void wave_stage(double* stg, const double* src, int64
   __builtin_amdgcn_wave_barrier();
 }
 
-template <int KS>
+template <int KS, bool CODY>
 __global__ __launch_bounds__(kHB) void ob_probit_kernel(const ob_heck_seg a) {
   constexpr int NH = KS * (KS + 1) / 2, NP = NH + KS;
   __shared__ double red[64 * (NP + 1)];
@@ -161,8 +228,14 @@ __global__ __launch_bounds__(kHB) void ob_probit_kernel(const ob_heck_seg a) {
       double zg = 0.0;
 #pragma unroll
       for (int j = 0; j < KS; ++j) zg += z[j] * gam[j];
-      const double phi = npdf(zg);
-      const double bp = clamp_phi(ncdf(zg));
+      double phi, bp;
+      if constexpr (CODY) {
+        npdf_ncdf(zg, phi, bp);
+        bp = clamp_phi(bp);
+      } else {
+        phi = npdf(zg);
+        bp = clamp_phi(ncdf(zg));
+      }
       const double ib = hk_rcp(bp), iq = hk_rcp(1.0 - bp);
       const double lam = stg[ri] > 0.5 ? phi * ib : -phi * iq;  // probit.rs:66-70
       const double cwt = c * (phi * phi * ib * iq), cl = c * lam;  // sqrt_w^2 of probit.rs:75-76
@@ -340,7 +413,7 @@ __global__ __launch_bounds__(64) void ob_probit_step_kernel(const ob_heck_seg a)
 // Staged columns per row of the sums kernel: x_1..x_p, y, [s == 1], s, z_1..z_{ks-1}, (w).
 __host__ __device__ inline int heck_sums_cols(int p, int ks, int weighted) { return p + 2 + ks + (weighted ? 1 : 0); }
 
-template <int NB>
+template <int NB, bool CODY>
 __global__ __launch_bounds__(kHB) void ob_heck_sums_kernel(const ob_heck_seg a) {
   extern __shared__ __attribute__((aligned(16))) double hsm[];
   double* red = hsm;  // [64][NB + 1], then the waves' staged sub-tiles
@@ -386,8 +459,14 @@ __global__ __launch_bounds__(kHB) void ob_heck_sums_kernel(const ob_heck_seg a) 
       acc[3] += c * w * y;  // total gap (builder.rs:676-684, all rows)
       acc[4] += c * w;
       if (stg[cind * 64 + ri] == 1.0) {  // heckman.rs:56-69: lambda = phi / Phi, 0 when Phi < 1e-10
-        const double bp = ncdf(zg);
-        const double lam = bp < 1e-10 ? 0.0 : npdf(zg) * hk_rcp(bp);
+        double pd, bp;
+        if constexpr (CODY) {
+          npdf_ncdf(zg, pd, bp);
+        } else {
+          pd = npdf(zg);
+          bp = ncdf(zg);
+        }
+        const double lam = bp < 1e-10 ? 0.0 : pd * hk_rcp(bp);
         const double cl = c * lam;
         acc[0] += cl * y;
         acc[1] += cl * lam;
@@ -548,7 +627,10 @@ __global__ __launch_bounds__(64) void ob_heck_solve_kernel(const ob_heck_seg a) 
 template <int KS>
 hipError_t launch_probit_iter(const ob_heck_seg& a, hipStream_t s, hipEvent_t* ev) {
   if (ev) (void)hipEventRecord(ev[0], s);
-  hipLaunchKernelGGL(ob_probit_kernel<KS>, dim3(a.n_chunks, a.rep_pad / 64), dim3(kHB), 0, s, a);
+  if (hk_cody())
+    hipLaunchKernelGGL((ob_probit_kernel<KS, true>), dim3(a.n_chunks, a.rep_pad / 64), dim3(kHB), 0, s, a);
+  else
+    hipLaunchKernelGGL((ob_probit_kernel<KS, false>), dim3(a.n_chunks, a.rep_pad / 64), dim3(kHB), 0, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   if (ev) (void)hipEventRecord(ev[1], s);
@@ -609,16 +691,21 @@ int heckman_segment(const ob_heck_seg& a, hipStream_t s, int* iters, ob_heck_tim
   const int nb = nhs <= 32 ? 32 : (nhs <= 40 ? 40 : 64);
   const size_t lds_sums =
       sizeof(double) * (64 * (size_t)(nb + 1) + 4 * 64 * (size_t)heck_sums_cols(a.p, a.ks, a.weighted));
-  const void* fn = nb == 32 ? (const void*)ob_heck_sums_kernel<32>
-                            : (nb == 40 ? (const void*)ob_heck_sums_kernel<40> : (const void*)ob_heck_sums_kernel<64>);
+  const bool cody = hk_cody();
+  auto sums = [&](auto nbc, auto cc) {
+    constexpr int NB = decltype(nbc)::value;
+    constexpr bool C = decltype(cc)::value;
+    return (const void*)ob_heck_sums_kernel<NB, C>;
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+  const void* fn = nb == 32   ? (cody ? sums(std::integral_constant<int, 32>{}, T{}) : sums(std::integral_constant<int, 32>{}, F{}))
+                   : nb == 40 ? (cody ? sums(std::integral_constant<int, 40>{}, T{}) : sums(std::integral_constant<int, 40>{}, F{}))
+                              : (cody ? sums(std::integral_constant<int, 64>{}, T{}) : sums(std::integral_constant<int, 64>{}, F{}));
   HK_OK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_sums));
   if (tm) HK_OK(hipEventRecord(ev.e[2], s));
-  if (nb == 32)
-    hipLaunchKernelGGL(ob_heck_sums_kernel<32>, grid, dim3(kHB), lds_sums, s, a);
-  else if (nb == 40)
-    hipLaunchKernelGGL(ob_heck_sums_kernel<40>, grid, dim3(kHB), lds_sums, s, a);
-  else
-    hipLaunchKernelGGL(ob_heck_sums_kernel<64>, grid, dim3(kHB), lds_sums, s, a);
+  void* args[] = {const_cast<ob_heck_seg*>(&a)};
+  HK_OK(hipLaunchKernel(fn, grid, dim3(kHB), args, lds_sums, s));
   HK_OK(hipGetLastError());
   if (tm) HK_OK(hipEventRecord(ev.e[3], s));
   const size_t lds = heck_solve_lds(a);
