@@ -623,7 +623,7 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
     if constexpr (LIVE) {
       read(buf, 1, fb1);
       __builtin_amdgcn_sched_barrier(0);
-      if (!(DIAG & 2) && s < s1) oz_mfmas<NQ>(acc, 0, ar[j], fb0);
+      if constexpr (!(DIAG & 2)) oz_mfmas<NQ>(acc, 0, ar[j], fb0);
       __builtin_amdgcn_sched_barrier(0);
     }
     if constexpr (DIAG & 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -634,21 +634,25 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
     if constexpr (LIVE) {
       read((buf + 1) & (kNbuf - 1), 0, fb0);
       __builtin_amdgcn_sched_barrier(0);
-      if (!(DIAG & 2) && s < s1) oz_mfmas<NQ>(acc, 1, ar[j], fb1);
+      if constexpr (!(DIAG & 2)) oz_mfmas<NQ>(acc, 1, ar[j], fb1);
       __builtin_amdgcn_sched_barrier(0);
       // unconditional (past the end: a re-read of the last sub-tile, never used), so the compiler's
       // count of outstanding A loads is exact at every MFMA
       if constexpr (!(DIAG & 4)) aload(ar[j], min(s + 3, s1 - 1));
     }
   };
-  // whole groups of three steps: the last group's steps past s1 are ghosts that issue the same loads
-  // (clamped), waits and barriers but no MFMAs, so no path through the loop issues or waits
-  // differently from another (at most two ghost steps per block of ~490 at configs[1])
-  for (uint32_t s = s0; s < s1; s += 3) {
+  // groups of three steps, then the one or two left: every step, the tail's included, issues the
+  // same loads and waits, so each path through the loop presents the same queue at each barrier.
+  // (Ghost steps past the end with branch-guarded MFMAs, the round-4 first form, read 5 GB more
+  // per launch and ran 1.5 % slower: profiles/r04_ab_gram_tail.txt.)
+  uint32_t s = s0;
+  for (; s + 3 <= s1; s += 3) {
     step(s, IC<0>{});
     step(s + 1, IC<1>{});
     step(s + 2, IC<2>{});
   }
+  if (s < s1) step(s, IC<0>{});
+  if (s + 1 < s1) step(s + 1, IC<1>{});
   // slices -> f64: this wave's digits meet exactly in int64, one ldexp each; group 1 goes through
   // LDS to its group-0 partner, which adds (one rounding) and stores.
   int E[2];
