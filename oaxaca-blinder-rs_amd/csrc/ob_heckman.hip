@@ -54,6 +54,11 @@ __device__ __forceinline__ double ncdf(double z) { return 0.5 * erfc(-z * 0.7071
 // pdf's exp(-z^2 / 2). Checked against scipy's erfc on z in [-12, 12]: at most 3e-14 relative (the
 // rounding of z^2 inside the shared exp, amplified at large |z|; about 1e-15 where the clamped
 // probabilities are used).
+__device__ __forceinline__ double nd_rcp(double v) {  // 1/v within ~1 ulp (as hk_rcp below)
+  double r = __builtin_amdgcn_rcp(v);
+  r = fma(fma(-v, r, 1.0), r, r);
+  return fma(fma(-v, r, 1.0), r, r);
+}
 __device__ __forceinline__ void npdf_ncdf(double z, double& pdf, double& cdf) {
   const double x = -z * 0.7071067811865476, y = fabs(x);
   const double e = exp(-0.5 * z * z);
@@ -68,7 +73,7 @@ __device__ __forceinline__ void npdf_ncdf(double z, double& pdf, double& cdf) {
     xd = (xd + 2.44024637934444173e02) * ysq;
     xn = (xn + 3.77485237685302021e02) * ysq;
     xd = (xd + 1.28261652607737228e03) * ysq;
-    cdf = 0.5 * (1.0 - x * (xn + 3.20937758913846947e03) / (xd + 2.84423683343917062e03));
+    cdf = 0.5 * (1.0 - x * (xn + 3.20937758913846947e03) * nd_rcp(xd + 2.84423683343917062e03));
     return;
   }
   if (y <= 4.0) {
@@ -87,9 +92,9 @@ __device__ __forceinline__ void npdf_ncdf(double z, double& pdf, double& cdf) {
     xd = (xd + 4.36261909014324716e03) * y;
     xn = (xn + 2.05107837782607147e03) * y;
     xd = (xd + 3.43936767414372164e03) * y;
-    r = (xn + 1.23033935479799725e03) / (xd + 1.23033935480374942e03) * e;
+    r = (xn + 1.23033935479799725e03) * nd_rcp(xd + 1.23033935480374942e03) * e;
   } else {
-    const double ysq = 1.0 / (y * y);
+    const double iy = nd_rcp(y), ysq = iy * iy;
     double xn = 1.63153871373020978e-2 * ysq, xd = ysq;
     xn = (xn + 3.05326634961232344e-1) * ysq;
     xd = (xd + 2.56852019228982242e00) * ysq;
@@ -99,8 +104,8 @@ __device__ __forceinline__ void npdf_ncdf(double z, double& pdf, double& cdf) {
     xd = (xd + 5.27905102951428412e-1) * ysq;
     xn = (xn + 1.60837851487422766e-2) * ysq;
     xd = (xd + 6.05183413124413191e-2) * ysq;
-    r = ysq * (xn + 6.58749161529837803e-4) / (xd + 2.33520497626869185e-3);
-    r = (5.6418958354775628695e-1 - r) / y * e;
+    r = ysq * (xn + 6.58749161529837803e-4) * nd_rcp(xd + 2.33520497626869185e-3);
+    r = (5.6418958354775628695e-1 - r) * iy * e;
   }
   cdf = 0.5 * (x >= 0.0 ? r : 2.0 - r);
 }
