@@ -241,9 +241,11 @@ __global__ __launch_bounds__(kHB) void ob_probit_kernel(const ob_heck_seg a) {
         phi = npdf(zg);
         bp = clamp_phi(ncdf(zg));
       }
-      const double ib = hk_rcp(bp), iq = hk_rcp(1.0 - bp);
-      const double lam = stg[ri] > 0.5 ? phi * ib : -phi * iq;  // probit.rs:66-70
-      const double cwt = c * (phi * phi * ib * iq), cl = c * lam;  // sqrt_w^2 of probit.rs:75-76
+      // one reciprocal: r = 1 / (Phi (1 - Phi)), so 1 / Phi = (1 - Phi) r, 1 / (1 - Phi) = Phi r and
+      // the weight phi^2 / (Phi (1 - Phi)) = phi^2 r
+      const double qb = 1.0 - bp, r = hk_rcp(bp * qb);
+      const double lam = stg[ri] > 0.5 ? phi * (qb * r) : -phi * (bp * r);  // probit.rs:66-70
+      const double cwt = c * (phi * phi * r), cl = c * lam;  // sqrt_w^2 of probit.rs:75-76
       int e = 0;
 #pragma unroll
       for (int j = 0; j < KS; ++j) {
