@@ -3,11 +3,12 @@
 
 Workload = BASELINE.json configs[1]: a 1,000,000-row two-group panel (500k/500k) with 20 numeric
 predictors, two-fold WLS decomposition (builder default reference coefficients GroupA), 10,000
-bootstrap replicates per GPU per step. One step = one full bootstrap run with the panel already
+bootstrap replicates per step. One step = one full bootstrap run with the panel already
 resident in HBM: OBRS-2 resampling + Gram + solves + OB terms for every replicate (HIP), the
 RCCL all-gather of the per-replicate component columns over xGMI (N > 1), and the SE/p/CI aggregation of
-every reported component on rank 0 (builder.rs:841-930). Replicates are sharded across ranks
-(weak scaling: each rank runs its own 10,000 replicate ids per step).
+every reported component on rank 0 (builder.rs:841-930). On N > 1 GPUs the default is configs[2]:
+the 10,000 replicates of a step are sharded over the ranks (strong scaling); --weak gives each rank
+its own 10,000 replicate ids per step.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -383,8 +384,11 @@ def load_probit_pmc(rows, preds, reps, ks):
         with open(os.path.join(ROOT, "profiles", "pmc_probit.json")) as f:
             j = json.load(f)
         # the counts belong to one build of the kernel: the normal pdf/cdf path must match
-        # (ob_heckman.hip: npdf_ncdf unless OB_HK_ERFC=0)
-        variant = "library_erfc" if os.environ.get("OB_HK_ERFC", "").strip() == "0" else "npdf_ncdf"
+        # (ob_heckman.hip: npdf_ncdf unless option hk_erfc = 0, which only a tuning build reads
+        # from OB_HK_ERFC)
+        ob = importlib.import_module("oaxaca-blinder-rs_amd")
+        tuning = ob._native.lib().ob_tuning_build() == 1
+        variant = "library_erfc" if tuning and os.environ.get("OB_HK_ERFC", "").strip() == "0" else "npdf_ncdf"
         if ((j.get("rows"), j.get("preds"), j.get("reps"), j.get("ks")) == (rows, preds, reps, ks)
                 and j.get("erfc", "library_erfc") == variant):
             return j
@@ -444,13 +448,32 @@ def end_to_end(ob, ctx, d, ya, yb, n, ref, stat_cols, dev):
                     "replicates + host aggregation, host clock"}
 
 
-def workload_label(strong, taus, total, world, per_rank):
-    """config.workload of the default bench line. A non-strong run at a replicate count other than
-    configs[1]'s 10,000 per GPU is named for what it is: 1,250 is configs[2]'s per-GPU share at 8 GPUs."""
+def replicate_plan(reps, world, strong=False, weak=False):
+    """(scaling, replicates per step in total, replicates per GPU per step). One GPU: configs[1],
+    reps per step. Several GPUs: configs[2] by default -- reps per step in total, sharded over the
+    ranks (strong scaling: the reference runs a fixed replicate count as independent Rayon tasks,
+    builder.rs:816-839); --weak gives every rank its own reps per step instead."""
+    if weak and strong:
+        raise SystemExit("bench.py: --weak and --strong exclude each other")
+    if world > 1 and not weak:
+        strong = True
+    total = reps if strong else reps * world
+    return ("strong" if strong else "weak"), total, -(-total // world)
+
+
+def workload_label(mode, taus, total, world, per_rank):
+    """config.workload of the default bench line, named for what it runs: configs[1] is one GPU at
+    10,000 replicates per step; configs[2] is 10,000 per step in total sharded over the GPUs; a weak
+    run on several GPUs is configs[1]'s panel at a per-GPU replicate count, never configs[1]; a
+    one-GPU run at 1,250 is configs[2]'s per-GPU share at 8 GPUs."""
     if taus:
         return f"configs[3]: RIF decomposition at tau={taus}, two-fold WLS, GroupA"
-    if strong:
-        return f"configs[2]: {total} replicates per step in total, sharded over {world} GPU(s)"
+    if mode == "strong" and world > 1:
+        if total == 10000:
+            return f"configs[2]: 10,000 replicates per step in total, sharded over {world} GPUs (strong)"
+        return f"configs[1]'s panel, {total:,} replicates per step in total, sharded over {world} GPUs (strong)"
+    if world > 1:
+        return f"configs[1]'s panel, {per_rank:,} replicates per GPU, weak ({world} GPUs)"
     if per_rank == 10000:
         return "configs[1]: two-fold WLS bootstrap, GroupA reference coefficients"
     if 10000 % per_rank == 0 and 10000 // per_rank > 1:
@@ -510,15 +533,18 @@ def launch_ranks(argv, n):
     return proc.wait()
 
 
-def main():
+def parse_args(argv):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--reps", type=int, default=10000,
-                    help="replicates per GPU per step (weak scaling), or per step in total with --strong")
+                    help="replicates per step: in total, sharded over the GPUs (configs[2], the default for "
+                         "N > 1), or per GPU with --weak")
     ap.add_argument("--strong", action="store_true",
-                    help="configs[2]: --reps replicates per step in total, sharded over the GPUs (strong scaling)")
+                    help="--reps replicates per step in total, sharded over the GPUs (already the default)")
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling: every GPU runs its own --reps replicates per step")
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--preds", type=int, default=20)
     ap.add_argument("--ref", type=int, default=0, help="ReferenceCoefficients (0 = GroupA)")
@@ -537,18 +563,23 @@ def main():
     ap.add_argument("--heckman", action="store_true",
                     help="Heckman two-step bootstrap on configs[1]'s panel plus a selection equation "
                          "(2000 replicates per GPU per step); reports Heckman replicates/s")
-    args = ap.parse_args()
-    taus = [float(t) for t in args.taus.split(",") if t.strip()]
-    if args.heckman and "--reps" not in set(a.split("=")[0] for a in sys.argv[1:]):
+    args = ap.parse_args(argv)
+    explicit = set(x.split("=")[0] for x in argv)
+    if args.heckman and "--reps" not in explicit:
         args.reps = 2000
     if args.mm:
-        explicit = set(a.split("=")[0] for a in sys.argv[1:])
         if "--rows" not in explicit:
             args.rows = 500_000
         if "--preds" not in explicit:
             args.preds = 15
         if "--reps" not in explicit:
             args.reps = 12
+    return args
+
+
+def main():
+    args = parse_args(sys.argv[1:])
+    taus = [float(t) for t in args.taus.split(",") if t.strip()]
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(sys.argv[1:], args.gpus))
@@ -594,9 +625,8 @@ def main():
     if (rccl_rank, rccl_world) != (rank, world):
         raise RuntimeError(f"engine RCCL communicator is rank {rccl_rank} of {rccl_world}, expected {rank} of {world}")
     panel = ob.Panel(d["xa"], ya, d["xb"], yb, d["wa"], d["wb"], ctx=ctx)
-    # weak: every rank runs --reps replicates per step; strong (configs[2]): --reps in total
-    total = args.reps if args.strong else args.reps * world
-    per_rank = -(-total // world)
+    # strong (configs[2], the default at N > 1): --reps per step in total; --weak: --reps per rank
+    mode, total, per_rank = replicate_plan(args.reps, world, args.strong, args.weak)
     rl, ny = panel.row_len, panel.n_y
     dev = torch.device("cuda", local)
     kd = panel.k + panel.n_base
@@ -711,7 +741,6 @@ def main():
                     "frac": achieved / F64_MFMA_PEAK_TFLOPS, "traffic": traffic,
                     "kernel": "ob_gram_kernel", "avg_launch_ms": gram_launch_ms,
                     "flops_per_replicate": flops_rep}
-        mode = "strong" if args.strong else "weak"
         out = {
             "metric": "bootstrap replicates/sec on 1M-row×20-pred panel at 1/2/4/8 MI355X" if not taus else
                       "RIF bootstrap replicate-quantiles/sec (configs[3], quantiles share each resample)",
@@ -727,7 +756,7 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (SURVEY.md §8d wage panel, numpy seed 20260424; OBRS-2 bootstrap seed 0x0B5EED)",
-            "config": {"workload": workload_label(args.strong, taus, total, world, per_rank),
+            "config": {"workload": workload_label(mode, taus, total, world, per_rank),
                        "rows": args.rows, "predictors": args.preds, "weighted": weighted,
                        "replicates_per_step": total, "replicates_per_gpu_per_step": per_rank,
                        "parallelism": f"replicates sharded x{world}, engine RCCL all-gather (ob_boot_run_sharded_device)"},

@@ -252,6 +252,20 @@ int ob_debug_chunks(const ob_panel* panel, uint32_t* table, int32_t cap, int32_t
    where it converged. For checks of LP optimality (objective, residual signs) on degenerate data. */
 int ob_debug_mm_betas(ob_panel* panel, uint64_t seed, int32_t simulations, uint64_t rep, double* betas,
                       uint8_t* done);
+/* Process-wide engine options (no reference counterpart: test and A/B switches). The library reads
+   no environment variable; a caller sets these explicitly. value NaN restores the default.
+     "gram_path"   1: f64 MFMA Gram, 2: i8 Gram (OB_E_UNSUPPORTED if its images do not fit)
+     "gram_digits" 7: seven digit slices on every i8 column tile
+     "hk_erfc"     0: library erfc in the Heckman probit/IMR kernels (default: npdf_ncdf)
+     "mm_reduce"   0: no Machado-Mata row reduction, 1: always (default: both groups >= 2^16 rows)
+     "mm_trace"    nonzero: Machado-Mata per-iteration trace on stderr
+     "mm_state_gb", "mm_delta1", "mm_delta2", "mm_tol1", "mm_fit_stride", "mm_kappa", "mm_band0":
+                   Machado-Mata tuning (the verification keeps results exact)
+     "gram_diag", "l1_diag": timing ablations, tuning builds only (OB_E_UNSUPPORTED otherwise)
+   Unknown names are OB_E_INVALID. ob_tuning_build() is 1 in a -DOB_TUNING=1 build (`make tuning`),
+   which also reads OB_<NAME> from the environment for options nobody set. */
+int ob_set_option(const char* name, double value);
+int ob_tuning_build(void);
 
 /* ---- inference (host) --------------------------------------------------------------------- */
 /* inference.rs:4-34: out = {std_err, p_value, ci_lower, ci_upper}; n = 0 gives NaNs. */

@@ -6,6 +6,7 @@ called, the call raises -- the bootstrap never silently runs on the CPU.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
 import threading
@@ -41,7 +42,7 @@ EXPORTED = (
     "ob_get_unique_id", "ob_ctx_create_rank", "ob_ctx_rank", "ob_boot_run_sharded", "ob_boot_run_sharded_device",
     "ob_boot_run_multi", "ob_debug_counts", "ob_prepared_boot_sharded", "ob_debug_gram",
     "ob_debug_gram_exceptions", "ob_panel_set_gather_columns", "ob_debug_shard_sim", "ob_debug_mm_fail",
-    "ob_debug_chunks", "ob_debug_mm_betas",
+    "ob_debug_chunks", "ob_debug_mm_betas", "ob_set_option", "ob_tuning_build",
 )
 
 
@@ -198,6 +199,8 @@ _SIGS = {
     "ob_debug_counts": (C.c_int, [_P, C.c_uint64, C.c_uint64, C.c_uint32, C.c_int, C.POINTER(C.c_uint32), _U8]),
     "ob_debug_chunks": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_int32, C.POINTER(C.c_int32)]),
     "ob_debug_mm_betas": (C.c_int, [_P, C.c_uint64, C.c_int32, C.c_uint64, _D, _U8]),
+    "ob_set_option": (C.c_int, [C.c_char_p, C.c_double]),
+    "ob_tuning_build": (C.c_int, []),
 }
 
 _lib = None
@@ -300,6 +303,22 @@ def ctx_rank(ctx) -> tuple:
     r, w = C.c_int(0), C.c_int(0)
     check(lib().ob_ctx_rank(ctx, C.byref(r), C.byref(w)))
     return r.value, w.value
+
+
+def set_option(name: str, value) -> None:
+    """ob_set_option: a process-wide engine switch (include/oaxaca_boot.h); None restores the default.
+    The library reads no environment variable -- tests and tools set these explicitly."""
+    check(lib().ob_set_option(name.encode(), float("nan") if value is None else float(value)))
+
+
+@contextlib.contextmanager
+def option(name: str, value):
+    """set_option for the duration of a with-block, then back to the default."""
+    set_option(name, value)
+    try:
+        yield
+    finally:
+        set_option(name, None)
 
 
 def device_count() -> int:

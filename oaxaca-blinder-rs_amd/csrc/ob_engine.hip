@@ -30,6 +30,7 @@
 #include "ob_device.hpp"
 #include "ob_engine.hpp"
 #include "ob_heckman.hpp"
+#include "ob_options.hpp"
 #include "ob_spec.h"
 
 typedef double ob_d4 __attribute__((ext_vector_type(4)));
@@ -1305,13 +1306,8 @@ struct Plan {
   int n_chunks() const { return (int)(chunks.size() / 3); }
 };
 
-int diag_mode() {
-  static int m = [] {
-    const char* e = getenv("OB_GRAM_DIAG");
-    return e ? atoi(e) : 0;
-  }();
-  return m;
-}
+// Timing ablations (gram_diag, tools/gram_ablate.py): tuning builds only, 0 otherwise (ob_options.hpp).
+int diag_mode() { return ob::opt_int(ob::Opt::GramDiag, 0); }
 
 // Two staged sub-tiles (the next one's DMA under this one's MFMAs) while they fit in the 160 KB of
 // LDS (k1 <= 101); wider panels (p up to 120) stage one at a time.
@@ -1734,12 +1730,10 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     return ob::fail(OB_E_INVALID, "internal: the chunk table changed with the replicate count");
   if (p->heckman) OB_TRY(ensure_heck(p, pl));
   // Gram path: the exact integer-sliced i8 GEMM (ob_gram_i8.hip) unless forced to f64 MFMA
-  // (OB_GRAM_PATH=f64) or the digit images do not fit. Heckman's kernels read either image layout.
+  // (option gram_path = 1, ob_set_option) or the digit images do not fit. Heckman's kernels read
+  // either image layout.
   int force = p->gram_force;
-  if (!force) {
-    const char* ev = getenv("OB_GRAM_PATH");
-    force = ev && !strcmp(ev, "f64") ? 1 : (ev && !strcmp(ev, "i8") ? 2 : 0);
-  }
+  if (!force) force = ob::opt_int(ob::Opt::GramPath, 0);
   bool use_i8 = force != 1;
   std::memset(&p->timing, 0, sizeof(p->timing));
   if (use_i8) {
@@ -1752,12 +1746,10 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   const size_t lds_l1 = sizeof(uint32_t) * std::max(l1_lds_words(p->ntiles[0]), l1_lds_words(p->ntiles[1]));
   ob_ky_tables ky{};
   OB_TRY(ky_device(ctx->device, &ky));
-  static const int l1_diag = [] {
-    const char* e = getenv("OB_L1_DIAG");
-    return e ? atoi(e) & 31 : 0;
-  }();
   using L1Kernel = void (*)(uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t*,
                             const ob_ky_tables);
+#if OB_TUNING  // timing ablations of level 1 (l1_diag, tools/l1_ablate.sh)
+  const int l1_diag = ob::opt_int(ob::Opt::L1Diag, 0) & 31;
   const L1Kernel l1k = l1_diag == 0    ? ob_level1_kernel<0>
                        : l1_diag == 1  ? ob_level1_kernel<1>
                        : l1_diag == 3  ? ob_level1_kernel<3>
@@ -1765,6 +1757,9 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
                        : l1_diag == 16 ? ob_level1_kernel<16>
                        : l1_diag == 20 ? ob_level1_kernel<20>
                                        : ob_level1_kernel<0>;
+#else
+  const L1Kernel l1k = ob_level1_kernel<0>;
+#endif
   HIP_OK(hipFuncSetAttribute((const void*)l1k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_l1));
   HIP_OK(hipFuncSetAttribute((const void*)ob_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                              (int)solve_lds_bytes(p)));
@@ -1893,7 +1888,7 @@ int engine_collect(ob_panel* p) {
     return ob::fail(OB_E_OVERFLOW, "a resampled row was drawn more than 255 times in one replicate");
   if (flag & 3u)  // p ~ 1e-215 per row and replicate; the f64 Gram path takes counts up to 255
     return ob::fail(OB_E_OVERFLOW, "a resampled row was drawn more than 127 times in one replicate "
-                                   "(the i8 Gram's range; OB_GRAM_PATH=f64 runs the f64 MFMA Gram)");
+                                   "(the i8 Gram's range; option gram_path = 1 runs the f64 MFMA Gram)");
   return OB_OK;
 }
 

@@ -41,6 +41,7 @@
 
 #include "ob_common.hpp"
 #include "ob_engine.hpp"
+#include "ob_options.hpp"
 #include "ob_spec.h"
 
 typedef int ob_v4i __attribute__((ext_vector_type(4)));
@@ -62,14 +63,6 @@ constexpr int kSix0 = OB_OZ_SIX0;      // six-slice blocks: slices of group 0 (g
 // which run together on one XCD, share them through its L2. Nontemporal loads (OB_OZ_A_NT=1,
 // tools/build_alt.sh) measured 14.6 ms per Gram launch against 13.4 ms at configs[1].
 #define OB_OZ_A_NT 0
-#endif
-
-#ifndef OB_OZ_A_LDS
-// 1: A fragments by LDS-DMA beside B (oz_gram_la_kernel); 0: from L2 into registers (oz_gram_kernel,
-// the default). The LDS variant measured 14.42 ms per Gram launch against 13.62 ms at configs[1]
-// (profiles/r03_ab_gram.txt), and 12.87-12.94 against 12.41-12.45 ms in round 4 with uniform steps
-// and six slices (profiles/r04_ab_gram_alds.txt). OB_OZ_A_LDS=0/1 in the environment overrides it.
-#define OB_OZ_A_LDS 0
 #endif
 
 #define OZ_HIP(expr)                                                                                  \
@@ -506,6 +499,41 @@ __device__ __forceinline__ void oz_dma16(const void* src, uint32_t lds) {
 
 __device__ __forceinline__ void oz_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+#ifndef OB_OZ_RASTER
+#define OB_OZ_RASTER 1
+#endif
+// Block -> (column tile, replicate tile, chunk). A "group" is the n_ct column tiles of one
+// (chunk, replicate tile); its blocks share that tile's count images, so they run on one XCD
+// (blocks b and b + 8 share an XCD under round-robin dispatch: speed only, never correctness).
+// OB_OZ_RASTER 1: groups are dealt to the 8 XCDs in turn (8 consecutive groups = one "super group"
+// of 8 n_ct blocks, group = bid mod 8 inside it), so all XCDs sweep the chunks together and the
+// chunk's digit block (47 MB at configs[1]) is re-read from the Infinity Cache by every replicate
+// tile. 0: each XCD sweeps a contiguous eighth of the groups (8 chunks in flight at once).
+__device__ __forceinline__ void oz_map(const OzArgs& a, uint32_t* ct, uint32_t* rt, uint32_t* chunk) {
+  const uint32_t nwg = gridDim.x, bid = blockIdx.x, nct = (uint32_t)a.n_ct;
+  uint32_t grp, c;
+#if OB_OZ_RASTER
+  const uint32_t sgb = 8u * nct, sg = bid / sgb, r = bid - sg * sgb;
+  const uint32_t left = nwg - sg * sgb;  // blocks from this super group on
+  if (left >= sgb) {
+    grp = sg * 8u + (r & 7u);
+    c = r >> 3;
+  } else {  // the last, partial super group: left / n_ct groups
+    const uint32_t ng = left / nct;
+    grp = sg * 8u + r % ng;
+    c = r / ng;
+  }
+#else
+  const uint32_t xcd = bid & 7u, slot = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7u;
+  const uint32_t wi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  grp = wi / nct;
+  c = wi - grp * nct;
+#endif
+  *ct = c;
+  *rt = grp % a.n_rt;
+  *chunk = grp / a.n_rt;
+}
+
 template <int N>
 struct IC {
   static constexpr int value = N;
@@ -544,12 +572,9 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   constexpr int slo = SLO;                    // this wave's first slice
   // XCD-aware remap (as ob_gram_kernel's map_work): consecutive work items -- the column tiles of
   // one replicate tile, then the replicate tiles of one chunk -- share an XCD's L2.
-  const uint32_t nwg = gridDim.x, bid = blockIdx.x;
-  const uint32_t xcd = bid & 7u, slot = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7u;
-  const uint32_t wi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
-  const int ct = (int)(wi % (uint32_t)a.n_ct);
-  const uint32_t tq = wi / (uint32_t)a.n_ct;
-  const uint32_t rt = tq % a.n_rt, chunk = tq / a.n_rt;
+  uint32_t ctu, rt, chunk;
+  oz_map(a, &ctu, &rt, &chunk);
+  const int ct = (int)ctu;
   const uint32_t g = a.chunks[3 * chunk];
   const uint32_t n = g ? a.n1 : a.n0, tg0 = g ? a.tiles0 : 0u;
   const uint32_t s0 = a.chunks[3 * chunk + 1] * 4u;
@@ -705,205 +730,15 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   }
 }
 
-// ---- A through LDS (OB_OZ_A_LDS=1, measured slower) ----------------------------------------------
-// Every operand arrives by LDS-DMA: per 64-row sub-tile a ring stage holds the 14 KB B image and
-// the block's 16 KB of A fragments (4 replicate batches x 4 x 1 KB), 30 one-KB pieces spread over
-// the 8 waves. The two waves of a batch (slice groups 0 and 1) read one copy of its A from LDS
-// instead of each loading it from L2, and no vector-memory load is tracked by the compiler, so the
-// hand-counted wait before each barrier covers exactly the stage it publishes (the tracked A
-// loads of the register path also waited for the DMA issued after them, a sub-tile early).
-constexpr int kAUnits = 4 * 4 * 64;                      // A fragments of a stage (16 KB)
-constexpr int kStageUnits = kSubUnits + kAUnits;          // 30 KB
-constexpr int kPieces = kStageUnits / 64;                 // 30 one-KB DMA pieces per stage
-constexpr size_t kLdsLA = kNbuf * (size_t)kStageUnits * 16;  // 120 KB
-constexpr size_t kLdsBytesLA = kLdsLA > kLdsX ? kLdsLA : kLdsX;
-static_assert(kPieces == 30, "piece split below: 4 per wave on waves 0-5, 3 on waves 6-7");
-
-template <int NQ, int NP, bool LIVE, int DIAG>
-__device__ __forceinline__ void oz_gram_body_la(const OzArgs& a, unsigned char* smem, int wave) {
-  const ob_v4i* st = reinterpret_cast<const ob_v4i*>(smem);  // [kNbuf][kStageUnits]
-  const int lane = threadIdx.x & 63;
-  const int wb = wave & 3, grp = wave >> 2;
-  const int slo = grp ? kSlo : 0;
-  const uint32_t nwg = gridDim.x, bid = blockIdx.x;
-  const uint32_t xcd = bid & 7u, slot = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7u;
-  const uint32_t wi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
-  const int ct = (int)(wi % (uint32_t)a.n_ct);
-  const uint32_t tq = wi / (uint32_t)a.n_ct;
-  const uint32_t rt = tq % a.n_rt, chunk = tq / a.n_rt;
-  const uint32_t g = a.chunks[3 * chunk];
-  const uint32_t n = g ? a.n1 : a.n0, tg0 = g ? a.tiles0 : 0u;
-  const uint32_t s0 = a.chunks[3 * chunk + 1] * 4u;
-  const uint32_t s1 = min(a.chunks[3 * chunk + 2] * 4u, (n + 63u) >> 6);
-  const ob_v4i* Bg = g ? a.B1 : a.B0;
-  const uint32_t batch = rt * 4u + (uint32_t)wb;
-  // this wave's pieces p = 8 t + wave of stage buf <- sub-tile s: B pieces 0..13, then A piece
-  // p - 14 = (batch in tile) * 4 + m (a batch past the last loads the last one's, never read)
-  auto dma = [&](int buf, uint32_t s) {
-#pragma unroll
-    for (int t = 0; t < NP; ++t) {
-      const int p = t * kWaves + wave;
-      const ob_v4i* src;
-      if (p < kBDmaTotal) {
-        src = Bg + ((size_t)s * a.n_ct + ct) * kSubUnits + p * 64;
-      } else {
-        const int ap = p - kBDmaTotal;
-        const uint32_t bb = min(rt * 4u + (uint32_t)(ap >> 2), a.nb_rep - 1u);
-        src = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + bb) * 4 + (s & 3)) * 256 + (ap & 3) * 64;
-      }
-      oz_dma16(src + lane, (uint32_t)(buf * kStageUnits + p * 64) * 16u);
-    }
-  };
-  auto read_b = [&](int buf, int h, ob_v4i (&bf)[kSlo]) {
-    const ob_v4i* bb = st + buf * kStageUnits + (slo * 2 + h) * 64 + lane;
-#pragma unroll
-    for (int q = 0; q < NQ; ++q) bf[q] = bb[q * 128];
-  };
-  auto read_a = [&](int buf, ob_v4i (&af)[4]) {
-    const ob_v4i* ab = st + buf * kStageUnits + kSubUnits + wb * 256 + lane;
-#pragma unroll
-    for (int m = 0; m < 4; ++m) af[m] = ab[m * 64];
-  };
-
-  ob_v4i acc[4][kSlo][2];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int q = 0; q < kSlo; ++q) acc[m][q][0] = acc[m][q][1] = (ob_v4i){};
-#pragma unroll
-  for (int j = 0; j < kNbuf; ++j)
-    if (s0 + j < s1) dma(j, s0 + j);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  ob_v4i fb0[kSlo], fb1[kSlo], ar[2][4];
-  if constexpr (LIVE) {
-    read_b(0, 0, fb0);
-    read_a(0, ar[0]);
-  }
-  // Step s: read B (s, 1); MFMAs (s, 0). Barrier B_s publishes stage s + 1: its DMA was issued
-  // after B_(s-3), and after it at most the DMA rounds of B_(s-2), B_(s-1) (while s + 2, s + 3 <
-  // s1), NP pieces each. Then refill stage s with s + 4, read B (s + 1, 0) and A (s + 1), MFMAs
-  // (s, 1).
-  auto step = [&](uint32_t s, auto J) {
-    constexpr int j = decltype(J)::value;
-    const int buf = (int)((s - s0) & (kNbuf - 1));
-    if constexpr (LIVE) {
-      read_b(buf, 1, fb1);
-      __builtin_amdgcn_sched_barrier(0);
-      if (!(DIAG & 2) && s < s1) oz_mfmas<NQ>(acc, 0, ar[j], fb0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // uniform steps, as oz_gram_body: every step refills (past the end, the last sub-tile again into
-    // the stage just freed) and waits the same count
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NP) : "memory");
-    oz_barrier();
-    dma(buf, min(s + kNbuf, s1 - 1));
-    if constexpr (LIVE) {
-      const int nb = (buf + 1) & (kNbuf - 1);
-      read_b(nb, 0, fb0);
-      read_a(nb, ar[j ^ 1]);
-      __builtin_amdgcn_sched_barrier(0);
-      if (!(DIAG & 2) && s < s1) oz_mfmas<NQ>(acc, 1, ar[j], fb1);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  for (uint32_t s = s0; s < s1; s += 2) {  // whole pairs of steps (a ghost step past the end)
-    step(s, IC<0>{});
-    step(s + 1, IC<1>{});
-  }
-  // slices -> f64 (as oz_gram_body)
-  int E[2];
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int pair = ct * kPairsPerTile + 16 * h + (lane & 15);
-    E[h] = a.pexp[chunk * a.n_pairs_pad + min(pair, a.n_pairs_pad - 1)];
-  }
-  double v[4][2][4];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int shift = E[h] - kFracBits + 8 * (kS - slo - NQ);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        long long part = 0;
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) part = part * 256 + acc[m][q][h][i];
-        v[m][h][i] = ldexp((double)part, shift);
-      }
-    }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();  // every wave is done with the ring: the exchange overlays it
-  double* xch = reinterpret_cast<double*>(smem);
-  if (grp) {
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          xch[(wb * 64 + 16 * m + 4 * (lane >> 4) + i) * kPairsPerTile + 16 * h + (lane & 15)] = v[m][h][i];
-  }
-  __syncthreads();
-  if (grp || !LIVE) return;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int pair = ct * kPairsPerTile + 16 * h + (lane & 15);
-    if (pair >= a.e_pad) continue;
-#pragma unroll
-    for (int m = 0; m < 4; ++m)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int rl = 16 * m + 4 * (lane >> 4) + i;
-        const uint32_t rep = batch * 64u + (uint32_t)rl;
-        const double val = v[m][h][i] + xch[(wb * 64 + rl) * kPairsPerTile + 16 * h + (lane & 15)];
-        if (rep < a.n_reps) a.partial[((size_t)chunk * a.rep_pad + rep) * a.e_pad + pair] = val;
-      }
-  }
-}
-
-template <int DIAG>
-__global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_la_kernel(const OzArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t nwg = gridDim.x, bid = blockIdx.x;
-  const uint32_t xcd = bid & 7u, slot = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7u;
-  const uint32_t wi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
-  const uint32_t tq = wi / (uint32_t)a.n_ct, rt = tq % a.n_rt, chunk = tq / a.n_rt;
-  const bool live = rt * 4u + (uint32_t)(wave & 3) < a.nb_rep;
-  // waves 0-3: slices 0-3; 4-7: slices 4-6; DMA pieces: 4 on waves 0-5, 3 on waves 6-7
-  const bool six = a.nsl[chunk * (uint32_t)a.n_ct + wi % (uint32_t)a.n_ct] == 6;
-  if (six && wave >= 4) {  // six slices: group 1 runs slices 4-5 (its DMA pieces are unchanged)
-    if (wave < 6) {
-      if (live) oz_gram_body_la<6 - kSlo, 4, true, DIAG>(a, smem, wave);
-      else oz_gram_body_la<6 - kSlo, 4, false, DIAG>(a, smem, wave);
-    } else {
-      if (live) oz_gram_body_la<6 - kSlo, 3, true, DIAG>(a, smem, wave);
-      else oz_gram_body_la<6 - kSlo, 3, false, DIAG>(a, smem, wave);
-    }
-  } else if (wave < 4) {
-    if (live) oz_gram_body_la<kSlo, 4, true, DIAG>(a, smem, wave);
-    else oz_gram_body_la<kSlo, 4, false, DIAG>(a, smem, wave);
-  } else if (wave < 6) {
-    if (live) oz_gram_body_la<kS - kSlo, 4, true, DIAG>(a, smem, wave);
-    else oz_gram_body_la<kS - kSlo, 4, false, DIAG>(a, smem, wave);
-  } else {
-    if (live) oz_gram_body_la<kS - kSlo, 3, true, DIAG>(a, smem, wave);
-    else oz_gram_body_la<kS - kSlo, 3, false, DIAG>(a, smem, wave);
-  }
-}
-
 template <int DIAG>
 __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // the replicate tile of this block (same map as the body) decides which batches exist
-  const uint32_t nwg = gridDim.x, bid = blockIdx.x;
-  const uint32_t xcd = bid & 7u, slot = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7u;
-  const uint32_t wi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
-  const uint32_t tq = wi / (uint32_t)a.n_ct, rt = tq % a.n_rt, chunk = tq / a.n_rt;
+  uint32_t ct, rt, chunk;
+  oz_map(a, &ct, &rt, &chunk);
   const bool live = rt * 4u + (uint32_t)(wave & 3) < a.nb_rep;
-  const bool six = a.nsl[chunk * (uint32_t)a.n_ct + wi % (uint32_t)a.n_ct] == 6;
+  const bool six = a.nsl[chunk * (uint32_t)a.n_ct + ct] == 6;
   // B piece t of wave w is 8 t + w. Waves 0-3: slices 0-3, two B pieces; 4-5: slices 4-6, two B pieces; 6-7: slices 4-6, one piece.
   // Six slices: waves 0-3 take slices 0 .. kSix0 - 1, waves 4-7 the rest of 0-5, one piece each;
   // pieces 12-13 (slice 6) are not loaded.
@@ -1033,10 +868,7 @@ int oz_prepare(ob_panel* p, hipStream_t s) {
   const int npe = n_chunks * npp;
   hipLaunchKernelGGL(oz_pexp_finish_kernel, dim3((npe + 255) / 256), dim3(256), 0, s, p->d_oz_pexp, npe);
   OZ_HIP(hipGetLastError());
-  static const int force7 = [] {
-    const char* e = getenv("OB_GRAM_DIGITS");
-    return e && atoi(e) == 7 ? 1 : 0;
-  }();
+  const int force7 = ob::opt_int(ob::Opt::GramDigits, 0) == 7 ? 1 : 0;
   const int nct_all = n_chunks * n_ct;
   hipLaunchKernelGGL(oz_nsl_kernel, dim3((nct_all + 255) / 256), dim3(256), 0, s, (const int32_t*)p->d_oz_pexp,
                      (const long long*)p->d_oz_psum, (const uint32_t*)p->d_chunks, p->n[0], p->n[1], p->e, n_ct, npp,
@@ -1096,7 +928,7 @@ int oz_collect(ob_panel* p) {
   p->timing.oz_tiles = p->oz_tiles;
   if (p->oz_overflow)
     return ob::fail(OB_E_UNSUPPORTED, "more than %d rows hold non-finite values (NaN or inf); the i8 Gram keeps at most "
-                                      "that many exception rows (OB_GRAM_PATH=f64 runs the f64 MFMA Gram)",
+                                      "that many exception rows (option gram_path = 1 runs the f64 MFMA Gram)",
                     kOzExcCap);
   return OB_OK;
 }
@@ -1141,10 +973,6 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
   a.n_ct = p->oz_n_ct;
   a.e_pad = p->e_pad;
   a.n_pairs_pad = p->oz_n_ct * kPairsPerTile;
-  static const int diag = [] {
-    const char* e = getenv("OB_GRAM_DIAG");
-    return e ? atoi(e) & 30 : 0;
-  }();
   const uint32_t blocks = (uint32_t)n_chunks * a.n_rt * (uint32_t)a.n_ct;
   auto launch = [&](auto kern) -> hipError_t {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
@@ -1152,22 +980,8 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
     hipLaunchKernelGGL(kern, dim3(blocks), dim3(kWaves * 64), kLdsBytes, s, a);
     return hipGetLastError();
   };
-  static const bool a_lds = [] {  // OB_OZ_A_LDS=0/1 at run time overrides the build default (A/B)
-    const char* e = getenv("OB_OZ_A_LDS");
-    return e ? atoi(e) != 0 : OB_OZ_A_LDS != 0;
-  }();
-  if (a_lds && (diag == 0 || diag == 2)) {
-    auto launch_la = [&](auto kern) -> hipError_t {
-      hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytesLA);
-      if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(kern, dim3(blocks), dim3(kWaves * 64), kLdsBytesLA, s, a);
-      return hipGetLastError();
-    };
-    if (diag == 2) OZ_HIP(launch_la(oz_gram_la_kernel<2>));
-    else OZ_HIP(launch_la(oz_gram_la_kernel<0>));
-    return OB_OK;
-  }
-  switch (diag) {
+#if OB_TUNING  // timing ablations (gram_diag): wrong results by design
+  switch (ob::opt_int(ob::Opt::GramDiag, 0) & 30) {
     case 2: OZ_HIP(launch(oz_gram_kernel<2>)); break;
     case 4: OZ_HIP(launch(oz_gram_kernel<4>)); break;
     case 6: OZ_HIP(launch(oz_gram_kernel<6>)); break;
@@ -1175,6 +989,9 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
     case 16: OZ_HIP(launch(oz_gram_kernel<16>)); break;
     default: OZ_HIP(launch(oz_gram_kernel<0>)); break;
   }
+#else
+  OZ_HIP(launch(oz_gram_kernel<0>));
+#endif
   return OB_OK;
 }
 

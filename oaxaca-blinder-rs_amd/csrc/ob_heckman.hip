@@ -28,6 +28,7 @@
 #include "ob_device.hpp"
 #include "ob_engine.hpp"
 #include "ob_heckman.hpp"
+#include "ob_options.hpp"
 #include "ob_spec.h"
 
 namespace {
@@ -111,12 +112,9 @@ __device__ __forceinline__ void npdf_ncdf(double z, double& pdf, double& cdf) {
 }
 
 // The probit and sums kernels take pdf and cdf from npdf_ncdf (one exp per row; probit launch 11.8
-// -> 9.0 ms at configs[1] + selection, profiles/r04_ab_heckman_erfc.txt) unless OB_HK_ERFC=0, which
-// keeps the library's erfc beside a second exp.
-inline bool hk_cody() {
-  static const bool v = !(getenv("OB_HK_ERFC") && atoi(getenv("OB_HK_ERFC")) == 0);
-  return v;
-}
+// -> 9.0 ms at configs[1] + selection, profiles/r04_ab_heckman_erfc.txt) unless option hk_erfc = 0
+// (ob_set_option), which keeps the library's erfc beside a second exp.
+inline bool hk_cody() { return ob::opt_int(ob::Opt::HkErfc, 1) != 0; }
 
 // 1/v within ~1 ulp: v_rcp_f64 and two Newton steps instead of the IEEE division sequence (the
 // operands are normal numbers: clamped probabilities).

@@ -43,6 +43,7 @@
 #include "ob_device.hpp"
 #include "ob_engine.hpp"
 #include "ob_mm.hpp"
+#include "ob_options.hpp"
 #include "ob_spec.h"
 
 namespace {
@@ -1664,11 +1665,8 @@ struct Buffers {
 
 void free_workspace(void* b) { delete static_cast<Buffers*>(b); }
 
-// OB_MM_TRACE=1: per-iteration active fits and the final fit statuses on stderr.
-bool trace() {
-  static const bool t = getenv("OB_MM_TRACE") != nullptr;
-  return t;
-}
+// Option mm_trace (ob_set_option): per-iteration active fits and the final fit statuses on stderr.
+bool trace() { return ob::opt_int(ob::Opt::MmTrace, 0) != 0; }
 
 struct MmStats {
   double assemble_ms = 0.0, fit_rows = 0.0, sync_ms = 0.0;
@@ -1847,12 +1845,8 @@ int reduced_round(const MmArgs& a, int K, int round, hipStream_t s, MmStats& st)
   a2.rowlist = a.blist;
   a2.nrows = a.bnrows;
   a2.rp = 1;
-  static const double d2 = [] {  // OB_MM_DELTA2: tuning knob (results do not depend on it)
-    const char* e = getenv("OB_MM_DELTA2");
-    const double v = e ? atof(e) : 0.0;
-    return v > 0.0 ? v : kDelta2;
-  }();
-  a2.dscale = d2;
+  const double d2 = ob::opt_double(ob::Opt::MmDelta2, 0.0);  // option mm_delta2: tuning
+  a2.dscale = d2 > 0.0 ? d2 : kDelta2;
   return ipm(a2, K, 3, s, st);
 }
 
@@ -1907,25 +1901,14 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, MmS
     a1.nch[1] = rd.nch1[1];
     a1.rowlist = rd.list1;
     a1.nrows = rd.nrows1;
-    static const double tol1 = [] {  // OB_MM_TOL1: tuning knob (the verification keeps results exact)
-      const char* e = getenv("OB_MM_TOL1");
-      const double v = e ? atof(e) : 0.0;
-      return v > 0.0 ? v : kPhase1Tol;
-    }();
-    a1.tol = tol1;
+    const double tol1 = ob::opt_double(ob::Opt::MmTol1, 0.0);  // option mm_tol1 (the verification keeps results exact)
+    a1.tol = tol1 > 0.0 ? tol1 : kPhase1Tol;
     a1.gchol = rd.gchol;
-    static const double d1 = [] {  // OB_MM_DELTA1: tuning knob (results do not depend on it)
-      const char* e = getenv("OB_MM_DELTA1");
-      const double v = e ? atof(e) : 0.0;
-      return v > 0.0 ? v : kDelta1;
-    }();
-    a1.dscale = d1;
+    const double d1 = ob::opt_double(ob::Opt::MmDelta1, 0.0);  // option mm_delta1: tuning
+    a1.dscale = d1 > 0.0 ? d1 : kDelta1;
     // phase 1 solves S1 of the S quantiles (their own fit arrays); the others interpolate
-    static const int fstride = [] {  // OB_MM_FIT_STRIDE: tuning knob (results do not depend on it)
-      const char* e = getenv("OB_MM_FIT_STRIDE");
-      const int v = e ? atoi(e) : 0;
-      return v > 0 ? v : kFitStride;
-    }();
+    const int fs_opt = ob::opt_int(ob::Opt::MmFitStride, 0);  // option mm_fit_stride: tuning
+    const int fstride = fs_opt > 0 ? fs_opt : kFitStride;
     const int f = a.S >= kFitStrideMin ? fstride : 1;
     a1.S = f > 1 ? (a.S - 1 + f - 1) / f + 1 : a.S;
     a1.S_pad = (a1.S + 63) / 64 * 64;
@@ -1952,15 +1935,9 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, MmS
     al.gchol = rd.gchol;
     hipLaunchKernelGGL(mm_lev_kernel, dim3(nch, 1, a.n_rb), dim3(256), 0, s, al, K);
     MM_OK(hipGetLastError());
-    static const double kappa = [] {
-      const char* e = getenv("OB_MM_KAPPA");
-      const double v = e ? atof(e) : 0.0;
-      return v > 0.0 ? v : kBandKappa;
-    }();
-    static const double band0 = [] {  // OB_MM_BAND0: the same kind of knob, the bands' constant term
-      const char* e = getenv("OB_MM_BAND0");
-      return e ? atof(e) : kBand0;
-    }();
+    const double kappa_opt = ob::opt_double(ob::Opt::MmKappa, 0.0);  // options mm_kappa, mm_band0: tuning
+    const double kappa = kappa_opt > 0.0 ? kappa_opt : kBandKappa;
+    const double band0 = ob::opt_double(ob::Opt::MmBand0, kBand0);
     hipLaunchKernelGGL(mm_band_kernel, dim3((unsigned)n_fits), dim3(256), 0, s, a, K, kappa, band0);
     MM_OK(hipGetLastError());
     MM_OK(hipMemsetAsync(a.xmask, 0, sizeof(uint32_t) * (size_t)a.n_rb * nch * (a.S_pad / 64) * (a.cap / 32), s));
@@ -2038,22 +2015,20 @@ int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_
   const size_t rep_rows = (size_t)p->n[0] + p->n[1];
   if (p->n[0] > 1024u * kRc || p->n[1] > 1024u * kRc)  // mm_shift_kernel's chunk prefix (1024 chunks)
     return ob::fail(OB_E_UNSUPPORTED, "Machado-Mata groups take at most %u rows", 1024u * kRc);
-  // Row reduction: OB_MM_REDUCE=0 off, =1 on; by default on when both groups have >= 2^16 rows.
+  // Row reduction: option mm_reduce 0 off, 1 on; by default on when both groups have >= 2^16 rows.
   Reduction rd;
   {
-    const char* e = getenv("OB_MM_REDUCE");
-    rd.on = e && *e ? (e[0] != '0') : (p->n[0] >= 65536u && p->n[1] >= 65536u);
+    const int r = ob::opt_int(ob::Opt::MmReduce, -1);
+    rd.on = r >= 0 ? r != 0 : (p->n[0] >= 65536u && p->n[1] >= 65536u);
   }
   const uint32_t rcF = rd.on ? kRcF : kRc;  // the full lists' chunk rows (= their capacity)
   const uint32_t nch0 = (p->n[0] + rcF - 1) / rcF, nch1 = (p->n[1] + rcF - 1) / rcF;
   // replicate slots per batch: IPM state (x, z, w: 3 f64 per fit and list entry, rcF entries per
-  // chunk) within OB_MM_STATE_GB (default 160 of the 288 GB): a batch's tail iterations (few live
-  // fits) and phase 1 cost about the same time for 2 or 12 replicates, so wider batches amortize them
-  static const uint64_t state_budget = [] {
-    const char* e = getenv("OB_MM_STATE_GB");
-    const double v = e ? atof(e) : 0.0;
-    return (uint64_t)((v > 0.0 ? v : 160.0) * (double)(1ull << 30));
-  }();
+  // chunk) within option mm_state_gb (default 160 of the 288 GB): a batch's tail iterations (few
+  // live fits) and phase 1 cost about the same time for 2 or 12 replicates, so wider batches
+  // amortize them
+  const double sgb = ob::opt_double(ob::Opt::MmStateGb, 0.0);
+  const uint64_t state_budget = (uint64_t)((sgb > 0.0 ? sgb : 160.0) * (double)(1ull << 30));
   const size_t state_rows = (size_t)(nch0 + nch1) * rcF;
   const size_t state_per_rep = 3 * state_rows * S_pad * sizeof(double);
   const uint64_t want = std::max<uint64_t>(n_reps, 1);

@@ -88,7 +88,8 @@ def test_i8_gram_six_slices(ob, O):
 
 
 def test_i8_rows_equal_f64_rows(ob, O):
-    """Default (i8) rows vs OB_GRAM_PATH=f64 rows, all reference modes, with dummies."""
+    """Default (i8) rows vs the f64 MFMA Gram's rows (option gram_path = 1), all reference modes,
+    with dummies."""
     d = O.synthetic_panel(12000, 6, True, seed=4)
     rng = np.random.default_rng(4)
     cat_a = rng.integers(0, 4, d["xa"].shape[0])
@@ -100,12 +101,9 @@ def test_i8_rows_equal_f64_rows(ob, O):
         for ref in (0, 1, 2, 3):
             r8, ok8 = panel.boot(SEED, 0, 200, ref)
             assert panel.timing()["gram_path"] == 2
-            os.environ["OB_GRAM_PATH"] = "f64"
-            try:
+            with ob._native.option("gram_path", 1):
                 r64, ok64 = panel.boot(SEED, 0, 200, ref)
                 assert panel.timing()["gram_path"] == 1
-            finally:
-                del os.environ["OB_GRAM_PATH"]
             assert np.array_equal(ok8, ok64)
             gap = np.abs(r64[:, 5:6])
             assert np.all(np.abs(r8 - r64) <= 1e-9 * np.maximum(np.abs(r64), gap)), ref

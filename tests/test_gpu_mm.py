@@ -188,12 +188,13 @@ def test_mm_identities_at_size(ob):
 
 
 @pytest.fixture
-def reduce_env(monkeypatch):
-    """OB_MM_REDUCE: 1 forces the row reduction (subsample, bands, reduced LPs, verification) at
-    any size, 0 turns it off; unset, it runs when both groups have >= 2^16 rows."""
+def reduce_env(ob):
+    """Option mm_reduce: "1" forces the row reduction (subsample, bands, reduced LPs, verification)
+    at any size, "0" turns it off; "" (unset) runs it when both groups have >= 2^16 rows."""
     def set_(v):
-        monkeypatch.setenv("OB_MM_REDUCE", v)
-    return set_
+        ob._native.set_option("mm_reduce", int(v) if v else None)
+    yield set_
+    ob._native.set_option("mm_reduce", None)
 
 
 @pytest.mark.parametrize("n,p,sims", [(3000, 2, 40), (6000, 5, 24), (20000, 15, 8)])

@@ -37,17 +37,6 @@ def test_shipped_gram_kernel_waits_are_clean(gram_isa):
     assert C.check(insns) == []
 
 
-def test_a_through_lds_variant_waits_are_clean():
-    """oz_gram_la_kernel (OB_OZ_A_LDS=1, A/B variant): every operand by untracked LDS-DMA, the same
-    uniform steps and counted waits."""
-    if not os.path.exists(SO):
-        pytest.skip("engine library missing")
-    sym = "_ZN12_GLOBAL__N_117oz_gram_la_kernelILi0EEEvNS_6OzArgsE"
-    insns = C.parse(C.disassemble_symbol(SO, sym), sym)
-    assert sum(1 for i in insns if i.mnem.startswith("global_load_lds")) >= 64
-    assert C.check(insns) == []
-
-
 def test_checker_flags_the_reverted_manual_a_variant():
     """The compiled code of commit 32e45ae (tests/isa/reverted_manual_a.s, tools/isa_reverted_excerpt.sh):
     the epilogue writes v42 while the dead inline-asm A load into v[42:45] is still in flight."""

@@ -6,6 +6,7 @@
 #   (an empty string is the default environment) -> gpurun_out/TAG_env<i>_<round>.json
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+source "$(dirname "${BASH_SOURCE[0]}")/tuning_env.sh"  # OB_* switches: tuning build only
 T=${TAG:-abenv}
 if [ -n "${TESTS:-}" ]; then
   for e in "$@"; do

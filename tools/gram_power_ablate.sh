@@ -5,6 +5,7 @@
 # and MFMA busy cycles. Run on the GPU box:  bash tools/gram_power_ablate.sh TAG
 #   -> gpurun_out/TAG_power.txt
 set -euo pipefail
+source "$(dirname "${BASH_SOURCE[0]}")/tuning_env.sh"  # OB_* switches: tuning build only
 TAG=${1:-rXX}
 OUT=$PWD/gpurun_out
 REPO=$PWD

@@ -3,6 +3,7 @@
 # throughput and the phase-2 iteration trace per setting. Run on the GPU box:
 #   bash tools/mm_delta_sweep.sh TAG 1 0.3 0.1 ...   -> gpurun_out/TAG_delta.txt
 set -o pipefail
+source "$(dirname "${BASH_SOURCE[0]}")/tuning_env.sh"  # OB_* switches: tuning build only
 TAG=$1; shift
 mkdir -p gpurun_out
 : > gpurun_out/${TAG}_delta.txt

@@ -2,6 +2,7 @@
 # configs[4] at a given batch width: kernel-trace stats (rocprofv3) and the phase trace (OB_MM_TRACE=1).
 # usage: bash tools/mm_profile.sh TAG REPS  -> gpurun_out/TAG_mmstats/, TAG_mmtrace.log
 set -euo pipefail
+source "$(dirname "${BASH_SOURCE[0]}")/tuning_env.sh"  # OB_* switches: tuning build only
 TAG=${1:-mm}; R=${2:-12}
 OUT=$PWD/gpurun_out; REPO=$PWD
 mkdir -p "$OUT"

@@ -2,6 +2,7 @@
 # SQ counters of the level-1 kernel under the OB_L1_DIAG ablations (tools/l1_ablate.sh), one
 # rocprofv3 pass per variant. usage: bash tools/pmc_l1.sh TAG "0 1 3"  -> gpurun_out/TAG_l1pmc_*.txt
 set -euo pipefail
+source "$(dirname "${BASH_SOURCE[0]}")/tuning_env.sh"  # OB_* switches: tuning build only
 TAG=${1:-rXX}
 VARIANTS=${2:-"0 1 3 11 16 20"}
 OUT=$PWD/gpurun_out

@@ -3,6 +3,7 @@
 # pass; 4 SQ counters) -> the JSON bench.py --heckman prices its roofline with. Run on the GPU box:
 #   [OB_HK_ERFC=0] bash tools/pmc_probit.sh TAG   -> gpurun_out/TAG_pmc_probit.json
 set -euo pipefail
+source "$(dirname "${BASH_SOURCE[0]}")/tuning_env.sh"  # OB_* switches: tuning build only
 TAG=${1:-rXX}
 OUT=$PWD/gpurun_out
 REPO=$PWD
