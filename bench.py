@@ -669,8 +669,9 @@ def main():
             if pending:
                 stats = aggregate(pending.pop())
             pending.append(b)
-        panel.sync()
-        return stats, panel.timing()
+        # no host synchronization per step: step i + 1 is enqueued while step i runs; the engine
+        # sums the HIP-event kernel times of every call until panel.sync() (ob_panel_sync)
+        return stats
 
     def drain():
         return aggregate(pending.pop()) if pending else None
@@ -678,24 +679,22 @@ def main():
     for i in range(args.warmup):
         step(i)
     drain()
+    panel.sync()  # collects (and clears) the warmup's timings and overflow flag
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    sums = {"gram_ms": 0.0, "level1_ms": 0.0, "counts_ms": 0.0, "reduce_ms": 0.0, "solve_ms": 0.0, "gather_ms": 0.0}
-    launches = 0
     stats = None
-    gram_path = 1
-    tiles6 = (0, 0)
     for i in range(args.steps):
-        s_, tm = step(args.warmup + i)
+        s_ = step(args.warmup + i)
         stats = s_ if s_ is not None else stats
-        for k_ in sums:
-            sums[k_] += tm[k_]
-        launches += tm["gram_launches"]
-        gram_path = tm["gram_path"]
-        tiles6 = (tm["oz_tiles6"], tm["oz_tiles"])
     stats = drain() if rank == 0 else None  # the last step's aggregation, inside the timed region
+    panel.sync()  # every timed call's kernel times (HIP events), the overflow checks
+    tm = panel.timing()
+    sums = {k_: tm[k_] for k_ in ("gram_ms", "level1_ms", "counts_ms", "reduce_ms", "solve_ms", "gather_ms")}
+    launches = tm["gram_launches"]
+    gram_path = tm["gram_path"]
+    tiles6 = (tm["oz_tiles6"], tm["oz_tiles"])
     if dist:
         dist.barrier()
     torch.cuda.synchronize()

@@ -1660,7 +1660,8 @@ int engine_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_rep
   Plan pl = make_plan(p, n_reps, false);
   OB_TRY(ensure_buf(&p->d_m1, p->cap_m1, (size_t)tiles * pl.rep_pad));
   OB_TRY(ensure_buf(&p->d_counts, p->cap_counts, (size_t)tiles * pl.nb_rep * 4 * kCimgWords));
-  HIP_OK(hipMemsetAsync(p->d_flags, 0, sizeof(uint32_t), s));
+  // its own overflow word (d_flags[2]): word 0 belongs to boot calls that may still be pending
+  HIP_OK(hipMemsetAsync(p->d_flags + 2, 0, sizeof(uint32_t), s));
   const uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
   const size_t lds_l1 = sizeof(uint32_t) * std::max(l1_lds_words(p->ntiles[0]), l1_lds_words(p->ntiles[1]));
   HIP_OK(hipFuncSetAttribute((const void*)ob_level1_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_l1));
@@ -1670,6 +1671,7 @@ int engine_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_rep
                      (uint32_t)first_rep, tiles, key0, key1, p->d_m1, ky);
   HIP_OK(hipGetLastError());
   GramArgs ga = gram_args(p, pl);
+  ga.flags = p->d_flags + 2;
   ga.m1 = p->d_m1;
   ga.n_reps = n_reps;
   ga.first_rep = (uint32_t)first_rep;
@@ -1735,13 +1737,18 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   int force = p->gram_force;
   if (!force) force = ob::opt_int(ob::Opt::GramPath, 0);
   bool use_i8 = force != 1;
-  std::memset(&p->timing, 0, sizeof(p->timing));
+  if (!p->timing_pending) {  // the first call since the last collect: its timings start from zero
+    std::memset(&p->timing, 0, sizeof(p->timing));
+    p->pending_segments = 0;
+    p->pending_gathers = 0;
+  }
   if (use_i8) {
     OB_TRY(ob::oz_prepare(p, s));
     use_i8 = p->oz_state == 1;
     if (!use_i8 && force == 2) return ob::fail(OB_E_UNSUPPORTED, "the i8 Gram's digit images do not fit in HBM");
   }
-  HIP_OK(hipMemsetAsync(p->d_flags, 0, sizeof(uint32_t), s));
+  // the overflow flag (d_flags[0]) is sticky over the calls since the last collect, which reads and
+  // clears it: no per-call reset, so an enqueued call never erases a pending one's flag
 
   const size_t lds_l1 = sizeof(uint32_t) * std::max(l1_lds_words(p->ntiles[0]), l1_lds_words(p->ntiles[1]));
   ob_ky_tables ky{};
@@ -1767,10 +1774,9 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   p->timing.blocks = use_i8 ? (int32_t)((uint32_t)nch * ((pl.nb_rep + 3) / 4) * (uint32_t)p->oz_n_ct)
                             : (int32_t)(pl.nb_rep * pl.n_cg * (uint32_t)nch);
   p->timing.gram_path = use_i8 ? 2 : 1;
-  p->pending_segments = 0;
   const uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
   const size_t nseg = (size_t)((n_reps + seg - 1) / seg);
-  while (p->seg_events.size() < kSegEvents * nseg) {
+  while (p->seg_events.size() < kSegEvents * (nseg + (size_t)p->pending_segments)) {
     hipEvent_t e;
     HIP_OK(hipEventCreate(&e));
     p->seg_events.push_back(e);
@@ -1873,15 +1879,17 @@ int engine_collect(ob_panel* p) {
     }
   }
   if (p->heckman) p->timing.heckman_ms = p->timing.solve_ms;
-  if (p->gather_timed) {  // ob_shard.cpp: the RCCL all-gather after the last segment
+  for (int k = 0; k < p->pending_gathers; ++k) {  // ob_shard.cpp: the RCCL all-gathers
     float t = 0.f;
-    HIP_OK(hipEventElapsedTime(&t, p->gather_ev[0], p->gather_ev[1]));
-    p->timing.gather_ms = t;
-    p->gather_timed = false;
+    HIP_OK(hipEventElapsedTime(&t, p->gather_evs[2 * k], p->gather_evs[2 * k + 1]));
+    p->timing.gather_ms += t;
   }
+  p->pending_gathers = 0;
+  p->pending_segments = 0;
   if (p->timing.gram_path == 2) OB_TRY(ob::oz_collect(p));
   uint32_t flag = 0;
   HIP_OK(hipMemcpy(&flag, p->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (flag) HIP_OK(hipMemset(p->d_flags, 0, sizeof(uint32_t)));  // collected: the next calls start clean
   // a count of 256+ wraps its byte (bit 0: byte sums differ from the tile counts); on the i8 path
   // the bound is 127 either way
   if ((flag & 1u) && p->timing.gram_path != 2)
@@ -2140,7 +2148,14 @@ int ob_point_estimate(ob_panel* p, int ref_mode, double* row, double* resid_b) {
                       "%sInsufficient data for OLS calculation: n_obs (%u) must be strictly greater than k (%d)",
                       ob::error_prefix(OB_E_INSUFFICIENT), p->n[0] + p->n[1], p->k + 1);
   }
-  return ob::engine_point_estimate(p, ref_mode, row, resid_b);
+  // ordered after any call on this panel from another stream (an async boot on a user
+  // stream may still read the buffers the point estimate rewrites), and marked for the next one
+  HIP_OK(hipSetDevice(p->ctx->device));
+  hipStream_t s = p->ctx->stream;
+  OB_TRY(ob::engine_order(p, s));
+  const int rc = ob::engine_point_estimate(p, ref_mode, row, resid_b);
+  const int rm = ob::engine_mark(p, s);
+  return rc != OB_OK ? rc : rm;
 }
 
 int ob_boot_run_device(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps, int ref_mode,
@@ -2196,10 +2211,13 @@ int ob_debug_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_r
   HIP_OK(hipSetDevice(p->ctx->device));
   hipStream_t s = p->ctx->stream;
   uint32_t nb = 0, rep_pad = 0;
-  OB_TRY(ob::engine_counts(p, seed, first_rep, n_reps, s, &nb, &rep_pad));
+  OB_TRY(ob::engine_order(p, s));  // after any call on this panel from another stream
+  const int rc = ob::engine_counts(p, seed, first_rep, n_reps, s, &nb, &rep_pad);
+  OB_TRY(ob::engine_mark(p, s));
+  OB_TRY(rc);
   HIP_OK(hipStreamSynchronize(s));
   uint32_t flag = 0;
-  HIP_OK(hipMemcpy(&flag, p->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(&flag, p->d_flags + 2, sizeof(uint32_t), hipMemcpyDeviceToHost));  // engine_counts' word
   if (flag & 1u) return ob::fail(OB_E_OVERFLOW, "a resampled row was drawn more than 255 times in one replicate");
   const uint32_t tiles = p->ntiles[0] + p->ntiles[1], tg = p->ntiles[group], t0 = group ? p->ntiles[0] : 0u;
   const uint32_t n = p->n[group];

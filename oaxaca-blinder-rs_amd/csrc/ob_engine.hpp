@@ -90,8 +90,8 @@ struct ob_panel {
   std::vector<int32_t> gather_cols;   // gathered row columns, ascending (empty: every column)
   int32_t* d_gather_map = nullptr;    // [row_len] slot of each column or -1, then [nc] the columns
   bool gather_map_ready = false;
-  hipEvent_t gather_ev[2] = {nullptr, nullptr};
-  bool gather_timed = false;
+  std::vector<hipEvent_t> gather_evs;  // 2 per RCCL gather (start, end) since the last collect
+  int pending_gathers = 0;
   // integer-sliced Gram (ob_gram_i8.hip): digit images per group, pair exponents per chunk
   int oz_state = 0;  // 0 not built, 1 ready, -1 unavailable (the f64 MFMA Gram is used)
   int gram_force = 0;  // 0: i8 when available; 1: f64 MFMA Gram; 2: i8 (ob_debug_gram, OB_GRAM_PATH)
@@ -119,7 +119,9 @@ struct ob_panel {
   // the panel's chunk table (a function of the panel only), uploaded once into d_chunks
   std::vector<uint32_t> chunks;
   bool chunks_ready = false;
-  std::vector<hipEvent_t> seg_events;  // 6 per segment of the last boot run
+  // timing and the overflow flag accumulate over every boot call since the last engine_collect
+  // (ob_panel_sync), so a caller may enqueue several calls before it synchronizes
+  std::vector<hipEvent_t> seg_events;  // 6 per segment of the boot calls since the last collect
   ob_timing timing = {};
   bool timing_pending = false;
   hipStream_t last_stream = nullptr;

@@ -477,10 +477,15 @@ struct OzArgs {
 };
 
 constexpr int kWaves = 8;                         // 2 per SIMD: (replicate batch, slice group)
-constexpr int kNbuf = 4;                          // LDS ring stages (sub-tiles)
+#ifndef OB_OZ_SUB2
+// 1: two 64-row sub-tiles per barrier (one barrier per 128 rows) over an 8-stage ring; 0: one
+// sub-tile per barrier over a 4-stage ring
+#define OB_OZ_SUB2 1
+#endif
+constexpr int kNbuf = OB_OZ_SUB2 ? 8 : 4;         // LDS ring stages (sub-tiles)
 constexpr int kBDma = (kSubUnits + 64 * kWaves - 1) / (64 * kWaves);  // B DMA instructions per wave (<=)
 constexpr int kBDmaTotal = kSubUnits / 64;        // 14 per sub-tile, spread over the waves
-constexpr size_t kLdsB = kNbuf * (size_t)kSubUnits * 16;      // B ring (56 KB)
+constexpr size_t kLdsB = kNbuf * (size_t)kSubUnits * 16;      // B ring (56 KB; 112 KB with OB_OZ_SUB2)
 constexpr size_t kLdsX = 4 * 64 * (size_t)kPairsPerTile * 8;  // slice-group exchange (64 KB, over the ring)
 constexpr size_t kLdsBytes = kLdsB > kLdsX ? kLdsB : kLdsX;
 static_assert(kBDma == 2 && kBDmaTotal == 14, "B DMA split below assumes 14 instructions over 8 waves");
@@ -578,7 +583,10 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   const uint32_t g = a.chunks[3 * chunk];
   const uint32_t n = g ? a.n1 : a.n0, tg0 = g ? a.tiles0 : 0u;
   const uint32_t s0 = a.chunks[3 * chunk + 1] * 4u;
-  const uint32_t s1 = min(a.chunks[3 * chunk + 2] * 4u, (n + 63u) >> 6);
+  // OB_OZ_SUB2: an odd sub-tile count (a group's last chunk) runs one padding sub-tile more, whose
+  // count image and digits exist (tiles are 4 sub-tiles, s0 a multiple of 4) and hold zeros
+  const uint32_t s1 = OB_OZ_SUB2 ? (min(a.chunks[3 * chunk + 2] * 4u, (n + 63u) >> 6) + 1u) & ~1u
+                                 : min(a.chunks[3 * chunk + 2] * 4u, (n + 63u) >> 6);
   const ob_v4i* Bg = g ? a.B1 : a.B0;
   const uint32_t batch = rt * 4u + (uint32_t)wb;
   auto dma = [&](int buf, uint32_t s) {
@@ -670,6 +678,57 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   // same loads and waits, so each path through the loop presents the same queue at each barrier.
   // (Ghost steps past the end with branch-guarded MFMAs, the round-4 first form, read 5 GB more
   // per launch and ran 1.5 % slower: profiles/r04_ab_gram_tail.txt.)
+#if OB_OZ_SUB2
+  // Two sub-tiles (s, s + 1) per barrier. Sub-tile u uses A slot (u - s0) % 3 and ring stage
+  // (u - s0) % 8. Order: MFMAs (s, 0) | read (s, 1); MFMAs (s, 1) | read (s + 1, 0); A(s + 3) into
+  // s's slot; MFMAs (s + 1, 0) | read (s + 1, 1); wait + barrier: stages s + 2, s + 3 landed (their
+  // DMA was issued three barriers earlier), every read of s, s + 1 done; refill those two stages
+  // with s + 8, s + 9; read (s + 2, 0); MFMAs (s + 1, 1); A(s + 4) into s + 1's slot. Newer than the
+  // DMA of s + 2, s + 3 at the barrier: A(s - 2); A(s - 1), 2 NB DMA, A(s); A(s + 1), 2 NB DMA,
+  // A(s + 2); A(s + 3) = 24 + 4 NB (LIVE) or 4 NB loads.
+  constexpr int PER2 = 4 * NB + (LIVE ? 24 : 0);
+  auto step2 = [&](uint32_t s, auto J0, auto J1) {
+    constexpr int j0 = decltype(J0)::value, j1 = decltype(J1)::value;
+    const int b0 = (int)((s - s0) & (kNbuf - 1)), b1 = (b0 + 1) & (kNbuf - 1), b2 = (b0 + 2) & (kNbuf - 1);
+    if constexpr (LIVE) {
+      read(b0, 1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(DIAG & 2)) oz_mfmas<NQ>(acc, 0, ar[j0], fb0);
+      __builtin_amdgcn_sched_barrier(0);
+      read(b1, 0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(DIAG & 2)) oz_mfmas<NQ>(acc, 1, ar[j0], fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(DIAG & 4)) aload(ar[j0], min(s + 3, s1 - 1));
+      read(b1, 1, fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(DIAG & 2)) oz_mfmas<NQ>(acc, 0, ar[j1], fb0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (DIAG & 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER2) : "memory");
+    oz_barrier();
+    if constexpr (!(DIAG & 4)) {
+      dma(b0, min(s + kNbuf, s1 - 1));
+      dma(b1, min(s + kNbuf + 1, s1 - 1));
+    }
+    if constexpr (LIVE) {
+      read(b2, 0, fb0);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(DIAG & 2)) oz_mfmas<NQ>(acc, 1, ar[j1], fb1);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (!(DIAG & 4)) aload(ar[j1], min(s + 4, s1 - 1));
+    }
+  };
+  uint32_t s = s0;  // s1 - s0 is even here
+  for (; s + 6 <= s1; s += 6) {
+    step2(s, IC<0>{}, IC<1>{});
+    step2(s + 2, IC<2>{}, IC<0>{});
+    step2(s + 4, IC<1>{}, IC<2>{});
+  }
+  if (s < s1) step2(s, IC<0>{}, IC<1>{});
+  if (s + 2 < s1) step2(s + 2, IC<2>{}, IC<0>{});
+#else
   uint32_t s = s0;
   for (; s + 3 <= s1; s += 3) {
     step(s, IC<0>{});
@@ -678,6 +737,7 @@ __device__ __forceinline__ void oz_gram_body(const OzArgs& a, unsigned char* sme
   }
   if (s < s1) step(s, IC<0>{});
   if (s + 1 < s1) step(s + 1, IC<1>{});
+#endif
   // slices -> f64: this wave's digits meet exactly in int64, one ldexp each; group 1 goes through
   // LDS to its group-0 partner, which adds (one rounding) and stores.
   int E[2];

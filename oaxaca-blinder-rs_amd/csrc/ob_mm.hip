@@ -1999,8 +1999,23 @@ int run_batch(MmArgs a, int K, hipStream_t s, double* rows_h, uint8_t* ok_h, MmS
 
 namespace ob {
 
+static int mm_run_impl(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_q, uint64_t first_rep,
+                       uint64_t n_reps, bool with_point, double* rows, uint8_t* ok, int* max_iters);
+
+// Machado-Mata on the context stream, ordered after any call on this panel from another stream
+// (engine_order: an async boot on a user stream may still read the count images and flags this
+// run rewrites) and marked so that the next call on another stream waits for it.
 int mm_run(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_q, uint64_t first_rep,
            uint64_t n_reps, bool with_point, double* rows, uint8_t* ok, int* max_iters) {
+  MM_OK(hipSetDevice(p->ctx->device));
+  OB_TRY(ob::engine_order(p, p->ctx->stream));
+  const int rc = mm_run_impl(p, seed, sims, quantiles, n_q, first_rep, n_reps, with_point, rows, ok, max_iters);
+  const int rm = ob::engine_mark(p, p->ctx->stream);
+  return rc != OB_OK ? rc : rm;
+}
+
+static int mm_run_impl(ob_panel* p, uint64_t seed, int sims, const double* quantiles, int n_q, uint64_t first_rep,
+                       uint64_t n_reps, bool with_point, double* rows, uint8_t* ok, int* max_iters) {
   ob_ctx* ctx = p->ctx;
   MM_OK(hipSetDevice(ctx->device));
   const int K = p->k;

@@ -151,15 +151,17 @@ int shard_compute(ob_panel* p, uint64_t seed, const Shard& sh, int world, int re
   OB_TRY(ensure_dev(&p->d_gather_ok, &p->cap_gather_ok, slots * (size_t)world));
   if (sh.count) {
     OB_TRY(ob::engine_boot(p, seed, sh.first, sh.count, ref_mode, p->d_shard_rows, p->d_shard_ok, s));
-  } else {  // an empty shard (n_reps < world): nothing to time but the gather
+  } else if (!p->timing_pending) {  // an empty shard (n_reps < world): nothing to time but the gather
     std::memset(&p->timing, 0, sizeof(p->timing));
     p->pending_segments = 0;
+    p->pending_gathers = 0;
   }
-  if (!p->gather_ev[0]) {
-    SH_HIP(hipEventCreate(&p->gather_ev[0]));
-    SH_HIP(hipEventCreate(&p->gather_ev[1]));
+  while (p->gather_evs.size() < 2 * (size_t)(p->pending_gathers + 1)) {
+    hipEvent_t e;
+    SH_HIP(hipEventCreate(&e));
+    p->gather_evs.push_back(e);
   }
-  SH_HIP(hipEventRecord(p->gather_ev[0], s));
+  SH_HIP(hipEventRecord(p->gather_evs[2 * (size_t)p->pending_gathers], s));
   OB_TRY(ob::shard_pack(p->d_shard_rows, p->d_shard_ok, sh, (int)rl, nc, p->d_gather_map + rl, (int)ny, p->d_send,
                         p->d_send_ok, s));
   return OB_OK;
@@ -187,8 +189,8 @@ int shard_deliver(ob_panel* p, const Shard& sh, int world, uint64_t n_reps, doub
                   const double* own, hipStream_t s) {
   const size_t rl = (size_t)p->row_len, ny = (size_t)p->n_y;
   SH_HIP(hipSetDevice(p->ctx->device));
-  SH_HIP(hipEventRecord(p->gather_ev[1], s));
-  p->gather_timed = true;
+  SH_HIP(hipEventRecord(p->gather_evs[2 * (size_t)p->pending_gathers + 1], s));
+  p->pending_gathers += 1;
   p->timing_pending = true;  // ob_panel_sync waits on s and reads the gather's events
   p->last_stream = s;
   double* drows = rows;
@@ -418,8 +420,8 @@ void shard_free(ob_panel* p) {
   (void)hipFree(p->d_deliver_ok);
   (void)hipFree(p->d_own_rows);
   (void)hipFree(p->d_gather_map);
-  for (hipEvent_t e : p->gather_ev)
-    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : p->gather_evs) (void)hipEventDestroy(e);
+  p->gather_evs.clear();
 }
 
 }  // namespace ob

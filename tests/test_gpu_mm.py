@@ -358,3 +358,35 @@ def test_mm_degenerate_lp_reaches_the_optimum(ob, O):
                 assert c[r < -tol].sum() <= tau * c.sum() + 1e-9 and c[r > tol].sum() <= (1 - tau) * c.sum() + 1e-9
                 ties += int(np.abs(bh - betas[g, s]).max() > 1e-6)
     print(f"degenerate fits whose engine coefficients differ from the HiGHS vertex: {ties} of {4 * sims}")
+
+
+def test_mm_after_async_boot_on_a_side_stream(ob):
+    """an asynchronous boot on a user stream, followed at once by mm() on the same panel
+    (the context stream): MM rewrites the count images and flags the boot may still be reading, so
+    the engine orders it after the boot (engine_order / engine_mark). Both results must equal the
+    same calls made one after the other."""
+    import torch
+
+    d = mm_data(400_000, 15, seed=31)
+    panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"])
+    try:
+        n = 8000
+        want_rows, want_ok = panel.boot(SEED, 100, n, 0)
+        want_mm, want_mok = panel.mm(SEED, 16, QS, 0, 2)
+        dev = torch.device("cuda", 0)
+        rows = torch.empty((n, panel.row_len), dtype=torch.float64, device=dev)
+        ok = torch.empty(n, dtype=torch.uint8, device=dev)
+        side = torch.cuda.Stream(device=dev)
+        panel.boot_device(SEED, 100, n, rows.data_ptr(), ok.data_ptr(), 0, stream=side.cuda_stream)
+        got_mm, got_mok = panel.mm(SEED, 16, QS, 0, 2)  # no host sync in between
+        side.synchronize()
+        assert np.array_equal(rows.cpu().numpy(), want_rows) and np.array_equal(ok.cpu().numpy(), want_ok)
+        assert np.array_equal(got_mok, want_mok)
+        assert np.array_equal(got_mm, want_mm, equal_nan=True)
+        # and the other way round: a boot on the side stream right after mm() waits for it
+        got_mm2, _ = panel.mm(SEED, 16, QS, 2, 2)
+        panel.boot_device(SEED, 100, n, rows.data_ptr(), ok.data_ptr(), 0, stream=side.cuda_stream)
+        side.synchronize()
+        assert np.array_equal(rows.cpu().numpy(), want_rows)
+    finally:
+        panel.close()

@@ -47,10 +47,10 @@ def test_checker_flags_the_reverted_manual_a_variant():
 
 
 def test_checker_flags_a_wait_that_leaves_a_published_stage_in_flight(gram_isa):
-    """The shipped ISA with its partial waits (vmcnt(1) .. vmcnt(6): the publishing waits leave PER
-    = the wave's loads of one step in flight) widened to vmcnt(40): the stages published at a
+    """The shipped ISA with every partial wait (vmcnt(N), N > 0: the publishing waits leave the
+    wave's loads of the last steps in flight) widened to vmcnt(62): the stages published at a
     barrier are no longer guaranteed to have landed."""
-    mutated = re.sub(r"s_waitcnt vmcnt\([1-6]\)", "s_waitcnt vmcnt(40)", gram_isa)
+    mutated = re.sub(r"s_waitcnt vmcnt\([1-9][0-9]?\)", "s_waitcnt vmcnt(62)", gram_isa)
     assert mutated != gram_isa
     rules = {r for r, _, _ in C.check(C.parse(mutated, GRAM))}
     assert "dma-age" in rules
