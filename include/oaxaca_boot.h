@@ -265,6 +265,9 @@ int ob_debug_mm_betas(ob_panel* panel, uint64_t seed, int32_t simulations, uint6
    Unknown names are OB_E_INVALID. ob_tuning_build() is 1 in a -DOB_TUNING=1 build (`make tuning`),
    which also reads OB_<NAME> from the environment for options nobody set. */
 int ob_set_option(const char* name, double value);
+/* Test hook: the Heckman kernels' normal pdf and cdf (npdf_ncdf: W. J. Cody's rational erfc with
+   the pdf's exponential shared, ob_heckman.hip) on the device at z[0 .. n). */
+int ob_debug_normal(int device, const double* z, int64_t n, double* pdf, double* cdf);
 int ob_tuning_build(void);
 
 /* ---- inference (host) --------------------------------------------------------------------- */

@@ -43,6 +43,7 @@ EXPORTED = (
     "ob_boot_run_multi", "ob_debug_counts", "ob_prepared_boot_sharded", "ob_debug_gram",
     "ob_debug_gram_exceptions", "ob_panel_set_gather_columns", "ob_debug_shard_sim", "ob_debug_mm_fail",
     "ob_debug_chunks", "ob_debug_mm_betas", "ob_set_option", "ob_tuning_build",
+    "ob_debug_normal",
 )
 
 
@@ -201,6 +202,7 @@ _SIGS = {
     "ob_debug_mm_betas": (C.c_int, [_P, C.c_uint64, C.c_int32, C.c_uint64, _D, _U8]),
     "ob_set_option": (C.c_int, [C.c_char_p, C.c_double]),
     "ob_tuning_build": (C.c_int, []),
+    "ob_debug_normal": (C.c_int, [C.c_int, _D, C.c_int64, _D, _D]),
 }
 
 _lib = None

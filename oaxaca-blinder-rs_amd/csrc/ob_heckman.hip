@@ -727,3 +727,35 @@ int heckman_segment(const ob_heck_seg& a, hipStream_t s, int* iters, ob_heck_tim
 }
 
 }  // namespace ob
+
+namespace {
+__global__ void ob_normal_kernel(const double* z, int64_t n, double* pdf, double* cdf) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double p, c;
+  npdf_ncdf(z[i], p, c);
+  pdf[i] = p;
+  cdf[i] = c;
+}
+}  // namespace
+
+// Test hook (include/oaxaca_boot.h): npdf_ncdf, the probit's phi and Phi (Cody's erfc with one
+// shared exponential), evaluated on the device at z[0 .. n).
+extern "C" int ob_debug_normal(int device, const double* z, int64_t n, double* pdf, double* cdf) {
+  if (n < 0 || (n && (!z || !pdf || !cdf))) return ob::fail(OB_E_INVALID, "bad arguments");
+  if (n == 0) return OB_OK;
+  HK_OK(hipSetDevice(device));
+  double* d = nullptr;
+  HK_OK(hipMalloc(&d, sizeof(double) * 3 * (size_t)n));
+  int rc = OB_OK;
+  do {
+    if (hipMemcpy(d, z, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess) { rc = ob::fail(OB_E_HIP, "copy"); break; }
+    hipLaunchKernelGGL(ob_normal_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, d, n, d + n, d + 2 * n);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) { rc = ob::fail(OB_E_HIP, "launch"); break; }
+    if (hipMemcpy(pdf, d + n, sizeof(double) * n, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(cdf, d + 2 * n, sizeof(double) * n, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = ob::fail(OB_E_HIP, "copy back");
+  } while (0);
+  (void)hipFree(d);
+  return rc;
+}

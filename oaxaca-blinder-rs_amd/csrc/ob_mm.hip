@@ -63,13 +63,19 @@ constexpr double kPhase1Tol = 1e-4;  // phase-1 relative gap (beta_hat only cent
 constexpr int kFitStride = 16;       // phase 1 solves every 16th quantile (tau order) and the last ...
 constexpr int kFitStrideMin = 64;    // ... when a group has at least 64 simulations; the rest interpolate
 constexpr double kBandKappa = 3.5;   // band half-width in rank units: kappa sqrt(tau (1 - tau) K / m) + kBand0
-constexpr double kBand0 = 0.01;
-                                     // (OB_MM_KAPPA overrides it: a tuning knob; results do not depend on it)
+constexpr double kBand0 = 0.01;      // (options mm_kappa, mm_band0: tuning knobs)
 constexpr int kBandSamples = 4096;   // residuals per fit behind its band quantiles
-constexpr double kDelta1 = 3.0;      // phase 1 starts with 3x the shifted start's z/w offset (48 -> 36
-                                     // iterations at configs[4]) ...
-constexpr double kDelta2 = 2.0;      // ... phases 2/3 with twice phase 1's: all fits converge 3 iterations
-                                     // sooner (sweeps: profiles/r04_mm_delta.txt)
+// Start offsets of the IPM's z/w (the shifted start's 0.01 (1 + rms) offset, FS_DELTA, times dscale):
+constexpr double kDelta1 = 3.0;      // phase 1: 3x FS_DELTA (48 -> 36 iterations at configs[4])
+constexpr double kDelta2 = 2.0;      // phases 2/3 (reduced_round's a2, built from the unscaled args):
+                                     // 2x FS_DELTA, not 2x phase 1's offset; all fits converge 3
+                                     // iterations sooner (sweeps: profiles/r04_mm_delta.txt)
+// These tuning defaults (phase-1 tolerance, fit stride, band width, start offsets) move iteration
+// counts and which rows the reduction keeps, not the optimum a converged fit reaches (the sign
+// verification keeps the reduced optimum the full LP's). That holds only while every fit converges:
+// a fit pushed past kMmMaxIter is dropped like a failed solve_qr and changes the MM quantiles.
+// tests/test_gpu_fullsize.py::test_configs4_machado_mata_full_size checks that every fit of the point
+// pass and of two replicates converges at configs[4] under these defaults.
 
 enum { FS_TAU, FS_GAP, FS_OBJ, FS_MU, FS_SIGMU, FS_AP, FS_AD, FS_NACT, FS_DELTA, FS_LO, FS_HI, FS_EXT, FS_OBJFIX, kFs };
 
@@ -120,6 +126,7 @@ struct MmArgs {
   uint32_t block_lists;              // lists per (slot, chunk, fit block) (phase 2/3) instead of per chunk
   int rp;                            // X'x = b per fit (phase 2/3): primal residual in the solves
   double tol;                        // relative duality gap at convergence
+  int trace;                         // option mm_trace: device-side printf of rare events
   uint32_t* blist;                   // mm_classify_kernel output: [slot][chunk][fit block][cap]
   uint32_t* bnrows;                  // [slot][chunk][fit block]
   double *bvec, *rpv, *bhat;         // [fit][K]: b, b - X'x of the iterate, phase-1 beta (band centres)
@@ -356,8 +363,35 @@ __device__ __forceinline__ double mm_rcp(double v) {
   return fma(fma(-v, r, 1.0), r, r);
 }
 
+// The box variable x in [0, c] is stored by its distance to the nearer bound: d = x while x <= s,
+// d = -s otherwise (s = c - x, the upper slack). Both x and s then keep full relative precision
+// near either bound; derived as c - x, s lost it: a 500k-row fit whose rows sat at x = c (1 - 1e-16)
+// got s = 0 in a few rows, and the iteration's next direction turned NaN (configs[4],
+// tests/test_gpu_fullsize.py). Where the representation switches (x = s = c/2) the subtraction is
+// exact (Sterbenz).
+__device__ __forceinline__ void xs_decode(double d, double c, double& x, double& s) {
+  if (d >= 0.0) {
+    x = d;
+    s = c - d;
+  } else {
+    s = -d;
+    x = c - s;
+  }
+}
+__device__ __forceinline__ double xs_encode(double x, double s) { return x <= s ? x : -s; }
+// x += t from the precise (x, s): the smaller of the two takes the step, the other follows.
+__device__ __forceinline__ void xs_step(double x, double s, double c, double t, double& xn, double& sn) {
+  if (x <= s) {
+    xn = x + t;
+    sn = c - xn;
+  } else {
+    sn = s - t;
+    xn = c - sn;
+  }
+}
+
 // Per-row affine direction from the current state (shared by mm_affine, mm_final and the step
-// replay of mm_assemble).
+// replay of mm_assemble); xd is the stored (bound-distance) x.
 struct Affine {
   double xv, zv, wv, sv, ix, is, q, r, dxa, dza, dwa;  // ix = 1/x, is = 1/s (divisions shared)
 };
@@ -366,10 +400,9 @@ struct Affine {
 __device__ __forceinline__ Affine affine_row(double xv, double zv, double wv, double c, double y, double xb,
                                              double xd) {
   Affine f;
-  f.xv = xv;
+  xs_decode(xv, c, f.xv, f.sv);
   f.zv = zv;
   f.wv = wv;
-  f.sv = c - f.xv;
   f.r = y - xb;
   f.ix = mm_rcp(f.xv);
   f.is = mm_rcp(f.sv);
@@ -496,26 +529,32 @@ __global__ __launch_bounds__(256, K <= 16 ? 2 : 1) void mm_assemble_mfma_kernel(
               gap += c * y * y;
               obj += 1.0;
             } else {
-              double xv, zv, wv, r;
+              double xv, sv, zv, wv, r;
               if (!STEP) {
                 r = y - dots[0][j & 3];
                 zv = fmax(-r, 0.0) + delta;
                 wv = fmax(r, 0.0) + delta;
-                xv = mode == 3 ? c * wv / (zv + wv) : (1.0 - tau) * c;
+                if (mode == 3) {
+                  const double iz = c / (zv + wv);
+                  xv = wv * iz;
+                  sv = zv * iz;
+                } else {
+                  xv = (1.0 - tau) * c;
+                  sv = tau * c;
+                }
               } else {
                 const Affine f = affine_row(cx, cz, cw, c, y, dots[0][j & 3], dots[NDOT > 1 ? 1 : 0][j & 3]);
                 const double xdb = dots[NDOT > 2 ? 2 : 0][j & 3];
                 const Corrector d = corrector_row(f, xdb, sigmu);
-                xv = cx + ap * d.dx;
+                xs_step(f.xv, f.sv, c, ap * d.dx, xv, sv);
                 zv = cz + ad * d.dz;
                 wv = cw + ad * d.dw;
                 r = f.r - ad * xdb;  // y - x_i . (bprev + ad db)
               }
               const size_t si = state_at(b, e);
-              a.x[si] = xv;
+              a.x[si] = xs_encode(xv, sv);
               a.z[si] = zv;
               a.w[si] = wv;
-              const double sv = c - xv;
               q = xv * sv * mm_rcp(zv * sv + wv * xv);  // 1 / (z/x + w/s)
               qr = q * r;                          // rho_aff = r_d + w - z = y - X beta
               xq = xv;
@@ -938,16 +977,33 @@ __global__ __launch_bounds__(64) void mm_solve_affine_kernel(const MmArgs a, int
   if (rp_mode && lane < K) a.rpv[F * K + lane] = rpk;
   double* M = sm;
   double* v = sm + K * K;
-  for (int i = lane; i < K * K; i += 64) {
-    const int r = i % K, c = i / K;
-    M[i] = R[r <= c ? ob_pair_index(r, c, K) : ob_pair_index(c, r, K)];
+  // Late in a solve the weights Q = 1 / (z/x + w/s) spread over many decades and M = X'QX can lose
+  // positive definiteness in f64 (a 500k-row fit at tau 0.54 did after 114 iterations). As
+  // Clarabel does (its static regularization, 1e-8 relative), the factorization is then retried on
+  // M + delta max_i M_ii I for delta = 1e-14, 1e-12, 1e-10, 1e-8: the Newton direction becomes
+  // slightly inexact, while the step lengths, the gap and the stopping rule stay exact.
+  double dmax = 0.0;
+  for (int i = lane; i < K; i += 64) dmax = fmax(dmax, R[ob_pair_index(i, i, K)]);
+  for (int o = 32; o > 0; o >>= 1) dmax = fmax(dmax, __shfl_xor(dmax, o));
+  bool chol = false;
+  for (int attempt = 0; attempt < 5 && !chol; ++attempt) {
+    const double reg = attempt ? dmax * (attempt == 1 ? 1e-14 : attempt == 2 ? 1e-12 : attempt == 3 ? 1e-10 : 1e-8) : 0.0;
+    for (int i = lane; i < K * K; i += 64) {
+      const int r = i % K, c = i / K;
+      M[i] = R[r <= c ? ob_pair_index(r, c, K) : ob_pair_index(c, r, K)] + (r == c ? reg : 0.0);
+    }
+    __syncthreads();
+    chol = wave_cholesky(M, K, lane);
+    __syncthreads();
+  }
+  if (!chol) {  // no usable direction: accept the point at Clarabel's own Solved tolerance (1e-8), else fail
+    if (lane == 0 && a.trace)
+      printf("[mm] fit %zu: no Cholesky of M (K %d, max diag %.3e), gap %.3e obj %.6e rp %.3e\n", F, K, dmax, gap, obj, rpm);
+    if (lane == 0) a.fstat[F] = gap < 1e-8 * (1.0 + fabs(obj)) && rpm <= 1e-8 * (1.0 + bm) ? kDone : (kDone | kFailed);
+    return;
   }
   for (int i = lane; i < K; i += 64) v[i] = R[NP + i] - rpk;  // M dba = X'Q rho_aff - (b - X'x)
   __syncthreads();
-  if (!wave_cholesky(M, K, lane)) {  // the normal matrix lost rank: accept a near-optimal point
-    if (lane == 0) a.fstat[F] = gap < 1e-9 * (1.0 + fabs(obj)) && rpm <= 1e-9 * (1.0 + bm) ? kDone : (kDone | kFailed);
-    return;
-  }
   wave_chol_solve(M, K, v, lane);
   for (int i = lane; i < K * K; i += 64) a.L[F * K * K + i] = M[i];
   for (int i = lane; i < K; i += 64) a.dba[F * K + i] = v[i];
@@ -1764,7 +1820,22 @@ int ipm(const MmArgs& a, int K, int first_mode, hipStream_t s, MmStats& st) {
       const auto ts = std::chrono::steady_clock::now();
       MM_OK(hipStreamSynchronize(s));
       st.sync_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - ts).count();
-      if (trace()) fprintf(stderr, "[mm] iteration %d: %u of %zu fits active\n", it, active, n_fits);
+      if (trace()) {
+        fprintf(stderr, "[mm] iteration %d: %u of %zu fits active\n", it, active, n_fits);
+        if (active && active <= 4) {  // the last live fits: where they stand
+          std::vector<uint32_t> fst(n_fits);
+          std::vector<double> fsh(n_fits * kFs);
+          MM_OK(hipMemcpy(fst.data(), a.fstat, sizeof(uint32_t) * n_fits, hipMemcpyDeviceToHost));
+          MM_OK(hipMemcpy(fsh.data(), a.fs, sizeof(double) * n_fits * kFs, hipMemcpyDeviceToHost));
+          for (size_t f = 0; f < n_fits; ++f)
+            if ((int)(f % a.S_pad) < a.S && !(fst[f] & (kDone | kFailed))) {
+              const double* q = fsh.data() + f * kFs;
+              fprintf(stderr, "[mm]   live fit %zu tau %.5f gap %.3e obj %.6e rel %.3e mu %.3e ap %.3e ad %.3e nact %.0f\n",
+                      f, q[FS_TAU], q[FS_GAP], q[FS_OBJ], q[FS_GAP] / (1 + fabs(q[FS_OBJ])), q[FS_MU], q[FS_AP],
+                      q[FS_AD], q[FS_NACT]);
+            }
+        }
+      }
       if (active == 0) break;
     }
     pass(K, 1, a, grid, 0, s);
@@ -2124,6 +2195,7 @@ static int mm_run_impl(ob_panel* p, uint64_t seed, int sims, const double* quant
   a.stride = 1;
   a.cap = rcF;
   a.tol = kTol;
+  a.trace = trace() ? 1 : 0;
   a.blist = b.rowlist + lists_full * rcF;
   a.bnrows = b.nrows + lists_full;
   rd.list1 = b.rowlist + (lists_full + lists_blk) * rcF;

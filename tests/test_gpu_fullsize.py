@@ -172,3 +172,108 @@ def test_configs1_scale_normalized_categorical(ob, O, ref):
     _stats_close(rows, ok, orows, ook, list(range(orows.shape[1])), gap, ob, O)
     scale = np.maximum(np.abs(orows), gap)
     assert np.all(np.abs(rows - orows) <= RTOL * scale)
+
+
+def test_configs3_rif_multi_tau_full_size(ob, O):
+    """configs[3] at its size (builder.rs:711-757, rif.rs:14-88): 1M rows x 20
+    predictors, WLS, RIF outcomes at tau = 0.1, 0.5, 0.9 through the public decompose_quantiles
+    (one panel, one bootstrap for all three quantiles: K1 = 24 columns, 300 pairs, two-valued RIF
+    columns), 128 replicates. Per tau: every component's estimate / SE / CI / p vs the oracle's
+    reference algorithm on the RIF outcome (1e-6, mixed), and the result equal to a single-tau
+    decompose_quantile run bitwise."""
+    taus = (0.1, 0.5, 0.9)
+    reps = 128
+    d = O.synthetic_panel(1_000_000, 20, True)
+    na, nb = len(d["ya"]), len(d["yb"])
+    names = [f"x{j + 1}" for j in range(20)]
+    x = np.vstack([d["xa"], d["xb"]])
+    frame = {"wage": np.concatenate([d["ya"], d["yb"]]), "gender": np.array(["M"] * na + ["F"] * nb, dtype=object),
+             "w": np.concatenate([d["wa"], d["wb"]])}
+    frame.update({nm: np.ascontiguousarray(x[:, j]) for j, nm in enumerate(names)})
+
+    def builder():
+        return (ob.OaxacaBuilder(frame, "wage", "gender", "F").predictors(names).weights("w")
+                .bootstrap_reps(reps).seed(SEED))
+
+    multi = builder().decompose_quantiles(taus)
+    from test_gpu_parity import compare_results
+
+    xa, xb = O.with_intercept(d["xa"]), O.with_intercept(d["xb"])
+    cfg = O.PassConfig(21, 20, 0, True)
+    agg = O.OracleBuilder({}, "wage", "gender", "F")
+    for t, q in enumerate(taus):
+        single = builder().decompose_quantile(q)
+        for tab in ("two_fold", "three_fold"):
+            for cm, cs in zip(getattr(multi[t], tab).aggregate, getattr(single, tab).aggregate):
+                assert (cm.name, cm.estimate, cm.std_err, cm.p_value, cm.ci_lower, cm.ci_upper) == \
+                       (cs.name, cs.estimate, cs.std_err, cs.p_value, cs.ci_lower, cs.ci_upper), (q, cm.name)
+        for tab in ("detailed_explained", "detailed_unexplained"):
+            for cm, cs in zip(getattr(multi[t].two_fold, tab), getattr(single.two_fold, tab)):
+                assert (cm.estimate, cm.std_err, cm.ci_lower, cm.ci_upper) == \
+                       (cs.estimate, cs.std_err, cs.ci_lower, cs.ci_upper), (q, tab, cm.name)
+        ra, rb = O.rif(d["ya"], q), O.rif(d["yb"], q)
+        rc, point, resid = O.single_pass(cfg, xa, ra, d["wa"], xb, rb, d["wb"], residuals=True)
+        assert rc == 0
+        rows, ok = O.boot_ref(cfg, xa, ra, d["wa"], xb, rb, d["wb"], SEED, 0, reps, threads=_threads(), full=False)
+        prep = {"cfg": cfg, "detail_names": ["__ob_intercept__"] + names, "ya": ra, "yb": rb}
+        o = agg.aggregate(prep, point, rows, ok, resid)
+        compare_results(multi[t], o)
+        assert multi[t].n_failed == 0
+
+
+def _qr_objectives(x, y, c, betas, taus, block=100):
+    """sum_i c_i rho_tau(y_i - x_i beta) for every fit (quantile_regression.rs:22-129's objective)."""
+    out = np.empty(len(taus))
+    for s0 in range(0, len(taus), block):
+        r = y[:, None] - x @ betas[s0: s0 + block].T
+        t = np.asarray(taus[s0: s0 + block])[None, :]
+        out[s0: s0 + block] = (c[:, None] * np.where(r >= 0.0, t * r, (t - 1.0) * r)).sum(axis=0)
+    return out
+
+
+def test_configs4_machado_mata_full_size(ob, O):
+    """configs[4] at its size (quantile_decomposition.rs:173-279): 500k rows x 15
+    predictors, 1,000 simulations per group, 2 replicates plus the point pass.
+    * Every quantile regression converges, on the default (row-reduced) path and on the unreduced
+      solve (option mm_reduce = 0): the reference drops a fit only when Clarabel does not report
+      Solved, so a fit the engine drops would shift the simulation pairing (:238-258).
+    * The reduced optimum is the full LP's: on the point pass every fit's objective
+      sum c rho_tau(y - x beta) agrees between the two paths to 1e-11 relative (the IPM stops at a
+      1e-12 relative gap; the optimal beta itself is only determined to about 1e-6 in flat
+      directions at this size).
+    * Characteristics + coefficients = gap at every quantile, and the rows of both paths agree to
+      1e-6 of the largest value (x beta at drawn rows of those betas)."""
+    from test_gpu_mm import QS, mm_data
+
+    d = mm_data(500_000, 15, seed=45)
+    sims = 1000
+    panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"])
+    try:
+        rows, ok = panel.mm(SEED, sims, QS, 0, 2)
+        t_red = panel.timing()
+        conv = {}
+        for rep in (0xFFFFFFFF, 0, 1):  # the point pass and both replicates
+            b_r, done_r = panel.debug_mm_betas(SEED, sims, rep)
+            with ob._native.option("mm_reduce", 0):
+                b_f, done_f = panel.debug_mm_betas(SEED, sims, rep)
+            conv[rep] = (int(done_r.size - done_r.sum()), int(done_f.size - done_f.sum()))
+            if rep == 0xFFFFFFFF:
+                point = (b_r, b_f)
+        with ob._native.option("mm_reduce", 0):
+            rows0, ok0 = panel.mm(SEED, sims, QS, 0, 2)
+            t_full = panel.timing()
+    finally:
+        panel.close()
+    assert all(v == (0, 0) for v in conv.values()), conv
+    assert t_red["mm_reduced"] == 1 and t_full["mm_reduced"] == 0
+    assert ok.all() and ok0.all()
+    taus = [O.mm_tau(SEED, 0xFFFFFFFF, s) for s in range(sims)]
+    for g, (x, y) in enumerate(((d["xa"], d["ya"]), (d["xb"], d["yb"]))):
+        xi = np.hstack([np.ones((len(y), 1)), x])
+        c = np.ones(len(y))
+        o_r = _qr_objectives(xi, y, c, point[0][g], taus)
+        o_f = _qr_objectives(xi, y, c, point[1][g], taus)
+        assert np.all(np.abs(o_r - o_f) <= 1e-11 * np.abs(o_f)), np.max(np.abs(o_r - o_f) / np.abs(o_f))
+    r = rows.reshape(len(rows), len(QS), 3)
+    assert np.allclose(r[..., 1] + r[..., 2], r[..., 0], rtol=0, atol=1e-9)
+    assert np.allclose(rows, rows0, rtol=0, atol=1e-6 * np.abs(rows0).max()), np.abs(rows - rows0).max()

@@ -148,3 +148,54 @@ def test_heckman_identities_at_size(ob):
     sel = rows[:, 6 + 7 * k1:]
     assert sel.shape[1] == 4 and np.all(sel[:, 0] == 0.0)
     assert np.all(np.abs(ba[:, 1] - 2.0) < 0.1)  # the outcome slope on x survives selection
+
+
+def test_normal_pdf_cdf_device(N):
+    """npdf_ncdf (Cody's rational erfc sharing phi's exponential, the default in the
+    probit and IMR kernels) on the device over z in [-40, 40], the three CALERF regions, the
+    region edges (|x| = 0.46875, 4 with x = -z / sqrt 2) and the probit's clamp thresholds
+    (Phi = 1e-10 near z = -6.36), against the standard library's erfc and exp: the cdf to 1e-13
+    relative on |z| <= 12 (and within the exponent-rounding bound beyond), 1e-13 absolute
+    everywhere, the pdf to 1e-14 relative plus the same tail bound."""
+    import ctypes as C
+    import math
+
+    edges = [s * e * math.sqrt(2.0) for e in (0.46875, 4.0) for s in (-1, 1)]
+    z = np.concatenate([np.linspace(-40.0, 40.0, 80001), edges, np.nextafter(edges, np.inf),
+                        np.nextafter(edges, -np.inf), [-6.361340902404056, -6.3613409024040557, -5.66, 5.66]])
+    pdf, cdf = np.empty_like(z), np.empty_like(z)
+    dp = C.POINTER(C.c_double)
+    N.check(N.lib().ob_debug_normal(0, z.ctypes.data_as(dp), z.size, pdf.ctypes.data_as(dp), cdf.ctypes.data_as(dp)))
+    want_cdf = np.array([0.5 * math.erfc(-v / math.sqrt(2.0)) for v in z])
+    want_pdf = np.array([math.exp(-0.5 * v * v) / math.sqrt(2.0 * math.pi) for v in z])
+    # exp(-z^2 / 2) carries the rounding of z^2 / 2 into its exponent: |z|^2 eps relative error in
+    # both implementations, so far in the tail the bound grows with z^2 (and stays below 1e-13 on
+    # |z| <= 12, where the clamped probabilities of the probit live)
+    tol = 1e-13 + 8.0 * z * z * 2.2e-16
+    big = want_cdf > 1e-300
+    rel = np.abs(cdf[big] - want_cdf[big]) / want_cdf[big]
+    assert np.all(rel <= tol[big]), (rel.max(), z[big][np.argmax(rel - tol[big])])
+    assert np.all(rel[np.abs(z[big]) <= 12.0] <= 1e-13)
+    assert np.all(np.abs(cdf - want_cdf) <= 1e-13)
+    assert np.all(cdf[~big] <= 1e-300)
+    relp = np.abs(pdf - want_pdf) / np.maximum(want_pdf, 1e-300)
+    live = want_pdf > 1e-300
+    assert np.all(relp[live] <= 1e-14 + tol[live] - 1e-13), relp.max()
+    assert np.all((cdf >= 0.0) & (cdf <= 1.0)) and np.all(np.diff(cdf[:80001]) >= 0.0)
+
+
+@pytest.mark.parametrize("n,preds,zs,ref,weighted", CASES[1:2])
+def test_heckman_rows_match_oracle_library_erfc(ob, O, N, n, preds, zs, ref, weighted):
+    """The same parity under option hk_erfc = 0 (the library erfc beside a second exp)."""
+    f = heckman_frame(n, seed=n, weighted=weighted)
+    b, o = builders(ob, O, f, preds, zs, 64, ref, weighted)
+    want = o.run()
+    with N.option("hk_erfc", 0):
+        pr = b.prepare()
+        try:
+            rows, ok = pr.boot(0, 64)
+        finally:
+            pr.close()
+    assert (ok.astype(bool) == want["ok"].astype(bool)).all()
+    good, worst = close(rows[ok.astype(bool)], want["rows"][want["ok"].astype(bool)], want["total_gap"])
+    assert good, worst
