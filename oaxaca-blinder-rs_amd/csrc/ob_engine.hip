@@ -1016,51 +1016,64 @@ __device__ void normalize_coeffs(double* beta, const SolveArgs& a, const int32_t
   }
 }
 
-__global__ __launch_bounds__(64) void ob_solve_kernel(const SolveArgs a) {
+// One block per replicate. DUAL (two waves, when both groups' matrices fit in LDS together): wave g
+// factors group g's normal equations while the other wave factors the other group's, each with
+// wave-local synchronization; then wave 0 picks beta* (the pooled system's own factorization
+// included) and writes the row with its lanes. Otherwise one wave does the two groups in turn.
+template <bool DUAL>
+__global__ __launch_bounds__(128) void ob_solve_kernel(const SolveArgs a) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int lane = threadIdx.x;
+  __shared__ int st_sh[2];
+  const int lane = threadIdx.x & 63, w = DUAL ? (int)(threadIdx.x >> 6) : 0;
   const uint32_t rep = blockIdx.x;
   if (rep >= a.n_reps) return;
   const int k = a.k, k1 = a.k1, kp = k + 1;
-  double* M = sm;                 // kp * kp
-  double* rhs = M + kp * kp;      // kp
-  double* beta_a = rhs + kp;      // k
-  double* beta_b = beta_a + kp;   // k
-  double* xam = beta_b + kp;      // k
-  double* xbm = xam + kp;         // k
-  double* bstar = xbm + kp;       // kp (pooled before removal)
-  double* base = bstar + kp;      // 3 * n_norm: a, b, star
+  double* M = sm;                              // kp * kp (group A, then the pooled system)
+  double* M1 = M + kp * kp;                    // DUAL: k * k (group B)
+  double* rhs = M1 + (DUAL ? k * k : 0);       // kp
+  double* rhs1 = rhs + kp;                     // kp
+  double* beta_a = rhs1 + kp;                  // k
+  double* beta_b = beta_a + kp;                // k
+  double* xam = beta_b + kp;                   // k
+  double* xbm = xam + kp;                      // k
+  double* bstar = xbm + kp;                    // kp (pooled before removal)
+  double* base = bstar + kp;                   // 3 * n_norm: a, b, star
   const double* GA = a.gram + (size_t)rep * 2 * a.e_pad;
   const double* GB = GA + a.e_pad;
   double* row = a.rows + (size_t)rep * a.row_len;
   if (a.gram_out && rep == 0)
-    for (int i = lane; i < 2 * a.e_pad; i += 64) a.gram_out[i] = GA[i];
+    for (int i = threadIdx.x; i < 2 * a.e_pad; i += blockDim.x) a.gram_out[i] = GA[i];
 
-  uint8_t status = 1;
   // OLS for both groups (estimation.rs:53-54 -> ols.rs:44-144)
-  for (int g = 0; g < 2 && status == 1; ++g) {
+  int ok_g = 1;
+  for (int g = w; g < 2; g += DUAL ? 2 : 1) {
     const double* G = g ? GB : GA;
     double* beta = g ? beta_b : beta_a;
+    double* Mg = (DUAL && g) ? M1 : M;
+    double* rg = (DUAL && g) ? rhs1 : rhs;
     for (int i = lane; i < k * k; i += 64) {
       const int r = i % k, c = i / k;
-      M[r + c * k] = gpair(G, r, c, k1);
+      Mg[r + c * k] = gpair(G, r, c, k1);
     }
-    for (int i = lane; i < k; i += 64) rhs[i] = gpair(G, i, a.yc, k1);
-    __syncthreads();
-    if (!wave_cholesky(M, k, lane)) {
-      status = 0;
+    for (int i = lane; i < k; i += 64) rg[i] = gpair(G, i, a.yc, k1);
+    ob_sync<DUAL>();
+    if (!wave_cholesky<DUAL>(Mg, k, lane)) {
+      ok_g = 0;
       break;
     }
-    wave_chol_solve(M, k, rhs, lane);
+    wave_chol_solve<DUAL>(Mg, k, rg, lane);
     if (g == 1 && a.raw_beta_b && rep == 0)
-      for (int i = lane; i < k; i += 64) a.raw_beta_b[i] = rhs[i];
+      for (int i = lane; i < k; i += 64) a.raw_beta_b[i] = rg[i];
     const double sw = G[0];
     for (int i = lane; i < k; i += 64) {
-      beta[i] = rhs[i];
+      beta[i] = rg[i];
       (g ? xbm : xam)[i] = gpair(G, 0, i, k1) / sw;  // estimation.rs:56-71 (weighted or row mean)
     }
-    __syncthreads();
   }
+  if (lane == 0) st_sh[w] = ok_g;
+  __syncthreads();
+  if (w != 0) return;
+  uint8_t status = (st_sh[0] && (!DUAL || st_sh[1])) ? 1 : 0;
   const int32_t* nst = a.norm;
   const int32_t* nidx = a.norm + a.off_idx;
   const int32_t* pst = a.norm + a.off_pstart;
@@ -1075,7 +1088,7 @@ __global__ __launch_bounds__(64) void ob_solve_kernel(const SolveArgs a) {
       normalize_coeffs(beta_b, a, nst, nidx, base_b);
       for (int v = 0; v < a.n_norm; ++v) base_s[v] = 0.0;
     }
-    __syncthreads();
+    ob_sync<DUAL>();
   }
   // beta* (builder.rs:536-621)
   if (status == 1) {
@@ -1120,11 +1133,11 @@ __global__ __launch_bounds__(64) void ob_solve_kernel(const SolveArgs a) {
           rhs[u] = gpair(GA, o, a.yc, k1) + gpair(GB, o, a.yc, k1);
         }
       }
-      __syncthreads();
-      if (!wave_cholesky(M, kp, lane)) {
+      ob_sync<DUAL>();
+      if (!wave_cholesky<DUAL>(M, kp, lane)) {
         status = 0;
       } else {
-        wave_chol_solve(M, kp, rhs, lane);
+        wave_chol_solve<DUAL>(M, kp, rhs, lane);
         if (lane == 0) {
           if (a.n_norm > 0) normalize_coeffs(rhs, a, pst, pidx, base_s);
           for (int u = 0, d = 0; u < kp; ++u)
@@ -1133,29 +1146,39 @@ __global__ __launch_bounds__(64) void ob_solve_kernel(const SolveArgs a) {
       }
     }
   }
-  __syncthreads();
-  if (lane == 0) {
-    if (status != 1) {
-      for (int i = 0; i < a.row_len; ++i) row[i] = __builtin_nan("");
-    } else {
-      const int kd = k + a.n_base;
-      double* dex = row + 6;
-      double* dun = row + 6 + kd;
-      double expl = 0.0, ta = 0.0, tb = 0.0, endow = 0.0, coef = 0.0, inter = 0.0;
-      for (int j = 0; j < k; ++j) {  // decomposition.rs:56-89
-        const double dx = xam[j] - xbm[j], db = beta_a[j] - beta_b[j];
-        expl += dx * bstar[j];
-        ta += xam[j] * beta_a[j];
-        tb += xbm[j] * beta_b[j];
-        endow += dx * beta_b[j];
-        coef += xbm[j] * db;
-        inter += dx * db;
-      }
-      double unexpl = (ta - tb) - expl;
-      for (int j = 0; j < k; ++j) {  // decomposition.rs:92-122
-        dex[j] = (xam[j] - xbm[j]) * bstar[j];
-        dun[j] = xam[j] * (beta_a[j] - bstar[j]) + xbm[j] * (bstar[j] - beta_b[j]);
-      }
+  ob_sync<DUAL>();
+  if (status != 1) {
+    for (int i = lane; i < a.row_len; i += 64) row[i] = __builtin_nan("");
+  } else {
+    // decomposition.rs:56-122 with the lanes over the coefficients; the six sums by a wave reduction
+    const int kd = k + a.n_base;
+    double* dex = row + 6;
+    double* dun = row + 6 + kd;
+    double sum[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};  // explained, x_A b_A, x_B b_B, endowments, coefficients, interaction
+    double* tail = row + 6 + 2 * kd;
+    for (int j = lane; j < k; j += 64) {
+      const double xa = xam[j], xb = xbm[j], ba = beta_a[j], bb = beta_b[j], bs = bstar[j];
+      const double dx = xa - xb, db = ba - bb;
+      sum[0] += dx * bs;
+      sum[1] += xa * ba;
+      sum[2] += xb * bb;
+      sum[3] += dx * bb;
+      sum[4] += xb * db;
+      sum[5] += dx * db;
+      dex[j] = dx * bs;
+      dun[j] = xa * (ba - bs) + xb * (bs - bb);
+      tail[j] = ba;
+      tail[k + j] = bb;
+      tail[2 * k + j] = xa;
+      tail[3 * k + j] = xb;
+      tail[4 * k + j] = bs;
+    }
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) sum[q] += __shfl_xor(sum[q], off);
+    if (lane == 0) {
+      double expl = sum[0], unexpl = (sum[1] - sum[2]) - sum[0];
       for (int v = 0, bi = 0; v < a.n_norm; ++v) {  // builder.rs:634-674
         if (!has[v]) continue;
         double sa = 0.0, sb = 0.0;
@@ -1174,21 +1197,13 @@ __global__ __launch_bounds__(64) void ob_solve_kernel(const SolveArgs a) {
       }
       row[0] = expl;
       row[1] = unexpl;
-      row[2] = endow;
-      row[3] = coef;
-      row[4] = inter;
+      row[2] = sum[3];
+      row[3] = sum[4];
+      row[4] = sum[5];
       row[5] = gpair(GA, 0, a.yc, k1) / GA[0] - gpair(GB, 0, a.yc, k1) / GB[0];  // builder.rs:676-684
-      double* tail = row + 6 + 2 * kd;
-      for (int j = 0; j < k; ++j) {
-        tail[j] = beta_a[j];
-        tail[k + j] = beta_b[j];
-        tail[2 * k + j] = xam[j];
-        tail[3 * k + j] = xbm[j];
-        tail[4 * k + j] = bstar[j];
-      }
     }
-    a.ok[rep] = a.raw_status ? status : (uint8_t)(status == 1);
   }
+  if (lane == 0) a.ok[rep] = a.raw_status ? status : (uint8_t)(status == 1);
 }
 
 // y_B - X_B beta_B on the unresampled group B (ols.rs:118-119; OaxacaResults::residuals).
@@ -1354,9 +1369,24 @@ Plan make_plan(const ob_panel* p, uint64_t n_reps, bool unit) {
   return pl;
 }
 
-size_t solve_lds_bytes(const ob_panel* p) {
-  const int kp = p->k + 1;
-  return sizeof(double) * ((size_t)kp * kp + 6 * kp + 3 * (size_t)std::max(p->norm.n_norm, 1));
+size_t solve_lds_bytes_t(const ob_panel* p, bool dual) {
+  const int k = p->k, kp = k + 1;
+  return sizeof(double) * ((size_t)kp * kp + (dual ? (size_t)k * k : 0) + 7 * (size_t)kp +
+                           3 * (size_t)std::max(p->norm.n_norm, 1));
+}
+// Two waves per replicate (ob_solve_kernel<true>) while both groups' matrices fit in 64 KB of LDS.
+bool solve_dual(const ob_panel* p) { return solve_lds_bytes_t(p, true) <= 64 * 1024; }
+size_t solve_lds_bytes(const ob_panel* p) { return solve_lds_bytes_t(p, solve_dual(p)); }
+
+hipError_t launch_solve(const ob_panel* p, const SolveArgs& sa, uint32_t blocks, hipStream_t s) {
+  const bool dual = solve_dual(p);
+  const size_t lds = solve_lds_bytes(p);
+  const void* fn = dual ? (const void*)ob_solve_kernel<true> : (const void*)ob_solve_kernel<false>;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (e != hipSuccess) return e;
+  if (dual) hipLaunchKernelGGL(ob_solve_kernel<true>, dim3(blocks), dim3(128), lds, s, sa);
+  else hipLaunchKernelGGL(ob_solve_kernel<false>, dim3(blocks), dim3(64), lds, s, sa);
+  return hipGetLastError();
 }
 
 template <int CB, bool U>
@@ -1610,8 +1640,7 @@ int engine_point_estimate(ob_panel* p, int ref_mode, double* row, double* resid_
       sa.gram_out = t == 0 ? d_gout : nullptr;
       sa.raw_status = 1;
       sa.raw_beta_b = d_beta + (size_t)t * p->k;
-      hipLaunchKernelGGL(ob_solve_kernel, dim3(1), dim3(64), solve_lds_bytes(p), s, sa);
-      PE_OK(hipGetLastError());
+      PE_OK(launch_solve(p, sa, 1, s));
     }
     uint8_t okh = 0;
     std::vector<double> gout(2 * p->e_pad);
@@ -1759,6 +1788,7 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   const int l1_diag = ob::opt_int(ob::Opt::L1Diag, 0) & 31;
   const L1Kernel l1k = l1_diag == 0    ? ob_level1_kernel<0>
                        : l1_diag == 1  ? ob_level1_kernel<1>
+                       : l1_diag == 2  ? ob_level1_kernel<2>
                        : l1_diag == 3  ? ob_level1_kernel<3>
                        : l1_diag == 11 ? ob_level1_kernel<11>
                        : l1_diag == 16 ? ob_level1_kernel<16>
@@ -1768,8 +1798,6 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   const L1Kernel l1k = ob_level1_kernel<0>;
 #endif
   HIP_OK(hipFuncSetAttribute((const void*)l1k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_l1));
-  HIP_OK(hipFuncSetAttribute((const void*)ob_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)solve_lds_bytes(p)));
   p->timing.chunks = nch;
   p->timing.blocks = use_i8 ? (int32_t)((uint32_t)nch * ((pl.nb_rep + 3) / 4) * (uint32_t)p->oz_n_ct)
                             : (int32_t)(pl.nb_rep * pl.n_cg * (uint32_t)nch);
@@ -1849,8 +1877,7 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
       sa.gram_out = nullptr;
       sa.raw_beta_b = nullptr;
       sa.raw_status = 0;
-      hipLaunchKernelGGL(ob_solve_kernel, dim3(ns), dim3(64), solve_lds_bytes(p), s, sa);
-      HIP_OK(hipGetLastError());
+      HIP_OK(launch_solve(p, sa, ns, s));
     }
     if (timed) HIP_OK(hipEventRecord(ev[5], s));
     p->timing.gram_launches += 1;
