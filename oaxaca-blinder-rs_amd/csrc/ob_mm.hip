@@ -369,25 +369,23 @@ __device__ __forceinline__ double mm_rcp(double v) {
 // got s = 0 in a few rows, and the iteration's next direction turned NaN (configs[4],
 // tests/test_gpu_fullsize.py). Where the representation switches (x = s = c/2) the subtraction is
 // exact (Sterbenz).
-__device__ __forceinline__ void xs_decode(double d, double c, double& x, double& s) {
-  if (d >= 0.0) {
-    x = d;
-    s = c - d;
-  } else {
-    s = -d;
-    x = c - s;
-  }
+// (By value, with selects: the by-reference form left the assemble pass's x, s in a stack slot.)
+struct XS {
+  double x, s;
+};
+__device__ __forceinline__ XS xs_decode(double d, double c) {
+  const bool lo = d >= 0.0;
+  const double m = lo ? d : -d;  // the precise one
+  const double o = c - m;
+  return {lo ? m : o, lo ? o : m};
 }
-__device__ __forceinline__ double xs_encode(double x, double s) { return x <= s ? x : -s; }
+__device__ __forceinline__ double xs_encode(XS v) { return v.x <= v.s ? v.x : -v.s; }
 // x += t from the precise (x, s): the smaller of the two takes the step, the other follows.
-__device__ __forceinline__ void xs_step(double x, double s, double c, double t, double& xn, double& sn) {
-  if (x <= s) {
-    xn = x + t;
-    sn = c - xn;
-  } else {
-    sn = s - t;
-    xn = c - sn;
-  }
+__device__ __forceinline__ XS xs_step(XS v, double c, double t) {
+  const bool lo = v.x <= v.s;
+  const double m = lo ? v.x + t : v.s - t;
+  const double o = c - m;
+  return {lo ? m : o, lo ? o : m};
 }
 
 // Per-row affine direction from the current state (shared by mm_affine, mm_final and the step
@@ -400,7 +398,9 @@ struct Affine {
 __device__ __forceinline__ Affine affine_row(double xv, double zv, double wv, double c, double y, double xb,
                                              double xd) {
   Affine f;
-  xs_decode(xv, c, f.xv, f.sv);
+  const XS v = xs_decode(xv, c);
+  f.xv = v.x;
+  f.sv = v.s;
   f.zv = zv;
   f.wv = wv;
   f.r = y - xb;
@@ -546,13 +546,15 @@ __global__ __launch_bounds__(256, K <= 16 ? 2 : 1) void mm_assemble_mfma_kernel(
                 const Affine f = affine_row(cx, cz, cw, c, y, dots[0][j & 3], dots[NDOT > 1 ? 1 : 0][j & 3]);
                 const double xdb = dots[NDOT > 2 ? 2 : 0][j & 3];
                 const Corrector d = corrector_row(f, xdb, sigmu);
-                xs_step(f.xv, f.sv, c, ap * d.dx, xv, sv);
+                const XS v = xs_step({f.xv, f.sv}, c, ap * d.dx);
+                xv = v.x;
+                sv = v.s;
                 zv = cz + ad * d.dz;
                 wv = cw + ad * d.dw;
                 r = f.r - ad * xdb;  // y - x_i . (bprev + ad db)
               }
               const size_t si = state_at(b, e);
-              a.x[si] = xs_encode(xv, sv);
+              a.x[si] = xs_encode({xv, sv});
               a.z[si] = zv;
               a.w[si] = wv;
               q = xv * sv * mm_rcp(zv * sv + wv * xv);  // 1 / (z/x + w/s)
