@@ -119,7 +119,7 @@ __host__ __device__ inline uint32_t l1_lds_words(uint32_t ntiles) {
 }
 
 // OBRS-2 split on the device (ob_spec.h; oracle orc_split_left). The hot columns of every table
-// live in LDS, so a walk that ends within OB_KY_HOT columns of its first (p > 0.9999) makes no
+// live in LDS, so a walk that ends within OB_KY_HOT columns of its first (p > 0.99) makes no
 // global access; deeper columns read the global tables.
 struct KyLds {
   uint32_t i0[OB_KY_TABLES], obase[OB_KY_TABLES], lbase[OB_KY_TABLES];
@@ -177,7 +177,7 @@ __device__ __forceinline__ uint32_t l1_split_item(uint32_t q, uint32_t c, uint32
 // DIAG (OB_L1_DIAG, timing ablations only, wrong counts): 1 no random bits (left = c / 2),
 // 2 one round only, 4 no Knuth-Yao staging, 8 no m1 stores, 16 return after the staging barrier.
 template <int DIAG>
-__global__ __launch_bounds__(kBlock) void ob_level1_kernel(uint32_t n0, uint32_t n1, uint32_t tiles0,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void ob_level1_kernel(uint32_t n0, uint32_t n1, uint32_t tiles0,
                                                            uint32_t first_rep, uint32_t stride,
                                                            uint32_t key0, uint32_t key1, uint32_t* m1,
                                                            const ob_ky_tables ky_g) {

@@ -117,8 +117,8 @@ OB_HD ob_u32x4 ob_philox_x3(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, 
 #define OB_KY_MIN_LOG 7
 #define OB_KY_MAX_LOG 12
 #define OB_KY_TABLES (OB_KY_MAX_LOG - OB_KY_MIN_LOG + 1)
-#define OB_KY_HOT 16        // columns i0 .. i0 + 15 of each table staged in LDS: a walk ends there with p > 0.9999
-#define OB_KY_HOT_CAP 5120  // their entries, all tables (4,996 at OB_KY_HOT = 16)
+#define OB_KY_HOT 9         // columns i0 .. i0 + 8 of each table staged in LDS: a walk ends there with p > 0.99
+#define OB_KY_HOT_CAP 2192  // their entries, all tables (2,186 at OB_KY_HOT = 9)
 
 // The tables on the device (built once per process, ob_engine.hip ky_host): table t (n = 2^(t + 7))
 // has n + 2 column offsets at off + off_base[t] (positions in its own list) and its list at
