@@ -4,7 +4,7 @@
 Workload = BASELINE.json configs[1]: a 1,000,000-row two-group panel (500k/500k) with 20 numeric
 predictors, two-fold WLS decomposition (builder default reference coefficients GroupA), 10,000
 bootstrap replicates per step. One step = one full bootstrap run with the panel already
-resident in HBM: OBRS-2 resampling + Gram + solves + OB terms for every replicate (HIP), the
+resident in HBM: OBRS-3 resampling + Gram + solves + OB terms for every replicate (HIP), the
 RCCL all-gather of the per-replicate component columns over xGMI (N > 1), and the SE/p/CI aggregation of
 every reported component on rank 0 (builder.rs:841-930). On N > 1 GPUs the default is configs[2]:
 the 10,000 replicates of a step are sharded over the ranks (strong scaling); --weak gives each rank
@@ -226,7 +226,7 @@ def bench_mm(args, world, rank, local, dist):
         "metric": "Machado-Mata bootstrap replicates/sec (configs[4]: 1000 QR draws per group per replicate)",
         "value": value, "unit": "replicates/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "f64", "data": "synthetic (SURVEY.md §8d wage panel, numpy seed 20260424; OBRS-2/MM-1 seed 0x0B5EED)",
+        "dtype": "f64", "data": "synthetic (SURVEY.md §8d wage panel, numpy seed 20260424; OBRS-3/MM-1 seed 0x0B5EED)",
         "config": {"workload": "configs[4]: Machado-Mata, 1000 simulations, quantiles 0.1/0.25/0.5/0.75/0.9",
                    "rows": args.rows, "predictors": args.preds, "simulations": args.sims,
                    "replicates_per_gpu_per_step": R, "parallelism": f"replicates sharded x{world}, RCCL all-gather"},
@@ -754,7 +754,7 @@ def main():
             "scaling": mode,
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (SURVEY.md §8d wage panel, numpy seed 20260424; OBRS-2 bootstrap seed 0x0B5EED)",
+            "data": "synthetic (SURVEY.md §8d wage panel, numpy seed 20260424; OBRS-3 bootstrap seed 0x0B5EED)",
             "config": {"workload": workload_label(mode, taus, total, world, per_rank),
                        "rows": args.rows, "predictors": args.preds, "weighted": weighted,
                        "replicates_per_step": total, "replicates_per_gpu_per_step": per_rank,

@@ -131,7 +131,7 @@ int ob_panel_n_y(const ob_panel* panel);
    With n_y outcomes: row holds n_y x row_len, resid_b n_y x n_b (outcome-major). */
 int ob_point_estimate(ob_panel* panel, int ref_mode, double* row, double* resid_b);
 
-/* Bootstrap replicates [first_rep, first_rep + n_reps) of the OBRS-2 stream keyed by seed.
+/* Bootstrap replicates [first_rep, first_rep + n_reps) of the OBRS-3 stream keyed by seed.
    rows: n_reps x ob_panel_row_len(); ok[r] = 0 marks a replicate the reference would drop
    (filter_map + .ok(), builder.rs:816-839): Cholesky failure or zero total weight. Results are
    a pure function of (seed, replicate id): identical on 1 or 8 GPUs. With n_y outcomes rows
@@ -228,7 +228,7 @@ int ob_panel_set_gather_columns(ob_panel* panel, const int32_t* cols, int32_t n)
 int ob_debug_shard_sim(ob_panel* panel, int world, int self_rank, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
                        int ref_mode, double* rows, uint8_t* ok);
 
-/* ---- test hook: the OBRS-2 resample counts themselves (bitwise parity, builder.rs:822-827) ----
+/* ---- test hook: the OBRS-3 resample counts themselves (bitwise parity, builder.rs:822-827) ----
  * For replicates [first_rep, first_rep + n_reps) of `group` (0 = A, 1 = B): level1 receives
  * n_reps x ceil(n_g / 256) tile counts and row_counts n_reps x n_g per-row draw counts, exactly
  * as the Gram kernel consumes them. Either output may be NULL. */
@@ -403,7 +403,7 @@ void ob_matrices_free(ob_matrices* m);
  * quantiles (csrc/ob_spec.h; the reference draws from an unseeded thread_rng), one MM-1 row pick
  * per group per successful simulation, predictions x_A b_A, x_B b_B, x_A b_B, and empirical
  * quantiles. Each QR (math/quantile_regression.rs:22-129, Clarabel LP) is solved on the GPU by an
- * interior-point method on its dual LP; the replicates are OBRS-2 resamples. */
+ * interior-point method on its dual LP; the replicates are OBRS-3 resamples. */
 
 /* Runs the point pass (every row once; with_point != 0) then one pass per replicate of
    [first_rep, first_rep + n_reps). rows: (with_point + n_reps) x 3 n_quantiles host doubles,

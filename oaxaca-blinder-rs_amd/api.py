@@ -280,7 +280,7 @@ class OaxacaBuilder:
         return self
 
     def seed(self, seed: int | None):
-        """Extension: fix the OBRS-2 stream (the reference is unseeded; None = fresh entropy)."""
+        """Extension: fix the OBRS-3 stream (the reference is unseeded; None = fresh entropy)."""
         self._seed = None if seed is None else int(seed) & ((1 << 64) - 1)
         return self
 

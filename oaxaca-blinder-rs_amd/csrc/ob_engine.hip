@@ -1,4 +1,4 @@
-// ob_engine.hip -- the MI355X bootstrap engine: OBRS-2 resampling + X^T diag(c w) X on f64 MFMA
+// ob_engine.hip -- the MI355X bootstrap engine: OBRS-3 resampling + X^T diag(c w) X on f64 MFMA
 // + wave-parallel Cholesky solves + Oaxaca-Blinder algebra, all resident in HBM.
 //
 // Replaces, per replicate, builder.rs:816-839 (polars resample + vstack + run_single_pass):
@@ -84,7 +84,7 @@ struct GramArgs {
 };
 
 // ---------------------------------------------------------------------------------------------
-// Level 1: tile counts m_j for one (replicate, group) by binomial splitting (OBRS-2, ob_spec.h:
+// Level 1: tile counts m_j for one (replicate, group) by binomial splitting (OBRS-3, ob_spec.h:
 // popcounts below 4096 draws, Knuth-Yao samples above; oracle orc_level1_counts). Level l of the
 // dyadic tile tree lives in LDS buffer (D - l) & 1.
 // Levels l < 8 have at most 2^l nodes and give each 256 >> l threads (popcounts summed by LDS
@@ -335,11 +335,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
   // ordering a block on one CU needs. A device-scope __threadfence() here compiled to an L2
   // write-back and invalidate per block (buffer_wbl2 / buffer_inv): 1.6 of the kernel's 3.4 ms.
   __syncthreads();
-  if (tid < todo) {  // direct draws: Lemire over [0, n)
+  for (uint32_t r = tid; r < todo; r += kBlock) {  // direct draws: Lemire over [0, n)
     const uint32_t thresh = (0u - n) % n;
     uint64_t x;
     for (uint32_t j = 0;; ++j) {
-      const ob_u32x4 u = ob_philox(tid, rep, g, OB_TAG_L1D + (j >> 2), key0, key1);
+      const ob_u32x4 u = ob_philox(r, rep, g, OB_TAG_L1D + (j >> 2), key0, key1);
       const uint32_t wd[4] = {u.x, u.y, u.z, u.w};
       x = (uint64_t)wd[j & 3] * n;
       if ((uint32_t)x >= thresh) break;
@@ -1676,7 +1676,7 @@ int engine_point_estimate(ob_panel* p, int ref_mode, double* row, double* resid_
   return rc;
 }
 
-// OBRS-2 resample counts for replicates [first_rep, first_rep + n_reps) without the Gram: level-1
+// OBRS-3 resample counts for replicates [first_rep, first_rep + n_reps) without the Gram: level-1
 // tile counts into d_m1 ([replicate][tile]) and the level-2 count images into d_counts (the
 // ob_engine.hpp layout, replicate batches of 64). Used by the Machado-Mata driver (ob_mm.hip).
 int engine_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_reps, hipStream_t s,
@@ -1684,7 +1684,7 @@ int engine_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_rep
   HIP_OK(hipSetDevice(p->ctx->device));
   if (n_reps == 0) return OB_OK;
   if (first_rep + n_reps > 0xFFFFFFFFull)
-    return ob::fail(OB_E_INVALID, "replicate ids must stay below 2^32 - 1 (OBRS-2 / MM-1 counter word)");
+    return ob::fail(OB_E_INVALID, "replicate ids must stay below 2^32 - 1 (OBRS-3 / MM-1 counter word)");
   const uint32_t tiles = p->ntiles[0] + p->ntiles[1];
   Plan pl = make_plan(p, n_reps, false);
   OB_TRY(ensure_buf(&p->d_m1, p->cap_m1, (size_t)tiles * pl.rep_pad));
@@ -1734,7 +1734,7 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   HIP_OK(hipSetDevice(ctx->device));
   if (n_reps == 0) return OB_OK;
   if (first_rep + n_reps > 0x100000000ull)
-    return ob::fail(OB_E_INVALID, "replicate ids must stay below 2^32 (OBRS-2 counter word)");
+    return ob::fail(OB_E_INVALID, "replicate ids must stay below 2^32 (OBRS-3 counter word)");
   hipStream_t s = stream ? stream : ctx->stream;
   OB_TRY(engine_order(p, s));  // a previous call on another stream (the digit images, scratch buffers)
   const uint32_t tiles = p->ntiles[0] + p->ntiles[1];

@@ -145,7 +145,7 @@ int ob_aggregate(const double* rows, const uint8_t* ok, uint64_t n_reps, int32_t
 
 const char* ob_last_error(void) { return ob::last_error().c_str(); }
 
-const char* ob_version(void) { return "oaxaca-boot-mi355x 0.1.0 (gfx950, OBRS-2)"; }
+const char* ob_version(void) { return "oaxaca-boot-mi355x 0.2.0 (gfx950, OBRS-3)"; }
 
 int ob_bootstrap_stats(const double* estimates, int64_t n, double point_estimate, double out[4]) {
   (void)point_estimate;  // unused by the reference too (inference.rs:4)

@@ -2236,7 +2236,7 @@ static int mm_run_impl(ob_panel* p, uint64_t seed, int sims, const double* quant
     OB_TRY(run_batch(pa, K, s, rows, ok, st, rd));
     out = 1;
   }
-  // resamples: OBRS-2 count images per segment, then batches of rb_cap slots
+  // resamples: OBRS-3 count images per segment, then batches of rb_cap slots
   const uint64_t seg_cap = 4096;
   for (uint64_t s0 = 0; s0 < n_reps; s0 += seg_cap) {
     const uint32_t ns = (uint32_t)std::min<uint64_t>(seg_cap, n_reps - s0);

@@ -10,7 +10,7 @@ constexpr int kMmMaxK = 32;      // intercept + predictors (LDS row stride 34, t
 constexpr int kMmMaxSims = 4096;  // simulations per pass (LDS sort in the finish kernel)
 constexpr int kMmMaxIter = 200;   // IPM iterations per fit (Clarabel's default max_iter)
 
-// One MM pass per replicate of [first_rep, first_rep + n_reps) (OBRS-2 resamples), preceded by
+// One MM pass per replicate of [first_rep, first_rep + n_reps) (OBRS-3 resamples), preceded by
 // the point estimate (every row once, MM-1 replicate OB_MM_POINT_REP) when with_point. Rows:
 // [gap, characteristics, coefficients] per quantile, the point row first; ok[r] = 1 where the
 // pass succeeded (quantile_decomposition.rs:231-236 failure otherwise). Host buffers.

@@ -1,7 +1,7 @@
 // ob_shard.cpp -- replicates sharded over GPUs with one RCCL all-gather of the per-replicate rows
 // (replaces the Rayon `into_par_iter` of builder.rs:816-839 across devices).
 //
-// A replicate's row is a pure function of (seed, replicate id) and the panel (OBRS-2 counters are
+// A replicate's row is a pure function of (seed, replicate id) and the panel (OBRS-3 counters are
 // global replicate ids; the chunking depends on the panel only), so rank r simply runs replicate
 // ids [first + r*per, first + (r+1)*per) on its own GPU and the gathered rows equal a one-GPU run
 // bit for bit. The only collective is ncclAllGather over xGMI: (n_y x per x row_len) f64 plus

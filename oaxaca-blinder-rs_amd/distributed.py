@@ -2,7 +2,7 @@
 per-replicate rows -- the only collective the bootstrap needs.
 
 The reference runs every replicate in one process on a Rayon pool (builder.rs:816-839).
-Here rank r computes replicate ids [r*per, (r+1)*per) of the OBRS-2 stream (results are a pure
+Here rank r computes replicate ids [r*per, (r+1)*per) of the OBRS-3 stream (results are a pure
 function of (seed, replicate id), so the gathered rows equal a single-GPU run bit for bit), the
 rows are all-gathered, and rank 0 aggregates (builder.rs:841-950). Two gathers exist:
 

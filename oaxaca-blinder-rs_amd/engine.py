@@ -149,7 +149,7 @@ class Panel:
                                                    C.c_void_p(rows_ptr), C.c_void_p(ok_ptr), C.c_void_p(stream or 0)))
 
     def debug_counts(self, seed: int, first_rep: int, n_reps: int, group: int):
-        """OBRS-2 counts as the Gram kernel consumes them (ob_debug_counts): (level-1 tile counts
+        """OBRS-3 counts as the Gram kernel consumes them (ob_debug_counts): (level-1 tile counts
         [n_reps, tiles], per-row counts [n_reps, n_g] uint8)."""
         ng = self.n_a if group == 0 else self.n_b
         tiles = -(-ng // 256)

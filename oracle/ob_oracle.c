@@ -58,7 +58,7 @@ static inline uint64_t orc_draw_u64(const uint32_t w[4], int odd) {
     return odd ? (((uint64_t)w[3] << 32) | w[2]) : (((uint64_t)w[1] << 32) | w[0]);
 }
 
-/* Level 1 (OBRS-2): the tile counts m of n i.i.d. uniform row draws over [0, n),
+/* Level 1 (OBRS-3): the tile counts m of n i.i.d. uniform row draws over [0, n),
  * drawn by binomial splitting instead of one index per draw. T = ceil(n / 256) tiles, D =
  * ceil(log2 T); the dyadic tree over 2^D tiles (rows [0, 2^(D+8))) has node (l, k) = tiles
  * [k 2^(D-l), (k+1) 2^(D-l)). A round with c_0 draws at the root splits every node (l < D) with
@@ -66,9 +66,10 @@ static inline uint64_t orc_draw_u64(const uint32_t w[4], int odd) {
  * A child starting at tile >= T is padding: its draws are rejected. At the tiles, a partial last
  * tile (S = n - 256 (T-1) < 256 rows) accepts draw i iff byte (i & 3) of word ((i >> 2) & 3) of
  * Philox({i >> 4, rep, g, ORC_TAG_L1S + round}) is < S. Rejected draws R start the next round
- * while R > 256; the last R <= 256 are direct: draw r is Lemire's multiply-and-reject on word
- * (j & 3) of Philox({r, rep, g, ORC_TAG_L1D + (j >> 2)}), attempt j. Each split is an exact
- * Binomial(c, 1/2), so the accepted draws are i.i.d. uniform over the valid rows.
+ * while R > 2048; the last R <= 2048 (OBRS-2: 256) are direct: draw r is Lemire's
+ * multiply-and-reject on word (j & 3) of Philox({r, rep, g, ORC_TAG_L1D + (j >> 2)}), attempt j.
+ * Each split is an exact Binomial(c, 1/2), so the accepted draws are i.i.d. uniform over the valid
+ * rows.
  *
  * The split (OBRS-2): a node with c < 4096 draws takes OBRS-1's popcount of c fair bits (bit b =
  * bit (b & 31) of word ((b >> 5) & 3) of Philox({b >> 7, rep, (k << 1) | g, ORC_TAG_L1T + rl}),
@@ -86,7 +87,7 @@ static inline uint64_t orc_draw_u64(const uint32_t w[4], int odd) {
 #define ORC_TAG_L1K 0x4B310000u /* OBRS-2 "K1" + (round << 5) + level */
 #define ORC_TAG_L1S 0x4C530000u /* "LS" + round */
 #define ORC_TAG_L1D 0x4C440000u /* "LD" + (j >> 2) */
-#define ORC_L1_DIRECT 256u
+#define ORC_L1_DIRECT 2048u
 
 /* Knuth-Yao tables for B(n, 1/2), n = 2^j: W_k = C(n, k), p_k = W_k / 2^n; column i (1..n) of the
  * DDG tree holds the k whose bit n - i of W_k is set, ascending: list[off[i] .. off[i+1]). */

@@ -4,7 +4,7 @@ Imported by tests/, ``__graft_entry__.smoke()`` and bench.py's ``cpu_baseline`` 
 there, as the checker. The product package never imports it.
 
 Two layers:
-* ``liboboracle.so`` (ob_oracle.c): Philox/OBRS-2 resampling, ols() with nalgebra's Cholesky
+* ``liboboracle.so`` (ob_oracle.c): Philox/OBRS-3 resampling, ols() with nalgebra's Cholesky
   order, run_single_pass, the reference-algorithm bootstrap driver (gather every column, full
   X^T X per replicate, Rayon-like threads), bootstrap_stats, RIF.
 * ``OracleBuilder`` below: builder.rs's frame logic (clean_dataframe, create_dummies_manual,
@@ -13,7 +13,7 @@ Two layers:
 
 Pinning: tests/test_oracle_kat.py checks this restatement against every known-answer test the
 reference holds for the path. Bootstrap SE/CI/p parity is defined on the shared
-OBRS-2 stream (the reference's resampling is unseeded, builder.rs:822-827).
+OBRS-3 stream (the reference's resampling is unseeded, builder.rs:822-827).
 """
 from __future__ import annotations
 
@@ -165,7 +165,7 @@ def single_pass(cfg: PassConfig, xa, ya, wa, xb, yb, wb, residuals=False):
 
 
 def boot_ref(cfg: PassConfig, xa, ya, wa, xb, yb, wb, seed, first_rep, n_reps, threads=None, full=True):
-    """Reference-algorithm bootstrap (builder.rs:816-839) on the OBRS-2 stream -> (rows, ok)."""
+    """Reference-algorithm bootstrap (builder.rs:816-839) on the OBRS-3 stream -> (rows, ok)."""
     xa, xb = np.asfortranarray(xa, dtype=np.float64), np.asfortranarray(xb, dtype=np.float64)
     ya, yb = np.ascontiguousarray(ya, dtype=np.float64), np.ascontiguousarray(yb, dtype=np.float64)
     wa = None if wa is None else np.ascontiguousarray(wa, dtype=np.float64)
@@ -385,7 +385,7 @@ class OracleBuilder:
 
     def run_heckman(self):
         """run() with .heckman_selection(): every pass through heckman_single_pass, replicates
-        gathered by the OBRS-2 index stream."""
+        gathered by the OBRS-3 index stream."""
         df, dummy_names, _, _ = self._stage()
         ia, ib, _ = self.split_groups(df)
         if not ia or not ib:

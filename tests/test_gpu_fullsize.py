@@ -2,7 +2,7 @@
 
 * configs[1] (1M rows x 20 predictors, WLS; GroupA and Pooled): SE / p / CI of every reported
   component over 256 replicates (inference.rs:4-34 over builder.rs:816-839's replicates) vs the
-  oracle's reference algorithm on the same OBRS-2 stream, within 1e-6 (mixed tolerance).
+  oracle's reference algorithm on the same OBRS-3 stream, within 1e-6 (mixed tolerance).
 * configs[0] (the CLI mean path, main.rs:161-232): a 10k-row x 5-predictor CSV written here,
   read back through ob.read_csv (the LazyCsvReader stand-in), OaxacaBuilder.run() with 200
   unweighted replicates vs OracleBuilder on an independent parse of the same file.

@@ -1,7 +1,7 @@
 """The exact integer-sliced Gram (ob_gram_i8.hip) against the f64 MFMA Gram (ob_gram_kernel).
 
 Both compute G_r = sum_i c_ri v_i v_i^T (v = sqrt(w) [1, x, y], ols.rs:68-78) for the same
-OBRS-2 counts. The i8 path's only approximation is the 54-bit fixed-point split of each pair
+OBRS-3 counts. The i8 path's only approximation is the 54-bit fixed-point split of each pair
 product relative to its chunk's power of two (rounding <= 2^-55 of the chunk's largest regular
 |P| per row); rows whose magnitude dwarfs their chunk's ("exception rows": some |v_c| >= 2^B x
 the chunk's geometric-mean scale of column c, or non-finite) are summed in f64 instead

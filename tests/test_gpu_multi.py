@@ -1,6 +1,6 @@
 """Multi-GPU path and the resample counts themselves, on the MI355X.
 
-* OBRS-2 counts (builder.rs:822-827, polars sample_n_literal): the level-1 tile counts and the
+* OBRS-3 counts (builder.rs:822-827, polars sample_n_literal): the level-1 tile counts and the
   per-row count images the Gram kernel consumes (ob_debug_counts) must equal the oracle's
   restatement bit for bit -- np.bincount of oracle.resample_indices -- not only through rows.
 * The engine's RCCL path (ob_ctx_create_rank + ob_boot_run_sharded[_device], ob_boot_run_multi,

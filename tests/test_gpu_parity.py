@@ -1,4 +1,4 @@
-"""Parity of the HIP engine (through the C ABI) with the oracle on the same OBRS-2 stream.
+"""Parity of the HIP engine (through the C ABI) with the oracle on the same OBRS-3 stream.
 
 Tolerance (SURVEY.md §8c, f64 throughout): |engine - oracle| <= 1e-6 * max(|oracle|, |total_gap|)
 element-wise; observed differences are ~1e-9 relative (summation order only). Failure masks
@@ -220,7 +220,7 @@ def test_decompose_quantile_matches_oracle(ob, O):
 @pytest.mark.parametrize("weighted,ref", [(False, 1), (True, 2), (True, 0)])
 def test_decompose_quantiles_multi_tau(ob, O, weighted, ref):
     """one run serves several quantiles; each equals the single-quantile
-    run bitwise (same OBRS-2 stream, same per-pair MFMA columns) and the oracle within tolerance."""
+    run bitwise (same OBRS-3 stream, same per-pair MFMA columns) and the oracle within tolerance."""
     f = synthetic_frame(4000, seed=21, weighted=weighted)
     taus = (0.1, 0.5, 0.9)
 

@@ -224,7 +224,7 @@ def test_obrs2_split_is_binomial(O, c):
 
 
 def test_resample_is_multinomial(O):
-    """OBRS-2 draws: exact count n per replicate and a uniform per-row law (chi-square)."""
+    """OBRS-3 draws: exact count n per replicate and a uniform per-row law (chi-square)."""
     n = 1500
     tot = np.zeros(n)
     for rep in range(200):
