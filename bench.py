@@ -219,6 +219,7 @@ def bench_mm(args, world, rank, local, dist):
         return
     k = args.preds + 1
     bytes_row = 48.0  # mm_assemble per live (fit, row): x, z, w read, x, z, w written (direction replayed)
+    pmc = load_mm_pmc(args.rows, args.preds, args.sims, R)
     flops_row = 2.0 * (k * (k + 1) / 2 + 4 * k)  # X'QX pairs, X'Q r, x.bprev, x.dba, x.db
     gbps = fit_rows * bytes_row / (asm_ms * 1e-3) / 1e9
     value = world * R * args.steps / elapsed
@@ -231,7 +232,13 @@ def bench_mm(args, world, rank, local, dist):
                    "rows": args.rows, "predictors": args.preds, "simulations": args.sims,
                    "replicates_per_gpu_per_step": R, "parallelism": f"replicates sharded x{world}, RCCL all-gather"},
         "roofline": {"bound": "hbm", "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": gbps / HBM_PEAK_GBPS, "traffic": None, "kernel": "mm_assemble_mfma_kernel<16, true>",
+                     "frac": gbps / HBM_PEAK_GBPS,
+                     "traffic": pmc["bytes_per_live_fit_row"] * fit_rows / args.steps if pmc else None,
+                     "traffic_unit": "HBM bytes per step over the step's mm_assemble launches (PMC bytes per live "
+                                     "fit-row x this run's live fit-rows)",
+                     "traffic_source": "profiles/pmc_mm.json (FETCH_SIZE + WRITE_SIZE, 8-B loads calibrated on "
+                                       "the affine pass)" if pmc else None,
+                     "kernel": "mm_assemble_mfma_kernel<16, true>",
                      "assemble_ms": asm_ms, "live_fit_rows": fit_rows, "bytes_per_fit_row": bytes_row,
                      "tflops": fit_rows * flops_row / (asm_ms * 1e-3) / 1e12, "max_ipm_iterations": iters},
     }
@@ -376,6 +383,19 @@ def cpu_baseline_heckman(frame, names, zs, target_s, threads):
     return {"value": n / dt, "unit": "replicates/s", **host_info(threads), "kind": "port",
             "sample": f"{n} replicates of the same panel through oracle.heckman_single_pass (numpy), "
                       f"{threads} threads, {dt:.1f} s"}
+
+
+def load_mm_pmc(rows, preds, sims, reps):
+    """mm_assemble's measured HBM bytes per live (fit, row) from the committed PMC summary
+    (tools/gpu_r5_mm.sh -> profiles/pmc_mm.json), when it was taken at this shape."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_mm.json")) as f:
+            j = json.load(f)
+        if (j.get("rows"), j.get("predictors"), j.get("simulations"), j.get("replicates")) == (rows, preds, sims, reps):
+            return j["kernels"]["mm_assemble_mfma_kernel<16, true>"]
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
 
 
 def load_probit_pmc(rows, preds, reps, ks):
