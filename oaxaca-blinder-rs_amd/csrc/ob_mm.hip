@@ -187,8 +187,17 @@ struct Xs {
   static constexpr int NXB = (K + 15) / 16;           // 16-column blocks of X' v products
 };
 constexpr int kSub = 64;    // list rows per staged sub-tile (16 wave steps of 4 rows)
-constexpr int kRing = 4;    // wave steps of state in flight (affine / final)
-constexpr int kRingA = 4;   // the same for the assemble pass (its fragments sit in LDS to make room)
+#ifndef OB_MM_RING
+#define OB_MM_RING 4
+#endif
+#ifndef OB_MM_RING_A
+#define OB_MM_RING_A 4
+#endif
+#ifndef OB_MM_PASS_BLOCKS
+#define OB_MM_PASS_BLOCKS 3  // affine / final blocks per CU the compiler sizes registers for (K <= 16)
+#endif
+constexpr int kRing = OB_MM_RING;     // wave steps of state in flight (affine / final)
+constexpr int kRingA = OB_MM_RING_A;  // the same for the assemble pass (its fragments sit in LDS to make room)
 constexpr int kStoreAt = 4; // step after which the next sub-tile's staged values are written
 typedef double mm_d4 __attribute__((ext_vector_type(4)));
 static_assert(16 % kRing == 0, "ring slots are static per unrolled step");
@@ -663,7 +672,7 @@ __device__ __forceinline__ void state_walk(const MmArgs& a, const Blk& b, const 
 
 // [0] primal step bound, [1] dual step bound, [2..4] mu_aff terms, then X'q rho0, X'q rho1.
 template <int K>
-__global__ __launch_bounds__(256, K <= 16 ? 3 : 2) void mm_affine_kernel(const MmArgs a) {
+__global__ __launch_bounds__(256, K <= 16 ? OB_MM_PASS_BLOCKS : 2) void mm_affine_kernel(const MmArgs a) {
   constexpr int NV = 5 + 2 * K;
   constexpr int NXB = Xs<K>::NXB;
   __shared__ __attribute__((aligned(16))) double xs[2][kSub * Xs<K>::S];
@@ -721,7 +730,7 @@ __global__ __launch_bounds__(256, K <= 16 ? 3 : 2) void mm_affine_kernel(const M
 
 // Step-length bounds of the corrector direction (the next assemble replays the direction).
 template <int K>
-__global__ __launch_bounds__(256, 2) void mm_final_kernel(const MmArgs a) {
+__global__ __launch_bounds__(256, K <= 16 ? OB_MM_PASS_BLOCKS : 2) void mm_final_kernel(const MmArgs a) {
   __shared__ __attribute__((aligned(16))) double xs[2][kSub * Xs<K>::S];
   __shared__ uint32_t lst[kCap];
   const Blk b = blk_ctx(a, lst, false);

@@ -21,6 +21,6 @@ done
 cd "$REPO"
 for k in "mm_assemble_mfma_kernel<16, true>" "mm_affine_kernel<16>" "mm_final_kernel<16>"; do
   echo "## $k"
-  for i in 1 2 3 4; do python tools/pmc_clock.py "$OUT/${TAG}_pmcm$i" "$k" | tail -3; done
+  for i in 1 2 3 4; do python tools/pmc_sum.py "$OUT/${TAG}_pmcm$i" "$k"; done
 done > "$OUT/${TAG}_pmc_mm.txt"
 cat "$OUT/${TAG}_pmc_mm.txt"
