@@ -748,7 +748,7 @@ def main():
             i8_tops = ops_rep * reps_per_launch / (gram_launch_ms * 1e-3) / 1e12 if gram_launch_ms else 0.0
             roof = {"bound": "mfma", "achieved": i8_tops, "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS (i8)",
                     "frac": i8_tops / I8_MFMA_PEAK_TOPS, "traffic": traffic,
-                    "traffic_source": "profiles/pmc_gram_i8.json (PMC 2 x FETCH_SIZE + WRITE_SIZE, round 5 tree, profiles/r05_pmc_gram.json)",
+                    "traffic_source": "profiles/pmc_gram_i8.json (PMC 2 x FETCH_SIZE + WRITE_SIZE, final round-5 tree, profiles/r05_final_pmc_gram.json)",
                     "kernel": "oz_gram_kernel",
                     "avg_launch_ms": gram_launch_ms, "i8_ops_per_replicate": ops_rep,
                     "i8_ops_issued_per_replicate": ops_issued, "digit_slices_mean": slices,
