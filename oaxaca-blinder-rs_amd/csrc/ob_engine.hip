@@ -175,7 +175,8 @@ __device__ __forceinline__ uint32_t l1_split_item(uint32_t q, uint32_t c, uint32
 }
 
 // DIAG (OB_L1_DIAG, timing ablations only, wrong counts): 1 no random bits (left = c / 2),
-// 2 one round only, 4 no Knuth-Yao staging, 8 no m1 stores, 16 return after the staging barrier.
+// 2 one round only, 4 no Knuth-Yao staging, 8 no m1 stores, 16 return after the staging barrier,
+// 32 no random bits for the one-thread-per-node levels' nodes below 128 draws.
 template <int DIAG>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void ob_level1_kernel(uint32_t n0, uint32_t n1, uint32_t tiles0,
                                                            uint32_t first_rep, uint32_t stride,
@@ -255,6 +256,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
           uint32_t left = 0;
           const uint32_t ns = c ? ob_l1_items(c) : 0u;
           if constexpr (DIAG & 1) left = c >> 1;
+          else if ((DIAG & 32) && c < 128u) left = c >> 1;
           else
             for (uint32_t q = 0; q < ns; ++q)
               left += l1_split_item(q, c, rep, (kg << 1) | g, rl, key0, key1, kyl, ky_g.off, ky_g.list);
@@ -1785,10 +1787,11 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   using L1Kernel = void (*)(uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t*,
                             const ob_ky_tables);
 #if OB_TUNING  // timing ablations of level 1 (l1_diag, tools/l1_ablate.sh)
-  const int l1_diag = ob::opt_int(ob::Opt::L1Diag, 0) & 31;
+  const int l1_diag = ob::opt_int(ob::Opt::L1Diag, 0) & 63;
   const L1Kernel l1k = l1_diag == 0    ? ob_level1_kernel<0>
                        : l1_diag == 1  ? ob_level1_kernel<1>
                        : l1_diag == 2  ? ob_level1_kernel<2>
+                       : l1_diag == 32 ? ob_level1_kernel<32>
                        : l1_diag == 3  ? ob_level1_kernel<3>
                        : l1_diag == 11 ? ob_level1_kernel<11>
                        : l1_diag == 16 ? ob_level1_kernel<16>
