@@ -226,7 +226,8 @@ def bench_mm(args, world, rank, local, dist):
     out = {
         "metric": "Machado-Mata bootstrap replicates/sec (configs[4]: 1000 QR draws per group per replicate)",
         "value": value, "unit": "replicates/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak" if world > 1 else "single", "vs_baseline": None,
         "dtype": "f64", "data": "synthetic (SURVEY.md §8d wage panel, numpy seed 20260424; OBRS-3/MM-1 seed 0x0B5EED)",
         "config": {"workload": "configs[4]: Machado-Mata, 1000 simulations, quantiles 0.1/0.25/0.5/0.75/0.9",
                    "rows": args.rows, "predictors": args.preds, "simulations": args.sims,
@@ -324,7 +325,7 @@ def bench_heckman(args, world, rank, local, dist):
         "metric": "Heckman two-step bootstrap replicates/sec (configs[1] panel + selection equation)",
         "value": world * B * args.steps / elapsed, "unit": "replicates/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "scaling": "weak" if world > 1 else "single", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (SURVEY.md §8d wage panel + s = 1[0.3 + 0.5 z1 - 0.4 z2 + 0.2 x4 + u > 0])",
         "config": {"workload": "heckman_selection(s, [z1, z2, x4]), GroupA reference coefficients",
                    "rows": args.rows, "predictors": args.preds, "selection_predictors": len(zs),
@@ -449,18 +450,24 @@ def end_to_end(ob, ctx, d, ya, yb, n, ref, stat_cols, dev):
     t_point = time.perf_counter() - t1
     rows = torch.empty((n, panel.row_len), dtype=torch.float64, device=dev)
     ok = torch.empty(n, dtype=torch.uint8, device=dev)
+    t2 = time.perf_counter()
     panel.boot_sharded_device(0x0B5EED, 0, n, rows.data_ptr(), ok.data_ptr(), ref,
                               stream=torch.cuda.current_stream(dev).cuda_stream)
+    t_enqueue = time.perf_counter() - t2
     panel.sync()
+    t_boot = time.perf_counter() - t2
     tm = panel.timing()
+    t3 = time.perf_counter()
     hr = rows[:, : len(stat_cols)].cpu().numpy()
     ob.aggregate(np.ascontiguousarray(hr), ok.cpu().numpy(), stat_cols)
+    t_agg = time.perf_counter() - t3
     total_s = time.perf_counter() - t0
     assert np.isfinite(point[: len(stat_cols)]).all(), "point estimate"
 
     panel.close()
     return {"replicates": n, "ms": total_s * 1e3, "replicates_per_s": n / total_s,
             "panel_create_ms": t_create * 1e3, "point_estimate_ms": t_point * 1e3, "prep_ms": tm["prep_ms"],
+            "boot_enqueue_ms": t_enqueue * 1e3, "boot_wall_ms": t_boot * 1e3, "aggregate_ms": t_agg * 1e3,
             "boot_ms": tm["level1_ms"] + tm["counts_ms"] + tm["gram_ms"] + tm["reduce_ms"] + tm["solve_ms"],
             "oz_exceptions": tm["oz_exceptions"], "oz_bits": tm["oz_bits"],
             "what": "run() as builder.rs:787-983 runs it: fresh ob_panel_create (H2D + Gram panel) + the point "
@@ -478,6 +485,8 @@ def replicate_plan(reps, world, strong=False, weak=False):
     if world > 1 and not weak:
         strong = True
     total = reps if strong else reps * world
+    if world == 1:  # one GPU is neither weak nor strong scaling
+        return "single", total, total
     return ("strong" if strong else "weak"), total, -(-total // world)
 
 

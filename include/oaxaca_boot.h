@@ -262,9 +262,12 @@ int ob_debug_mm_betas(ob_panel* panel, uint64_t seed, int32_t simulations, uint6
      "mm_state_gb", "mm_delta1", "mm_delta2", "mm_tol1", "mm_fit_stride", "mm_kappa", "mm_band0":
                    Machado-Mata tuning (the verification keeps results exact)
      "gram_diag", "l1_diag": timing ablations, tuning builds only (OB_E_UNSUPPORTED otherwise)
-   Unknown names are OB_E_INVALID. ob_tuning_build() is 1 in a -DOB_TUNING=1 build (`make tuning`),
+     "debug_count_overflow" nonzero: the resample's count-overflow word is raised after every
+                   count kernel of a Machado-Mata run or ob_debug_counts (tests the OB_E_OVERFLOW path)
+   Unknown names are OB_E_INVALID. ob_get_option reads back what ob_set_option stored (NaN: unset). ob_tuning_build() is 1 in a -DOB_TUNING=1 build (`make tuning`),
    which also reads OB_<NAME> from the environment for options nobody set. */
 int ob_set_option(const char* name, double value);
+int ob_get_option(const char* name, double* value);
 /* Test hook: the Heckman kernels' normal pdf and cdf (npdf_ncdf: W. J. Cody's rational erfc with
    the pdf's exponential shared, ob_heckman.hip) on the device at z[0 .. n). */
 int ob_debug_normal(int device, const double* z, int64_t n, double* pdf, double* cdf);

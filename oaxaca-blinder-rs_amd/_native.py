@@ -7,6 +7,7 @@ called, the call raises -- the bootstrap never silently runs on the CPU.
 from __future__ import annotations
 
 import contextlib
+import math
 import ctypes as C
 import os
 import threading
@@ -42,7 +43,7 @@ EXPORTED = (
     "ob_get_unique_id", "ob_ctx_create_rank", "ob_ctx_rank", "ob_boot_run_sharded", "ob_boot_run_sharded_device",
     "ob_boot_run_multi", "ob_debug_counts", "ob_prepared_boot_sharded", "ob_debug_gram",
     "ob_debug_gram_exceptions", "ob_panel_set_gather_columns", "ob_debug_shard_sim", "ob_debug_mm_fail",
-    "ob_debug_chunks", "ob_debug_mm_betas", "ob_set_option", "ob_tuning_build",
+    "ob_debug_chunks", "ob_debug_mm_betas", "ob_set_option", "ob_get_option", "ob_tuning_build",
     "ob_debug_normal",
 )
 
@@ -201,6 +202,7 @@ _SIGS = {
     "ob_debug_chunks": (C.c_int, [_P, C.POINTER(C.c_uint32), C.c_int32, C.POINTER(C.c_int32)]),
     "ob_debug_mm_betas": (C.c_int, [_P, C.c_uint64, C.c_int32, C.c_uint64, _D, _U8]),
     "ob_set_option": (C.c_int, [C.c_char_p, C.c_double]),
+    "ob_get_option": (C.c_int, [C.c_char_p, C.POINTER(C.c_double)]),
     "ob_tuning_build": (C.c_int, []),
     "ob_debug_normal": (C.c_int, [C.c_int, _D, C.c_int64, _D, _D]),
 }
@@ -313,14 +315,23 @@ def set_option(name: str, value) -> None:
     check(lib().ob_set_option(name.encode(), float("nan") if value is None else float(value)))
 
 
+def get_option(name: str):
+    """ob_get_option: the value ob_set_option stored for ``name``, or None when it is unset."""
+    v = C.c_double()
+    check(lib().ob_get_option(name.encode(), C.byref(v)))
+    return None if math.isnan(v.value) else v.value
+
+
 @contextlib.contextmanager
 def option(name: str, value):
-    """set_option for the duration of a with-block, then back to the default."""
+    """set_option for the duration of a with-block, then back to the value it had before (so
+    nested blocks and fixtures that already set the option keep their setting)."""
+    prev = get_option(name)
     set_option(name, value)
     try:
         yield
     finally:
-        set_option(name, None)
+        set_option(name, prev)
 
 
 def device_count() -> int:

@@ -1219,6 +1219,116 @@ __global__ __launch_bounds__(kBlock) void ob_residual_kernel(const double* cols,
 }
 
 // ---------------------------------------------------------------------------------------------
+// Unit Gram of the point estimate (run_single_pass on the unresampled groups, builder.rs:810-811):
+// G_g = V_g^T V_g over every row once, V = sqrt(w) [1, x, y] (ols.rs:68-78). With unit counts the
+// count-weighted GEMM of the bootstrap collapses to a SYRK, so it runs as one: D(I, J) =
+// V[:, 16I..]^T V[:, 16J..] on v_mfma_f64_16x16x4f64 with A = the staged rows of column block I
+// and B those of block J (the same staged image the Gram kernels read, ob_panel_kernel). Each
+// block sums a fixed run of 64-row sub-tiles of one group -- a function of the group's size only,
+// so multi-outcome panels and their one-outcome slices agree bitwise -- and writes one partial
+// per pair; ob_unit_reduce_kernel adds the partials in block order. 168 MB of panel at 1M x 20
+// WLS, read once: the launch needs thousands of blocks, not the boot's 32 chunks.
+// ---------------------------------------------------------------------------------------------
+constexpr int kUgMaxBlocks = 1024;  // per group
+constexpr int kUgMaxPairs = 9;      // column-block pairs per wave: 4 waves x 9 >= 36 (k1 <= 128)
+
+struct UnitGramArgs {
+  const double* gp[2];  // Gram panels (ob_panel_kernel layout)
+  uint32_t n[2];
+  uint32_t subs[2];     // sub-tiles per block
+  uint32_t blocks0;     // blocks of group 0 (group 1 follows)
+  int k1, c_first, e, nbk;
+  double* partial;      // [e][total blocks]
+  uint32_t nblocks;
+};
+
+__global__ __launch_bounds__(kBlock) void ob_unit_gram_kernel(const UnitGramArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double xs[];  // [k1][kColStride]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t g = blockIdx.x < a.blocks0 ? 0u : 1u;
+  const uint32_t bi = g ? blockIdx.x - a.blocks0 : blockIdx.x;
+  const uint32_t n = a.n[g], nsub = (n + 63) >> 6;
+  const uint32_t s0 = bi * a.subs[g], s1 = min(nsub, s0 + a.subs[g]);
+  const int ncl = a.k1 - a.c_first;
+  const int npairs = a.nbk * (a.nbk + 1) / 2;
+  // this wave's column-block pairs (I <= J), dealt round-robin over the 4 waves
+  int pI[kUgMaxPairs], pJ[kUgMaxPairs];
+#pragma unroll
+  for (int q = 0; q < kUgMaxPairs; ++q) {
+    int t = wave + 4 * q, I = 0;
+    while (t >= a.nbk - I && I < a.nbk) {
+      t -= a.nbk - I;
+      ++I;
+    }
+    pI[q] = I;
+    pJ[q] = I + t;
+  }
+  ob_d4 acc[kUgMaxPairs];
+#pragma unroll
+  for (int q = 0; q < kUgMaxPairs; ++q) acc[q] = (ob_d4){0.0, 0.0, 0.0, 0.0};
+  const int kq = lane >> 4, li = lane & 15;
+  for (uint32_t s = s0; s < s1; ++s) {
+    const double2* src = reinterpret_cast<const double2*>(a.gp[g] + (size_t)s * ncl * kColStride);
+    double2* dst = reinterpret_cast<double2*>(xs + a.c_first * kColStride);
+    for (int i = tid; i < ncl * kColStride / 2; i += kBlock) dst[i] = src[i];
+    if (a.c_first == 1)  // the intercept's ones (LDS-resident in the Gram kernels), zero past n
+      for (int pos = tid; pos < kColStride; pos += kBlock) {
+        const int q = pos & 63;
+        xs[pos] = (s * 64u + (uint32_t)(((q & 15) << 2) | (q >> 4)) < n) ? 1.0 : 0.0;
+      }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kUgMaxPairs; ++q) {
+      if (wave + 4 * q >= npairs) break;
+      const int ca = pI[q] * 16 + li, cb = pJ[q] * 16 + li;
+      const double* pa = xs + ca * kColStride + kq * 16 + (ca & 31);
+      const double* pb = xs + cb * kColStride + kq * 16 + (cb & 31);
+      const bool va = ca < a.k1, vb = cb < a.k1;
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks)
+        acc[q] = __builtin_amdgcn_mfma_f64_16x16x4f64(va ? pa[ks] : 0.0, vb ? pb[ks] : 0.0, acc[q], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // D(I, J)[i][j] sits in lane (i % 4) * 16 + j, element i / 4: pair (16I + i, 16J + j), upper triangle
+#pragma unroll
+  for (int q = 0; q < kUgMaxPairs; ++q) {
+    if (wave + 4 * q >= npairs) break;
+    const int b = pJ[q] * 16 + li;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int c = pI[q] * 16 + kq + 4 * r;
+      if (c <= b && b < a.k1) {
+        const int e = c * a.k1 - c * (c - 1) / 2 + (b - c);
+        a.partial[(size_t)e * a.nblocks + blockIdx.x] = acc[q][r];
+      }
+    }
+  }
+}
+
+// gram[g][e] = the sum of group g's block partials of pair e, in block order then a fixed LDS tree
+// (deterministic); pairs e_pad > e >= E are zero. One block per (group, pair).
+__global__ __launch_bounds__(kBlock) void ob_unit_reduce_kernel(const double* partial, uint32_t nblocks,
+                                                                uint32_t blocks0, int e, int e_pad, double* gram) {
+  __shared__ double red[kBlock];
+  const int tid = threadIdx.x;
+  const int g = blockIdx.x >= (unsigned)e_pad ? 1 : 0;
+  const int ei = (int)blockIdx.x - g * e_pad;
+  double s = 0.0;
+  if (ei < e) {
+    const uint32_t b0 = g ? blocks0 : 0u, b1 = g ? nblocks : blocks0;
+    for (uint32_t b = b0 + tid; b < b1; b += kBlock) s += partial[(size_t)ei * nblocks + b];
+  }
+  red[tid] = s;
+  __syncthreads();
+  for (int h = kBlock / 2; h > 0; h >>= 1) {
+    if (tid < h) red[tid] += red[tid + h];
+    __syncthreads();
+  }
+  if (tid == 0) gram[g * e_pad + ei] = red[0];
+}
+
+// ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
 // Knuth-Yao tables of B(2^j, 1/2) for OBRS-2's level-1 split (ob_spec.h): W_k = C(2^j, k) exactly
@@ -1547,135 +1657,121 @@ int engine_point_estimate(ob_panel* p, int ref_mode, double* row, double* resid_
   HIP_OK(hipSetDevice(ctx->device));
   hipStream_t s = ctx->stream;
   Plan pl = make_plan(p, 1, true);
-  const int nch = pl.n_chunks();
-  double *d_partial = nullptr, *d_gram = nullptr, *d_row = nullptr, *d_gout = nullptr, *d_beta = nullptr,
-         *d_res = nullptr;
-  uint32_t* d_chunks = nullptr;
-  uint8_t* d_ok = nullptr;
-  auto cleanup = [&]() {
-    (void)hipFree(d_partial);
-    (void)hipFree(d_gram);
-    (void)hipFree(d_row);
-    (void)hipFree(d_gout);
-    (void)hipFree(d_beta);
-    (void)hipFree(d_res);
-    (void)hipFree(d_chunks);
-    (void)hipFree(d_ok);
-  };
-  int rc = OB_OK;
-  do {
-#define PE_OK(expr)                                                                            \
-  {                                                                                            \
-    hipError_t e_ = (expr);                                                                    \
-    if (e_ != hipSuccess) {                                                                    \
-      rc = ob::fail(OB_E_HIP, "HIP error %s at %s:%d", hipGetErrorString(e_), __FILE__, __LINE__); \
-      break;                                                                                   \
-    }                                                                                          \
+  // the unit Gram's blocks: a run of sub-tiles per block, at most kUgMaxBlocks per group
+  UnitGramArgs ua{};
+  uint32_t nblk[2];
+  for (int g = 0; g < 2; ++g) {
+    const uint32_t nsub = (p->n[g] + 63) / 64;
+    ua.subs[g] = std::max<uint32_t>(2u, (nsub + kUgMaxBlocks - 1) / kUgMaxBlocks);
+    nblk[g] = (nsub + ua.subs[g] - 1) / ua.subs[g];
+    ua.gp[g] = p->d_gpanel[g];
+    ua.n[g] = p->n[g];
   }
-    PE_OK(hipMalloc(&d_partial, sizeof(double) * (size_t)nch * pl.rep_pad * p->e_pad));
-    PE_OK(hipMalloc(&d_gram, sizeof(double) * 2 * (size_t)pl.rep_pad * p->e_pad));
-    PE_OK(hipMalloc(&d_row, sizeof(double) * p->row_len * p->n_y));
-    PE_OK(hipMalloc(&d_gout, sizeof(double) * 2 * p->e_pad));
-    PE_OK(hipMalloc(&d_chunks, sizeof(uint32_t) * pl.chunks.size()));
-    PE_OK(hipMalloc(&d_ok, p->n_y));
-    PE_OK(hipMemcpyAsync(d_chunks, pl.chunks.data(), sizeof(uint32_t) * pl.chunks.size(), hipMemcpyHostToDevice, s));
-    GramArgs ga = gram_args(p, pl);
-    ga.chunks = d_chunks;
-    ga.m1 = nullptr;
-    ga.n_reps = 1;
-    ga.first_rep = 0;
-    ga.partial = d_partial;
-    const uint32_t blocks = pl.nb_rep * pl.n_cg * (uint32_t)nch;
-    PE_OK(launch_gram(p, pl.cb, true, ga, blocks, s));
-    const size_t nred = (size_t)1 * p->e_pad;
-    hipLaunchKernelGGL(ob_reduce_kernel, dim3((unsigned)((nred + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                       (const double*)d_partial, (const uint32_t*)d_chunks, nch, pl.rep_pad, p->e_pad, 1u, d_gram);
-    PE_OK(hipGetLastError());
-    if (p->heckman) {  // estimation.rs:114-172 on the whole groups (every row once)
-      rc = ensure_heck(p, pl);
-      if (rc != OB_OK) break;
-      ob_heck_seg hs = heck_seg(p, pl, d_chunks, d_gram, ref_mode);
-      hs.counts = nullptr;
-      hs.n_reps = 1;
-      hs.rows = d_row;
-      hs.ok = d_ok;
-      hs.raw_status = 1;
-      int it = 0;
-      rc = ob::heckman_segment(hs, s, &it);
-      if (rc != OB_OK) break;
-      uint8_t okh = 0;
-      PE_OK(hipMemcpyAsync(row, d_row, sizeof(double) * p->row_len, hipMemcpyDeviceToHost, s));
-      PE_OK(hipMemcpyAsync(&okh, d_ok, 1, hipMemcpyDeviceToHost, s));
-      PE_OK(hipStreamSynchronize(s));
-      p->timing.probit_iterations = it;
-      switch (okh) {
-        case OB_HS_OK: break;
-        case OB_HS_NO_OUTCOMES:
-          rc = ob::fail(OB_E_GROUP, "%sNo observed outcomes in group", error_prefix(OB_E_GROUP));
-          break;
-        case OB_HS_PROBIT:
-          rc = ob::fail(OB_E_LINALG, "%sFailed to solve Hessian system in Probit", error_prefix(OB_E_LINALG));
-          break;
-        case OB_HS_INSUFFICIENT:
-          rc = ob::fail(OB_E_INSUFFICIENT, "%sInsufficient data for OLS calculation: n_obs must be strictly greater than k",
+  ua.blocks0 = nblk[0];
+  ua.nblocks = nblk[0] + nblk[1];
+  ua.k1 = p->k1;
+  ua.c_first = p->weighted ? 0 : 1;
+  ua.e = p->e;
+  ua.nbk = (p->k1 + 15) / 16;
+  if (ua.nbk * (ua.nbk + 1) / 2 > 4 * kUgMaxPairs) return ob::fail(OB_E_UNSUPPORTED, "point estimate: k1 > 128");
+  // persistent per-panel scratch (no hipMalloc / hipFree per call): partials, then the Gram
+  // [rep_pad][2][e_pad] (rep 0 used), the rows, the first outcome's reduced Grams, beta, residuals
+  const size_t o_part = 0, n_part = (size_t)p->e * std::max(ua.nblocks, 1u);
+  const size_t o_gram = o_part + n_part, n_gram = (size_t)2 * pl.rep_pad * p->e_pad;
+  const size_t o_row = o_gram + n_gram, n_row = (size_t)p->row_len * p->n_y;
+  const size_t o_gout = o_row + n_row, n_gout = (size_t)2 * p->e_pad;
+  const size_t o_beta = o_gout + n_gout, n_beta = (size_t)p->k * p->n_y;
+  const size_t o_res = o_beta + n_beta, n_res = std::max<uint32_t>(p->n[1], 1);
+  OB_TRY(ensure_buf(&p->d_pe, p->cap_pe, o_res + (resid_b ? n_res : 0)));
+  OB_TRY(ensure_buf(&p->d_pe_ok, p->cap_pe_ok, (size_t)std::max(p->n_y, 1)));
+  double* d_gram = p->d_pe + o_gram;
+  double* d_row = p->d_pe + o_row;
+  double* d_gout = p->d_pe + o_gout;
+  double* d_beta = p->d_pe + o_beta;
+  uint8_t* d_ok = p->d_pe_ok;
+  ua.partial = p->d_pe + o_part;
+  const size_t lds = sizeof(double) * (size_t)p->k1 * kColStride;
+  HIP_OK(hipFuncSetAttribute((const void*)ob_unit_gram_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  if (ua.nblocks) {
+    hipLaunchKernelGGL(ob_unit_gram_kernel, dim3(ua.nblocks), dim3(kBlock), lds, s, ua);
+    HIP_OK(hipGetLastError());
+  }
+  hipLaunchKernelGGL(ob_unit_reduce_kernel, dim3(2 * p->e_pad), dim3(kBlock), 0, s, (const double*)ua.partial,
+                     ua.nblocks, ua.blocks0, p->e, p->e_pad, d_gram);
+  HIP_OK(hipGetLastError());
+  if (p->heckman) {  // estimation.rs:114-172 on the whole groups (every row once)
+    if (!p->chunks_ready) {  // the probit/IMR passes walk the panel's chunk table
+      p->chunks = pl.chunks;
+      OB_TRY(ensure_buf(&p->d_chunks, p->cap_chunks, p->chunks.size()));
+      HIP_OK(hipMemcpyAsync(p->d_chunks, p->chunks.data(), sizeof(uint32_t) * p->chunks.size(), hipMemcpyHostToDevice, s));
+      p->chunks_ready = true;
+    }
+    OB_TRY(ensure_heck(p, pl));
+    ob_heck_seg hs = heck_seg(p, pl, p->d_chunks, d_gram, ref_mode);
+    hs.counts = nullptr;
+    hs.n_reps = 1;
+    hs.rows = d_row;
+    hs.ok = d_ok;
+    hs.raw_status = 1;
+    int it = 0;
+    OB_TRY(ob::heckman_segment(hs, s, &it));
+    uint8_t okh = 0;
+    HIP_OK(hipMemcpyAsync(row, d_row, sizeof(double) * p->row_len, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(&okh, d_ok, 1, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    p->timing.probit_iterations = it;
+    switch (okh) {
+      case OB_HS_OK: return OB_OK;  // residuals: zeros over B's selected rows (estimation.rs:152-153), the caller's
+      case OB_HS_NO_OUTCOMES:
+        return ob::fail(OB_E_GROUP, "%sNo observed outcomes in group", error_prefix(OB_E_GROUP));
+      case OB_HS_PROBIT:
+        return ob::fail(OB_E_LINALG, "%sFailed to solve Hessian system in Probit", error_prefix(OB_E_LINALG));
+      case OB_HS_INSUFFICIENT:
+        return ob::fail(OB_E_INSUFFICIENT, "%sInsufficient data for OLS calculation: n_obs must be strictly greater than k",
                         error_prefix(OB_E_INSUFFICIENT));
-          break;
-        case OB_HS_ZERO_WEIGHT:
-          rc = ob::fail(OB_E_GROUP, "%sNo data in groups for weighted coefficients.", error_prefix(OB_E_GROUP));
-          break;
-        default:
-          rc = ob::fail(OB_E_LINALG,
+      case OB_HS_ZERO_WEIGHT:
+        return ob::fail(OB_E_GROUP, "%sNo data in groups for weighted coefficients.", error_prefix(OB_E_GROUP));
+      default:
+        return ob::fail(OB_E_LINALG,
                         "%sFailed to perform Cholesky decomposition. Matrix may be singular or not positive "
                         "definite due to multicollinearity.",
                         error_prefix(OB_E_LINALG));
-      }
-      break;  // residuals: zeros over the selected rows of B (estimation.rs:152-153), filled by the caller
     }
-    PE_OK(hipMalloc(&d_beta, sizeof(double) * p->k * p->n_y));
-    for (int t = 0; t < p->n_y; ++t) {
-      SolveArgs sa = solve_args(p, ref_mode);
-      sa.yc = p->p + 1 + t;
-      sa.gram = d_gram;
-      sa.rows = d_row + (size_t)t * p->row_len;
-      sa.ok = d_ok + t;
-      sa.n_reps = 1;
-      sa.gram_out = t == 0 ? d_gout : nullptr;
-      sa.raw_status = 1;
-      sa.raw_beta_b = d_beta + (size_t)t * p->k;
-      PE_OK(launch_solve(p, sa, 1, s));
+  }
+  for (int t = 0; t < p->n_y; ++t) {
+    SolveArgs sa = solve_args(p, ref_mode);
+    sa.yc = p->p + 1 + t;
+    sa.gram = d_gram;
+    sa.rows = d_row + (size_t)t * p->row_len;
+    sa.ok = d_ok + t;
+    sa.n_reps = 1;
+    sa.gram_out = t == 0 ? d_gout : nullptr;
+    sa.raw_status = 1;
+    sa.raw_beta_b = d_beta + (size_t)t * p->k;
+    HIP_OK(launch_solve(p, sa, 1, s));
+  }
+  // the residuals (only when asked for) are computed before the one host synchronization
+  if (resid_b && p->n[1] > 0) {
+    double* d_res = p->d_pe + o_res;
+    for (int t = 0; t < p->n_y; ++t) {  // the kernel-stream order serializes d_res reuse
+      hipLaunchKernelGGL(ob_residual_kernel, dim3((p->n[1] + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
+                         (const double*)p->d_cols[1], p->ld[1], p->n[1], p->p, p->p + t,
+                         (const double*)(d_beta + (size_t)t * p->k), d_res);
+      HIP_OK(hipGetLastError());
+      HIP_OK(hipMemcpyAsync(resid_b + (size_t)t * p->n[1], d_res, sizeof(double) * p->n[1], hipMemcpyDeviceToHost, s));
     }
-    uint8_t okh = 0;
-    std::vector<double> gout(2 * p->e_pad);
-    PE_OK(hipMemcpyAsync(row, d_row, sizeof(double) * p->row_len * p->n_y, hipMemcpyDeviceToHost, s));
-    PE_OK(hipMemcpyAsync(&okh, d_ok, 1, hipMemcpyDeviceToHost, s));
-    PE_OK(hipMemcpyAsync(gout.data(), d_gout, sizeof(double) * gout.size(), hipMemcpyDeviceToHost, s));
-    PE_OK(hipStreamSynchronize(s));
-    if (okh == 2) {
-      rc = ob::fail(OB_E_GROUP, "%sNo data in groups for weighted coefficients.", error_prefix(OB_E_GROUP));
-      break;
-    }
-    if (okh != 1) {
-      rc = ob::fail(OB_E_LINALG,
+  }
+  uint8_t okh = 0;
+  HIP_OK(hipMemcpyAsync(row, d_row, sizeof(double) * p->row_len * p->n_y, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipMemcpyAsync(&okh, d_ok, 1, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  if (okh == 2) return ob::fail(OB_E_GROUP, "%sNo data in groups for weighted coefficients.", error_prefix(OB_E_GROUP));
+  if (okh != 1)
+    return ob::fail(OB_E_LINALG,
                     "%sFailed to perform Cholesky decomposition. Matrix may be singular or not positive "
                     "definite due to multicollinearity.",
                     error_prefix(OB_E_LINALG));
-      break;
-    }
-    if (resid_b) {
-      PE_OK(hipMalloc(&d_res, sizeof(double) * std::max<uint32_t>(p->n[1], 1)));
-      for (int t = 0; t < p->n_y && p->n[1] > 0; ++t) {  // the kernel-stream order serializes d_res reuse
-        hipLaunchKernelGGL(ob_residual_kernel, dim3((p->n[1] + kBlock - 1) / kBlock), dim3(kBlock), 0, s,
-                           (const double*)p->d_cols[1], p->ld[1], p->n[1], p->p, p->p + t,
-                           (const double*)(d_beta + (size_t)t * p->k), d_res);
-        PE_OK(hipGetLastError());
-        PE_OK(hipMemcpyAsync(resid_b + (size_t)t * p->n[1], d_res, sizeof(double) * p->n[1], hipMemcpyDeviceToHost, s));
-      }
-      PE_OK(hipStreamSynchronize(s));
-    }
-#undef PE_OK
-  } while (0);
-  cleanup();
-  return rc;
+  return OB_OK;
 }
 
 // OBRS-3 resample counts for replicates [first_rep, first_rep + n_reps) without the Gram: level-1
@@ -1691,8 +1787,9 @@ int engine_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_rep
   Plan pl = make_plan(p, n_reps, false);
   OB_TRY(ensure_buf(&p->d_m1, p->cap_m1, (size_t)tiles * pl.rep_pad));
   OB_TRY(ensure_buf(&p->d_counts, p->cap_counts, (size_t)tiles * pl.nb_rep * 4 * kCimgWords));
-  // its own overflow word (d_flags[2]): word 0 belongs to boot calls that may still be pending
-  HIP_OK(hipMemsetAsync(p->d_flags + 2, 0, sizeof(uint32_t), s));
+  // Overflow goes to its own word, d_flags[2] (word 0 belongs to boot calls that may still be
+  // pending). The caller clears it once before its first call and reads it after its last: the
+  // count kernel only ever ORs into it, so an overflow in any segment survives to the check.
   const uint32_t key0 = (uint32_t)seed, key1 = (uint32_t)(seed >> 32);
   const size_t lds_l1 = sizeof(uint32_t) * std::max(l1_lds_words(p->ntiles[0]), l1_lds_words(p->ntiles[1]));
   HIP_OK(hipFuncSetAttribute((const void*)ob_level1_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_l1));
@@ -1713,6 +1810,7 @@ int engine_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_rep
   hipLaunchKernelGGL(ob_count_kernel<false>, dim3((tiles + kCntTilesPerBlock - 1) / kCntTilesPerBlock, pl.nb_rep),
                      dim3(kBlock), 0, s, ga);
   HIP_OK(hipGetLastError());
+  if (opt_int(Opt::DebugCountOverflow, 0)) HIP_OK(hipMemsetAsync(p->d_flags + 2, 0xFF, sizeof(uint32_t), s));
   *nb_rep = pl.nb_rep;
   *rep_pad = pl.rep_pad;
   return OB_OK;
@@ -2146,6 +2244,8 @@ void ob_panel_destroy(ob_panel* p) {
   (void)hipFree(p->d_hactive);
   (void)hipFree(p->d_rows_tmp);
   (void)hipFree(p->d_ok_tmp);
+  (void)hipFree(p->d_pe);
+  (void)hipFree(p->d_pe_ok);
   ob::shard_free(p);
   ob::oz_free(p);
   (void)hipFree(p->d_mm_fail);
@@ -2242,6 +2342,7 @@ int ob_debug_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_r
   hipStream_t s = p->ctx->stream;
   uint32_t nb = 0, rep_pad = 0;
   OB_TRY(ob::engine_order(p, s));  // after any call on this panel from another stream
+  HIP_OK(hipMemsetAsync(p->d_flags + 2, 0, sizeof(uint32_t), s));  // engine_counts' overflow word
   const int rc = ob::engine_counts(p, seed, first_rep, n_reps, s, &nb, &rep_pad);
   OB_TRY(ob::engine_mark(p, s));
   OB_TRY(rc);

@@ -63,6 +63,9 @@ struct ob_panel {
   double* d_rows_tmp = nullptr;  // host-API staging
   uint8_t* d_ok_tmp = nullptr;
   uint64_t tmp_reps = 0;
+  double* d_pe = nullptr;        // point estimate scratch (unit-Gram partials, Gram, rows, beta, residuals)
+  uint8_t* d_pe_ok = nullptr;
+  size_t cap_pe = 0, cap_pe_ok = 0;
 
   double* d_hgamma = nullptr;     // Heckman: [2][rep_pad][ks] probit coefficients
   uint32_t* d_hflags = nullptr;   // Heckman: [2][rep_pad] done / failed

@@ -2169,8 +2169,9 @@ static int mm_run_impl(ob_panel* p, uint64_t seed, int sims, const double* quant
   MM_OK(b.reserve(need));
   MM_OK(hipMemcpy(b.quant, quantiles, sizeof(double) * n_q, hipMemcpyHostToDevice));
 
-  // the overflow flag of this call's count images (a point-pass-only call draws none)
-  MM_OK(hipMemsetAsync(p->d_flags, 0, sizeof(uint32_t), s));
+  // the overflow word of this call's count images (engine_counts ORs into d_flags[2] over every
+  // segment; word 0 is the boot calls' and may belong to an async boot not yet collected)
+  MM_OK(hipMemsetAsync(p->d_flags + 2, 0, sizeof(uint32_t), s));
   MmArgs a{};
   for (int g = 0; g < 2; ++g) {
     a.cols[g] = p->d_cols[g];
@@ -2264,7 +2265,7 @@ static int mm_run_impl(ob_panel* p, uint64_t seed, int sims, const double* quant
     }
   }
   uint32_t flag = 0;
-  MM_OK(hipMemcpy(&flag, p->d_flags, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  MM_OK(hipMemcpy(&flag, p->d_flags + 2, sizeof(uint32_t), hipMemcpyDeviceToHost));
   if (flag) return ob::fail(OB_E_OVERFLOW, "a resampled row was drawn more than 255 times in one replicate");
   p->timing.mm_assemble_ms = st.assemble_ms;
   p->timing.mm_fit_rows = st.fit_rows;

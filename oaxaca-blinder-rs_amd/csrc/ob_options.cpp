@@ -24,6 +24,7 @@ constexpr Entry kNames[] = {
     {"mm_tol1", ob::Opt::MmTol1},             {"mm_fit_stride", ob::Opt::MmFitStride},
     {"mm_kappa", ob::Opt::MmKappa},           {"mm_band0", ob::Opt::MmBand0},
     {"gram_diag", ob::Opt::GramDiag},         {"l1_diag", ob::Opt::L1Diag},
+    {"debug_count_overflow", ob::Opt::DebugCountOverflow},
 };
 static_assert(sizeof(kNames) / sizeof(kNames[0]) == (size_t)ob::Opt::Count, "one name per option");
 
@@ -81,6 +82,16 @@ int ob_set_option(const char* name, double value) {
         return ob::fail(OB_E_UNSUPPORTED, "option '%s' exists only in a tuning build (make tuning)", name);
 #endif
       table()[(size_t)e.opt].store(value, std::memory_order_relaxed);
+      return OB_OK;
+    }
+  return ob::fail(OB_E_INVALID, "unknown option '%s'", name);
+}
+
+int ob_get_option(const char* name, double* value) {
+  if (!name || !value) return ob::fail(OB_E_INVALID, "null pointer");
+  for (const Entry& e : kNames)
+    if (!std::strcmp(e.name, name)) {
+      *value = table()[(size_t)e.opt].load(std::memory_order_relaxed);  // what ob_set_option stored (NaN: unset)
       return OB_OK;
     }
   return ob::fail(OB_E_INVALID, "unknown option '%s'", name);

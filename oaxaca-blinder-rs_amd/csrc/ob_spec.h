@@ -45,6 +45,12 @@
 #ifndef OB_L1_DIRECT
 #define OB_L1_DIRECT 2048u     /* rejected draws at most this many are drawn directly (OBRS-3) */
 #endif
+#if !defined(OB_TUNING) || !OB_TUNING
+/* OBRS-3 fixes both constants: another value is another stream (the oracle and the golden rows
+   use 4096 / 2048), so only a tuning build may override them. */
+static_assert(OB_L1_DIRECT == 2048u, "OB_L1_DIRECT is part of the OBRS-3 stream");
+static_assert(OB_KY_MIN_C == 4096u, "OB_KY_MIN_C is part of the OBRS-3 stream");
+#endif
 #define OB_TAG_L2 0x4F425232u  /* "OBR2" */
 
 struct ob_u32x4 {

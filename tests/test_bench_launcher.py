@@ -71,10 +71,10 @@ def test_share_runs_are_labelled_as_configs2_shares():
     """a 1,250-replicate run is configs[2]'s per-GPU share, not configs[1]; a weak
     run on several GPUs is never labelled configs[1]."""
     b = _bench()
-    assert b.workload_label("weak", None, 10000, 1, 10000).startswith("configs[1]:")
-    assert b.workload_label("weak", None, 1250, 1, 1250).startswith("configs[2]'s per-GPU share at 8 GPUs")
+    assert b.workload_label("single", None, 10000, 1, 10000).startswith("configs[1]:")
+    assert b.workload_label("single", None, 1250, 1, 1250).startswith("configs[2]'s per-GPU share at 8 GPUs")
     assert b.workload_label("strong", None, 10000, 8, 1250).startswith("configs[2]:")
-    assert "not a BASELINE config" in b.workload_label("weak", None, 3000, 1, 3000)
+    assert "not a BASELINE config" in b.workload_label("single", None, 3000, 1, 3000)
     for n in (2, 4, 8):
         lab = b.workload_label("weak", None, 10000 * n, n, 10000)
         assert lab.startswith("configs[1]'s panel, 10,000 replicates per GPU, weak"), lab
@@ -90,11 +90,23 @@ def test_default_multi_gpu_run_is_configs2_strong():
     assert b.replicate_plan(args.reps, 8, args.strong, args.weak) == ("strong", 10000, 1250)
     args = b.parse_args(["--gpus", "8", "--steps", "20", "--warmup", "5"])
     assert b.replicate_plan(args.reps, 8, args.strong, args.weak) == ("strong", 10000, 1250)
-    assert b.replicate_plan(10000, 1) == ("weak", 10000, 10000)
-    assert b.workload_label("weak", None, 10000, 1, 10000).startswith("configs[1]:")
+    assert b.replicate_plan(10000, 1) == ("single", 10000, 10000)
+    assert b.replicate_plan(1250, 1) == ("single", 1250, 1250)
+    assert b.workload_label("single", None, 10000, 1, 10000).startswith("configs[1]:")
     for n, per in ((2, 5000), (4, 2500), (8, 1250)):
         mode, total, per_rank = b.replicate_plan(10000, n)
         assert (mode, total, per_rank) == ("strong", 10000, per), n
         assert b.workload_label(mode, None, total, n, per_rank).startswith("configs[2]:")
     assert b.replicate_plan(10000, 8, weak=True) == ("weak", 80000, 10000)
     assert b.replicate_plan(10000, 8, strong=True) == ("strong", 10000, 1250)
+
+
+def test_one_gpu_line_is_labelled_single():
+    """one GPU is neither weak nor strong scaling; the N = 1 line says "single", also
+    with --weak or --strong given."""
+    b = _bench()
+    for kw in ({}, {"weak": True}, {"strong": True}):
+        assert b.replicate_plan(10000, 1, **kw)[0] == "single", kw
+    src = open(os.path.join(ROOT, "bench.py")).read()
+    assert src.count('"weak" if world > 1 else "single"') == 2  # the --mm and --heckman lines
+

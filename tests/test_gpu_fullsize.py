@@ -14,6 +14,8 @@
   property of the data: there the engine must be deterministic and its ok rows finite.
 """
 import csv
+import hashlib
+import json
 import os
 
 import numpy as np
@@ -251,14 +253,15 @@ def test_configs4_machado_mata_full_size(ob, O):
     try:
         rows, ok = panel.mm(SEED, sims, QS, 0, 2)
         t_red = panel.timing()
-        conv = {}
+        conv, betas = {}, {}
         for rep in (0xFFFFFFFF, 0, 1):  # the point pass and both replicates
             b_r, done_r = panel.debug_mm_betas(SEED, sims, rep)
             with ob._native.option("mm_reduce", 0):
                 b_f, done_f = panel.debug_mm_betas(SEED, sims, rep)
             conv[rep] = (int(done_r.size - done_r.sum()), int(done_f.size - done_f.sum()))
-            if rep == 0xFFFFFFFF:
-                point = (b_r, b_f)
+            betas[rep] = (b_r, b_f)
+        point = betas[0xFFFFFFFF]
+        rep1_counts = [panel.debug_counts(SEED, 1, 1, g)[1][0].astype(np.int64) for g in (0, 1)]
         with ob._native.option("mm_reduce", 0):
             rows0, ok0 = panel.mm(SEED, sims, QS, 0, 2)
             t_full = panel.timing()
@@ -274,6 +277,35 @@ def test_configs4_machado_mata_full_size(ob, O):
         o_r = _qr_objectives(xi, y, c, point[0][g], taus)
         o_f = _qr_objectives(xi, y, c, point[1][g], taus)
         assert np.all(np.abs(o_r - o_f) <= 1e-11 * np.abs(o_f)), np.max(np.abs(o_r - o_f) / np.abs(o_f))
+    # the HiGHS-exact optima of tests/golden/make_mm_fullsize.py (the oracle's
+    # solve_qr restatement, quantile_regression.rs:22-129) at this size -- point-pass fits of both
+    # groups at 8 taus over [0.01, 0.99] and replicate 1's first fit -- against the engine's
+    # objective at its beta on both paths, 1e-10 relative (the objective is the same at every
+    # optimal beta, so it pins degenerate faces too)
+    gold = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "mm_fullsize_objectives.json")))
+    assert (gold["rows"], gold["predictors"], gold["data_seed"], gold["simulations"], gold["seed"]) == (
+        500_000, 15, 45, sims, SEED)
+    worst = 0.0
+    for f in gold["fits"]:
+        g, rep, sim = f["group"], f["rep"], f["sim"]
+        x, y = (d["xa"], d["ya"]) if g == 0 else (d["xb"], d["yb"])
+        xi = np.hstack([np.ones((len(y), 1)), x])
+        if rep == 0xFFFFFFFF:
+            c = np.ones(len(y))
+        else:
+            assert rep == 1
+            c = rep1_counts[g]
+            assert int(c.sum()) == f["counts_sum"]
+            assert hashlib.sha256(c.astype(np.uint8).tobytes()).hexdigest() == f["counts_sha256"]
+        assert O.mm_tau(SEED, rep, sim) == f["tau"]
+        want = f["primal_objective"]
+        assert abs(f["dual_objective"] - want) <= 1e-11 * abs(want)  # HiGHS's own duality gap
+        for path in (0, 1):  # reduced, unreduced
+            got = _qr_objectives(xi, y, c, betas[rep][path][g][sim: sim + 1], [f["tau"]])[0]
+            rel = abs(got - want) / abs(want)
+            worst = max(worst, rel)
+            assert rel <= 1e-10, (g, hex(rep), sim, f["tau"], path, got, want, rel)
+    print(f"configs[4] HiGHS objectives: {len(gold['fits'])} fits x 2 paths, worst relative {worst:.2e}")
     r = rows.reshape(len(rows), len(QS), 3)
     assert np.allclose(r[..., 1] + r[..., 2], r[..., 0], rtol=0, atol=1e-9)
     assert np.allclose(rows, rows0, rtol=0, atol=1e-6 * np.abs(rows0).max()), np.abs(rows - rows0).max()

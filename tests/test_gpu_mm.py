@@ -390,3 +390,35 @@ def test_mm_after_async_boot_on_a_side_stream(ob):
         assert np.array_equal(rows.cpu().numpy(), want_rows)
     finally:
         panel.close()
+
+
+def test_mm_count_overflow_raises_and_leaves_boot_flag(ob):
+    """the Machado-Mata run reads the overflow word engine_counts writes (d_flags[2]),
+    ORed over every segment, and does not clear the boot calls' word. With the overflow forced
+    (option debug_count_overflow) mm() and debug_counts() raise OB_E_OVERFLOW; with it unset the
+    same calls succeed, and an async boot issued before mm() still reports clean."""
+    import torch
+
+    N = ob._native
+    d = mm_data(4000, 3, seed=33)
+    panel = ob.Panel(d["xa"], d["ya"], d["xb"], d["yb"])
+    try:
+        with N.option("debug_count_overflow", 1):
+            with pytest.raises(N.OaxacaError) as e:
+                panel.mm(SEED, 16, QS, 0, 3)
+            assert e.value.code == N.OB_E_OVERFLOW
+            with pytest.raises(N.OaxacaError) as e:
+                panel.debug_counts(SEED, 0, 4, 0)
+            assert e.value.code == N.OB_E_OVERFLOW
+            # the point pass alone draws no counts, so it cannot overflow
+            panel.mm(SEED, 16, QS, 0, 0)
+        rows, ok = panel.mm(SEED, 16, QS, 0, 2)
+        assert ok.all()
+        dev = torch.device("cuda", 0)
+        brow = torch.empty((64, panel.row_len), dtype=torch.float64, device=dev)
+        bok = torch.empty(64, dtype=torch.uint8, device=dev)
+        panel.boot_device(SEED, 0, 64, brow.data_ptr(), bok.data_ptr(), 0)
+        panel.mm(SEED, 16, QS, 0, 1)
+        panel.sync()  # collects the boot's flag: clean
+    finally:
+        panel.close()

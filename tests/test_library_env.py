@@ -53,3 +53,17 @@ def test_options_are_explicit(N):
     with N.option("gram_path", 1):
         pass
     N.set_option("mm_reduce", None)
+
+
+def test_option_block_restores_the_outer_value(N):
+    """option() restores what was set before the block, not the default."""
+    assert N.get_option("mm_kappa") is None
+    with N.option("mm_kappa", 3.5):
+        assert N.get_option("mm_kappa") == 3.5
+        with N.option("mm_kappa", 5.0):
+            assert N.get_option("mm_kappa") == 5.0
+        assert N.get_option("mm_kappa") == 3.5
+    assert N.get_option("mm_kappa") is None
+    v = __import__("ctypes").c_double()
+    assert N.lib().ob_get_option(b"no_such_option", __import__("ctypes").byref(v)) == N.OB_E_INVALID
+
