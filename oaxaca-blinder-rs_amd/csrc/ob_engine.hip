@@ -48,7 +48,10 @@ constexpr uint64_t kCountBudget = 24ull << 30;  // bytes of level-2 count images
 // rows per group: 2^20 tiles (level 1 walks groups past 40960 tiles as subtrees, whose LDS
 // buffers are bounded; the count images then cap a segment's replicates via kCountBudget)
 constexpr int64_t kMaxGroupRows = (int64_t)1 << 28;
-constexpr size_t kSegEvents = 6;
+#ifndef OB_BOOT_OVERLAP
+#define OB_BOOT_OVERLAP 1  // 0: level 1 and counts on the boot stream (A/B builds, tools/build_alt.sh)
+#endif
+constexpr size_t kSegEvents = 7;  // level-1 start / end, counts end (resample stream), Gram start / end, reduce end, solve end
 constexpr int kColStride = 96;  // doubles per staged column: 64 rows rotated by (c mod 32), wrap duplicated
 
 #define HIP_OK(expr)                                                                     \
@@ -336,6 +339,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
   // __syncthreads() waits for this wave's stores (vmcnt(0)) before the barrier, which is all the
   // ordering a block on one CU needs. A device-scope __threadfence() here compiled to an L2
   // write-back and invalidate per block (buffer_wbl2 / buffer_inv): 1.6 of the kernel's 3.4 ms.
+  // (Round 6 measured drawing up to 65,536 rejects directly, four per Philox call, into an LDS
+  // histogram -- configs[1]'s whole second round: level 1 1.743 against 1.729 ms, no gain: the
+  // direct draws take 32 random bits each where the tree's popcount splits take one per level.)
   __syncthreads();
   for (uint32_t r = tid; r < todo; r += kBlock) {  // direct draws: Lemire over [0, n)
     const uint32_t thresh = (0u - n) % n;
@@ -1821,10 +1827,15 @@ int engine_order(ob_panel* p, hipStream_t s) {
   return OB_OK;
 }
 
-int engine_mark(ob_panel* p, hipStream_t s) {
+int engine_mark(ob_panel* p, hipStream_t s, bool scratch) {
   if (!p->order_ev) HIP_OK(hipEventCreateWithFlags(&p->order_ev, hipEventDisableTiming));
   HIP_OK(hipEventRecord(p->order_ev, s));
   p->order_stream = s;
+  if (scratch) {
+    if (!p->scratch_ev) HIP_OK(hipEventCreateWithFlags(&p->scratch_ev, hipEventDisableTiming));
+    HIP_OK(hipEventRecord(p->scratch_ev, s));
+    p->scratch_recorded = true;
+  }
   return OB_OK;
 }
 
@@ -1910,6 +1921,19 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     HIP_OK(hipEventCreate(&e));
     p->seg_events.push_back(e);
   }
+  // the resample stream (ob_engine.hpp): level 1 and counts wait only for the previous call's last
+  // read of the count images, not for its reduce / solve / gather
+  const bool overlap = OB_BOOT_OVERLAP && !p->heckman;
+  if (overlap) {
+    if (!p->rs_stream) HIP_OK(hipStreamCreateWithFlags(&p->rs_stream, hipStreamNonBlocking));
+    if (!p->rs_ev) HIP_OK(hipEventCreateWithFlags(&p->rs_ev, hipEventDisableTiming));
+    if (!p->scratch_ev) HIP_OK(hipEventCreateWithFlags(&p->scratch_ev, hipEventDisableTiming));
+    if (!p->scratch_recorded) {  // no engine call on this panel yet: start where s is
+      HIP_OK(hipEventRecord(p->scratch_ev, s));
+      p->scratch_recorded = true;
+    }
+  }
+  const hipStream_t sr = overlap ? p->rs_stream : s;
   for (uint64_t s0 = 0; s0 < n_reps; s0 += seg) {
     const uint32_t ns = (uint32_t)std::min<uint64_t>(seg, n_reps - s0);
     const Plan& plx = (ns == seg) ? pl : pl_tail;
@@ -1917,11 +1941,12 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     const uint32_t frep = (uint32_t)(first_rep + s0);
     hipEvent_t* ev = p->seg_events.data() + kSegEvents * (size_t)p->pending_segments;
     const bool timed = true;
-    if (timed) HIP_OK(hipEventRecord(ev[0], s));
-    hipLaunchKernelGGL(l1k, dim3(ns, 2), dim3(kBlock), lds_l1, s, p->n[0], p->n[1], p->ntiles[0], frep,
+    if (overlap) HIP_OK(hipStreamWaitEvent(sr, p->scratch_ev, 0));
+    if (timed) HIP_OK(hipEventRecord(ev[0], sr));
+    hipLaunchKernelGGL(l1k, dim3(ns, 2), dim3(kBlock), lds_l1, sr, p->n[0], p->n[1], p->ntiles[0], frep,
                        tiles, key0, key1, p->d_m1, ky);
     HIP_OK(hipGetLastError());
-    if (timed) HIP_OK(hipEventRecord(ev[1], s));
+    if (timed) HIP_OK(hipEventRecord(ev[1], sr));
     GramArgs ga = gram_args(p, plx);
     ga.chunks = p->d_chunks;
     ga.m1 = p->d_m1;
@@ -1934,24 +1959,34 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     ga.tiles_total = tiles;
     ga.diag = diag_mode();
     const dim3 cgrid((tiles + kCntTilesPerBlock - 1) / kCntTilesPerBlock, plx.nb_rep);
-    if (use_i8) hipLaunchKernelGGL(ob_count_kernel<true>, cgrid, dim3(kBlock), 0, s, ga);
-    else hipLaunchKernelGGL(ob_count_kernel<false>, cgrid, dim3(kBlock), 0, s, ga);
+    if (use_i8) hipLaunchKernelGGL(ob_count_kernel<true>, cgrid, dim3(kBlock), 0, sr, ga);
+    else hipLaunchKernelGGL(ob_count_kernel<false>, cgrid, dim3(kBlock), 0, sr, ga);
     HIP_OK(hipGetLastError());
-    if (timed) HIP_OK(hipEventRecord(ev[2], s));
+    if (timed) HIP_OK(hipEventRecord(ev[2], sr));
+    if (overlap) {
+      HIP_OK(hipEventRecord(p->rs_ev, sr));
+      HIP_OK(hipStreamWaitEvent(s, p->rs_ev, 0));
+    }
+    if (timed) HIP_OK(hipEventRecord(ev[3], s));
     if (use_i8) {
       OB_TRY(ob::oz_gram(p, p->d_chunks, nchx, p->d_counts, plx.nb_rep, plx.rep_pad, ns, p->d_partial, s));
     } else {
       const uint32_t blocks = plx.nb_rep * plx.n_cg * (uint32_t)nchx;
       HIP_OK(launch_gram(p, plx.cb, false, ga, blocks, s));
     }
-    if (timed) HIP_OK(hipEventRecord(ev[3], s));
+    if (timed) HIP_OK(hipEventRecord(ev[4], s));
+    const bool exc = use_i8 && ob::oz_exceptions_pending(p);
+    if (overlap && !exc) HIP_OK(hipEventRecord(p->scratch_ev, s));  // the count images are free again
     const size_t nred = (size_t)ns * p->e_pad;
     hipLaunchKernelGGL(ob_reduce_kernel, dim3((unsigned)((nred + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
                        (const double*)p->d_partial, (const uint32_t*)p->d_chunks, nchx, plx.rep_pad, p->e_pad, ns,
                        p->d_gram);
     HIP_OK(hipGetLastError());
-    if (use_i8) OB_TRY(ob::oz_exceptions(p, p->d_counts, plx.nb_rep, ns, p->d_gram, s));
-    if (timed) HIP_OK(hipEventRecord(ev[4], s));
+    if (exc) {
+      OB_TRY(ob::oz_exceptions(p, p->d_counts, plx.nb_rep, ns, p->d_gram, s));
+      if (overlap) HIP_OK(hipEventRecord(p->scratch_ev, s));
+    }
+    if (timed) HIP_OK(hipEventRecord(ev[5], s));
     if (p->heckman) {  // probit iterations + IMR sums + two-step solve (synchronizes the stream)
       ob_heck_seg hs = heck_seg(p, plx, p->d_chunks, p->d_gram, ref_mode);
       hs.counts = p->d_counts;
@@ -1980,13 +2015,13 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
       sa.raw_status = 0;
       HIP_OK(launch_solve(p, sa, ns, s));
     }
-    if (timed) HIP_OK(hipEventRecord(ev[5], s));
+    if (timed) HIP_OK(hipEventRecord(ev[6], s));
     p->timing.gram_launches += 1;
     p->pending_segments += 1;
   }
   p->timing_pending = true;
   p->last_stream = s;
-  return engine_mark(p, s);
+  return engine_mark(p, s, !overlap);
 }
 
 // Synchronize the last boot run, sum its per-segment kernel timings and check the
@@ -1996,11 +2031,13 @@ int engine_collect(ob_panel* p) {
   HIP_OK(hipSetDevice(p->ctx->device));
   HIP_OK(hipStreamSynchronize(p->last_stream));
   p->timing_pending = false;
-  double* dst[kSegEvents - 1] = {&p->timing.level1_ms, &p->timing.counts_ms, &p->timing.gram_ms,
+  // (ev[2] -> ev[3] is the Gram's wait for the previous call's tail on the boot stream: not a kernel)
+  double* dst[kSegEvents - 1] = {&p->timing.level1_ms, &p->timing.counts_ms, nullptr, &p->timing.gram_ms,
                                  &p->timing.reduce_ms, &p->timing.solve_ms};
   for (int sg = 0; sg < p->pending_segments; ++sg) {
     hipEvent_t* ev = p->seg_events.data() + kSegEvents * (size_t)sg;
     for (size_t i = 0; i + 1 < kSegEvents; ++i) {
+      if (!dst[i]) continue;
       float t = 0.f;
       HIP_OK(hipEventElapsedTime(&t, ev[i], ev[i + 1]));
       *dst[i] += t;
@@ -2246,6 +2283,10 @@ void ob_panel_destroy(ob_panel* p) {
   (void)hipFree(p->d_ok_tmp);
   (void)hipFree(p->d_pe);
   (void)hipFree(p->d_pe_ok);
+  if (p->rs_stream) (void)hipStreamSynchronize(p->rs_stream);
+  if (p->rs_ev) (void)hipEventDestroy(p->rs_ev);
+  if (p->scratch_ev) (void)hipEventDestroy(p->scratch_ev);
+  if (p->rs_stream) (void)hipStreamDestroy(p->rs_stream);
   ob::shard_free(p);
   ob::oz_free(p);
   (void)hipFree(p->d_mm_fail);

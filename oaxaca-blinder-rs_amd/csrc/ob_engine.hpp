@@ -134,6 +134,14 @@ struct ob_panel {
   // for order_ev, recorded after the previous call's last kernel (engine_order / engine_mark)
   hipEvent_t order_ev = nullptr;
   hipStream_t order_stream = nullptr;
+  // A boot's level-1 and count kernels run on the panel's resample stream (rs_stream), so that they
+  // start as soon as the previous call has stopped reading the count images (scratch_ev: after its
+  // Gram, or the end of a call of another kind) and overlap that call's reduce / solve / gather;
+  // the Gram waits for them (rs_ev). Heckman panels keep one stream (their passes read the images
+  // after the Gram).
+  hipStream_t rs_stream = nullptr;
+  hipEvent_t rs_ev = nullptr, scratch_ev = nullptr;
+  bool scratch_recorded = false;
 };
 
 namespace ob {
@@ -143,7 +151,9 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
 int engine_collect(ob_panel* p);
 // make stream s wait for the panel's previous call when that ran on another stream / mark s as it
 int engine_order(ob_panel* p, hipStream_t s);
-int engine_mark(ob_panel* p, hipStream_t s);
+// scratch: also mark the end of this call's use of d_m1 / d_counts (a boot marks that itself, after
+// its last Gram, so its reduce / solve / gather overlap the next boot's resample)
+int engine_mark(ob_panel* p, hipStream_t s, bool scratch = true);
 int engine_counts(ob_panel* p, uint64_t seed, uint64_t first_rep, uint32_t n_reps, hipStream_t s,
                   uint32_t* nb_rep, uint32_t* rep_pad);
 // ob_gram_i8.hip
@@ -151,6 +161,7 @@ int oz_prepare(ob_panel* p, hipStream_t s);
 int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t* counts, uint32_t nb_rep,
             uint32_t rep_pad, uint32_t n_reps, double* partial, hipStream_t s);
 // adds the exception rows' f64 terms to the reduced Grams [rep][2][e_pad] of a segment
+bool oz_exceptions_pending(const ob_panel* p);
 int oz_exceptions(ob_panel* p, const uint32_t* counts, uint32_t nb_rep, uint32_t n_reps, double* gram, hipStream_t s);
 // after the stream is synchronized: exception count / bits into p->timing, overflow -> error
 int oz_collect(ob_panel* p);

@@ -952,6 +952,9 @@ int oz_prepare(ob_panel* p, hipStream_t s) {
   return OB_OK;
 }
 
+// Whether oz_exceptions launches a kernel (which reads the count images after the reduce).
+bool oz_exceptions_pending(const ob_panel* p) { return p->oz_state == 1 && p->oz_nexc != 0; }
+
 // The exception rows' f64 terms of one segment (after ob_reduce_kernel). Skipped once a synchronized
 // run has shown the panel has none.
 int oz_exceptions(ob_panel* p, const uint32_t* counts, uint32_t nb_rep, uint32_t n_reps, double* gram, hipStream_t s) {

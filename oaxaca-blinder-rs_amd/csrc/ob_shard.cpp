@@ -207,7 +207,7 @@ int shard_deliver(ob_panel* p, const Shard& sh, int world, uint64_t n_reps, doub
     SH_HIP(hipMemcpyAsync(rows, drows, sizeof(double) * ny * n_reps * rl, hipMemcpyDeviceToHost, s));
     SH_HIP(hipMemcpyAsync(ok, dok, ny * n_reps, hipMemcpyDeviceToHost, s));
   }
-  return ob::engine_mark(p, s);
+  return ob::engine_mark(p, s, false);  // the gather reads no count image: scratch stays as the boot left it
 }
 
 bool valid_ref(int m) { return m >= OB_REF_GROUP_A && m <= OB_REF_NEUMARK; }
