@@ -724,6 +724,7 @@ def main():
     launches = tm["gram_launches"]
     gram_path = tm["gram_path"]
     tiles6 = (tm["oz_tiles6"], tm["oz_tiles"])
+    gram_kernel = "oz_gram_w_kernel" if tm["oz_wide"] else "oz_gram_kernel"
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -758,7 +759,7 @@ def main():
             roof = {"bound": "mfma", "achieved": i8_tops, "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS (i8)",
                     "frac": i8_tops / I8_MFMA_PEAK_TOPS, "traffic": traffic,
                     "traffic_source": "profiles/pmc_gram_i8.json (PMC 2 x FETCH_SIZE + WRITE_SIZE, final round-5 tree, profiles/r05_final_pmc_gram.json)",
-                    "kernel": "oz_gram_kernel",
+                    "kernel": gram_kernel,
                     "avg_launch_ms": gram_launch_ms, "i8_ops_per_replicate": ops_rep,
                     "i8_ops_issued_per_replicate": ops_issued, "digit_slices_mean": slices,
                     "tiles_on_6_slices": list(tiles6),

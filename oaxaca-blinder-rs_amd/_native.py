@@ -82,7 +82,7 @@ class ob_timing(C.Structure):
                 ("probit_ms", C.c_double), ("probit_launches", C.c_int32), ("heck_sums_ms", C.c_double),
                 ("mm_reduced", C.c_int32), ("mm_retried", C.c_int64), ("prep_ms", C.c_double),
                 ("oz_exceptions", C.c_int32), ("oz_bits", C.c_int32), ("oz_tiles6", C.c_int32),
-                ("oz_tiles", C.c_int32)]
+                ("oz_tiles", C.c_int32), ("oz_wide", C.c_int32)]
 
 
 class ob_unique_id(C.Structure):

@@ -474,6 +474,7 @@ struct OzArgs {
   double* partial;         // [chunk][rep_pad][e_pad]
   uint32_t n0, n1, tiles0, nb_rep, n_reps, rep_pad, n_rt;
   int n_ct, e_pad, n_pairs_pad;
+  int n_dct;  // oz_gram_w_kernel: column-tile pairs (64 pairs)
 };
 
 constexpr int kWaves = 8;                         // 2 per SIMD: (replicate batch, slice group)
@@ -822,6 +823,223 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Wide tile (round 6): one wave per SIMD, a block = 4 waves = (chunk, 256 replicates, 64 pairs).
+// Wave w owns replicate batch w and every digit slice of both 32-pair column tiles: per 64-row
+// sub-tile 4 replicate blocks x 6 slices x 4 pair blocks = 96 v_mfma_i32_16x16x64_i8 against one
+// 4 KB A load (its batch's count fragments, no longer loaded twice, once per slice group) and
+// 24 KB of B (both column tiles' six slices, LDS-DMA into a 4-stage ring, one barrier per sub-tile).
+// 384 accumulator registers (AGPRs) per wave: the block tile is twice the 8-wave kernel's, so each
+// A byte meets twice the MFMAs, and the four waves' A loads (16 KB per sub-tile, half of the
+// 8-wave kernel's 32 KB) plus B (24 KB per 64 pairs) are 40 KB per 384 MFMAs against 44 KB per
+// 192. The slice sums meet exactly as in oz_gram_body (slices 0-3 and 4-5 / 4-6 in int64, one
+// rounding each, then their sum): the partials are bitwise the 8-wave kernel's. A column-tile
+// pair whose tiles do not both run six slices takes its tiles one pass each (NH = 2).
+// ---------------------------------------------------------------------------------------------
+constexpr int kWNbuf = 4;  // ring stages (sub-tiles)
+constexpr int kWAgprTiles = 64;  // accumulator tiles (4 registers each) pinned to AGPRs
+constexpr size_t kWLds = kWNbuf * (size_t)2 * kS * 2 * 64 * 16;  // 4 x 28 KB (seven slices, one tile: 14 KB)
+
+__device__ __forceinline__ void oz_map_w(const OzArgs& a, uint32_t* dct, uint32_t* rt, uint32_t* chunk) {
+  // oz_map's chunk-major raster over groups of n_dct blocks
+  const uint32_t nwg = gridDim.x, bid = blockIdx.x, nct = (uint32_t)a.n_dct;
+  const uint32_t sgb = 8u * nct, sg = bid / sgb, r = bid - sg * sgb;
+  const uint32_t left = nwg - sg * sgb;
+  uint32_t grp, c;
+  if (left >= sgb) {
+    grp = sg * 8u + (r & 7u);
+    c = r >> 3;
+  } else {
+    const uint32_t ng = left / nct;
+    grp = sg * 8u + r % ng;
+    c = r / ng;
+  }
+  *dct = c;
+  *rt = grp % a.n_rt;
+  *chunk = grp / a.n_rt;
+}
+
+// NS digit slices (6 or 7), NH 16-pair blocks per pass (4: column tiles ct0, ct0 + 1; 2: ct0 only),
+// NB this wave's DMA pieces per sub-tile, LIVE its replicate batch exists.
+template <int NS, int NH, int NB, bool LIVE>
+__device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* smem, int wave, uint32_t ct0,
+                                               uint32_t rt, uint32_t chunk) {
+  constexpr int NC = NH / 2;                 // column tiles in this pass
+  constexpr int PIECES = NC * NS * 2;        // 1 KB DMA pieces per sub-tile
+  constexpr int STAGE = PIECES * 64;         // 16-byte units per ring stage
+  constexpr int PER = 2 * NB + (LIVE ? 12 : 0);  // vector-memory ops newer than the stage to publish
+  const ob_v4i* bs = reinterpret_cast<const ob_v4i*>(smem);
+  const int lane = threadIdx.x & 63;
+  const uint32_t g = a.chunks[3 * chunk];
+  const uint32_t n = g ? a.n1 : a.n0, tg0 = g ? a.tiles0 : 0u;
+  const uint32_t s0 = a.chunks[3 * chunk + 1] * 4u;
+  const uint32_t s1 = min(a.chunks[3 * chunk + 2] * 4u, (n + 63u) >> 6);
+  const ob_v4i* Bg = g ? a.B1 : a.B0;
+  const uint32_t batch = rt * 4u + (uint32_t)wave;
+  auto dma = [&](int buf, uint32_t s) {
+#pragma unroll
+    for (int t = 0; t < NB; ++t) {
+      const int piece = t * 4 + wave, c = piece / (NS * 2), q = piece - c * (NS * 2);
+      const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct0 + c) * kSubUnits + q * 64;
+      oz_dma16(src + lane, (uint32_t)(buf * STAGE + piece * 64) * 16u);
+    }
+  };
+  ob_v4i ar[3][4];
+  auto aload = [&](ob_v4i (&dst)[4], uint32_t s) {
+    const ob_v4i* src_a = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256 + lane;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) dst[m] = src_a[m * 64];
+  };
+  // B fragments of pair block h: column tile h >> 1, half h & 1, every slice
+  auto read = [&](int buf, int h, ob_v4i (&bf)[NS]) {
+    const ob_v4i* bb = bs + buf * STAGE + ((h >> 1) * NS * 2 + (h & 1)) * 64 + lane;
+#pragma unroll
+    for (int q = 0; q < NS; ++q) bf[q] = bb[q * 128];
+  };
+  // 4 x NS x NH accumulator tiles: the first kWAgprTiles live in AGPRs (inline-asm MFMAs with an "a"
+  // constraint), the rest in VGPRs. Left to itself the compiler copies accumulators between the two
+  // files and spills (tools/mfma_acc_probe.hip); pinned, 256 AGPRs + ~230 VGPRs hold the loop.
+  ob_v4i acc[4][NS][NH];
+#pragma unroll
+  for (int m = 0; m < 4; ++m)
+#pragma unroll
+    for (int q = 0; q < NS; ++q)
+#pragma unroll
+      for (int h = 0; h < NH; ++h) acc[m][q][h] = (ob_v4i){};
+  auto mfmas = [&](int h, const ob_v4i (&af)[4], const ob_v4i (&bf)[NS]) {
+#pragma unroll
+    for (int q = 0; q < NS; ++q)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        if ((m * NS + q) * NH + h < kWAgprTiles)
+          asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+a"(acc[m][q][h]) : "v"(af[m]), "v"(bf[q]));
+        else
+          asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+v"(acc[m][q][h]) : "v"(af[m]), "v"(bf[q]));
+      }
+  };
+  // prologue (as oz_gram_body): A of s0 .. s0 + 2 and B of s0 .. s0 + 3 in flight, then publish
+  if constexpr (LIVE) {
+    aload(ar[0], s0);
+    aload(ar[1], min(s0 + 1, s1 - 1));
+    aload(ar[2], min(s0 + 2, s1 - 1));
+  }
+#pragma unroll
+  for (int j = 0; j < kWNbuf; ++j)
+    if (s0 + j < s1) dma(j, s0 + j);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  ob_v4i fb[2][NS];
+  if constexpr (LIVE) read(0, 0, fb[0]);
+  // Step s: MFMAs of pair blocks 0 .. NH - 2 while the next block's B is read; wait + barrier (stage
+  // s + 1 landed, every read of stage s done); refill stage s with B of s + 4; read (s + 1, 0); MFMAs
+  // of the last block; A of s + 3 into the slot s frees. At barrier s the loads newer than B(s + 1)
+  // (issued right after barrier s - 3) are A(s), B(s + 2), A(s + 1), B(s + 3), A(s + 2): PER. Every
+  // step issues the same loads (past the end: the last sub-tile again), so every wait is the same.
+  auto step = [&](uint32_t s, auto J) {
+    constexpr int j = decltype(J)::value;
+    const int buf = (int)((s - s0) & (kWNbuf - 1));
+    if constexpr (LIVE) {
+#pragma unroll
+      for (int h = 0; h + 1 < NH; ++h) {
+        read(buf, h + 1, fb[(h + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        mfmas(h, ar[j], fb[h & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+    oz_barrier();
+    dma(buf, min(s + kWNbuf, s1 - 1));
+    if constexpr (LIVE) {
+      read((buf + 1) & (kWNbuf - 1), 0, fb[NH & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      mfmas(NH - 1, ar[j], fb[(NH - 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      aload(ar[j], min(s + 3, s1 - 1));
+    }
+  };
+  uint32_t s = s0;
+  for (; s + 3 <= s1; s += 3) {
+    step(s, IC<0>{});
+    step(s + 1, IC<1>{});
+    step(s + 2, IC<2>{});
+  }
+  if (s < s1) step(s, IC<0>{});
+  if (s + 1 < s1) step(s + 1, IC<1>{});
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing DMAs (past the end) have landed
+  __syncthreads();  // every wave is done with the ring: the epilogue stages accumulators in it
+  if constexpr (LIVE) {
+    // slices -> f64 exactly as oz_gram_body: slices 0-3 and 4 .. NS - 1 each in int64, one ldexp
+    // each, then their sum (the 8-wave kernel's group-0 value plus its group-1 value). One pair
+    // block at a time through this wave's quarter of the ring (a lane reads back only its own
+    // words), so the int64 arithmetic never holds every accumulator in VGPRs at once.
+    ob_v4i* st = reinterpret_cast<ob_v4i*>(smem) + (size_t)wave * (4 * NS * 64);
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int q = 0; q < NS; ++q) st[(m * NS + q) * 64 + lane] = acc[m][q][h];
+      __builtin_amdgcn_sched_barrier(0);
+      const int pair = (int)(ct0 + (h >> 1)) * kPairsPerTile + 16 * (h & 1) + (lane & 15);
+      const int E = a.pexp[chunk * a.n_pairs_pad + min(pair, a.n_pairs_pad - 1)];
+      const int sh0 = E - kFracBits + 8 * (kS - 0 - kSlo), sh1 = E - kFracBits + 8 * (kS - kSlo - (NS - kSlo));
+#pragma unroll
+      for (int m = 0; m < 4; ++m)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          long long p0 = 0, p1 = 0;
+#pragma unroll
+          for (int q = 0; q < kSlo; ++q) p0 = p0 * 256 + st[(m * NS + q) * 64 + lane][i];
+#pragma unroll
+          for (int q = kSlo; q < NS; ++q) p1 = p1 * 256 + st[(m * NS + q) * 64 + lane][i];
+          const double val = ldexp((double)p0, sh0) + ldexp((double)p1, sh1);
+          const uint32_t rep = batch * 64u + (uint32_t)(16 * m + 4 * (lane >> 4) + i);
+          if (pair < a.e_pad && rep < a.n_reps) a.partial[((size_t)chunk * a.rep_pad + rep) * a.e_pad + pair] = val;
+        }
+    }
+  }
+  __syncthreads();  // the staging is done before a next pass refills the ring
+}
+
+template <int NS, int NH, bool LIVE>
+__device__ __forceinline__ void oz_gram_w_pass(const OzArgs& a, unsigned char* smem, int wave, uint32_t ct0,
+                                               uint32_t rt, uint32_t chunk) {
+  constexpr int P = (NH / 2) * NS * 2;  // pieces per sub-tile, dealt round-robin over the 4 waves
+  if (wave < P % 4 || P % 4 == 0) oz_gram_w_body<NS, NH, (P + 3) / 4, LIVE>(a, smem, wave, ct0, rt, chunk);
+  else oz_gram_w_body<NS, NH, P / 4, LIVE>(a, smem, wave, ct0, rt, chunk);
+}
+
+template <int NS, int NH>
+__device__ __forceinline__ void oz_gram_w_pass_live(const OzArgs& a, unsigned char* smem, int wave, uint32_t ct0,
+                                                    uint32_t rt, uint32_t chunk, bool live) {
+  if (live) oz_gram_w_pass<NS, NH, true>(a, smem, wave, ct0, rt, chunk);
+  else oz_gram_w_pass<NS, NH, false>(a, smem, wave, ct0, rt, chunk);
+}
+
+__global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void oz_gram_w_kernel(const OzArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t dct, rt, chunk;
+  oz_map_w(a, &dct, &rt, &chunk);
+  const bool live = rt * 4u + (uint32_t)wave < a.nb_rep;
+  const uint32_t ct0 = 2u * dct;
+  const bool two = (int)ct0 + 1 < a.n_ct;
+  const bool six0 = a.nsl[chunk * (uint32_t)a.n_ct + ct0] == 6;
+  const bool six1 = two && a.nsl[chunk * (uint32_t)a.n_ct + ct0 + 1] == 6;
+  if (two && six0 && six1) {
+    oz_gram_w_pass_live<6, 4>(a, smem, wave, ct0, rt, chunk, live);
+    return;
+  }
+  // a seven-slice tile (or a lone last tile): one column tile per pass
+  if (six0) oz_gram_w_pass_live<6, 2>(a, smem, wave, ct0, rt, chunk, live);
+  else oz_gram_w_pass_live<7, 2>(a, smem, wave, ct0, rt, chunk, live);
+  if (!two) return;
+  if (six1) oz_gram_w_pass_live<6, 2>(a, smem, wave, ct0 + 1, rt, chunk, live);
+  else oz_gram_w_pass_live<7, 2>(a, smem, wave, ct0 + 1, rt, chunk, live);
+}
+
 }  // namespace
 
 namespace ob {
@@ -1036,7 +1254,27 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
   a.n_ct = p->oz_n_ct;
   a.e_pad = p->e_pad;
   a.n_pairs_pad = p->oz_n_ct * kPairsPerTile;
-  const uint32_t blocks = (uint32_t)n_chunks * a.n_rt * (uint32_t)a.n_ct;
+  a.n_dct = (a.n_ct + 1) / 2;
+  // Which kernel: the wide tile does a block's work (twice the 8-wave kernel's) in kWideCost of the
+  // 8-wave kernel's block time (configs[1]: 11.09 against 11.65 ms per launch, profiles/
+  // r06_ab_gram_wide.txt), but has half as many blocks, so a small launch wastes more of its last
+  // round over the CUs (configs[2]'s 1,250-replicate share: 640 blocks, 2.5 rounds, 1.81 against
+  // 1.56 ms). Rounds x cost decides; both kernels give bitwise the same partials.
+  const uint32_t wblocks = (uint32_t)n_chunks * a.n_rt * (uint32_t)a.n_dct;
+  const uint32_t blocks8 = (uint32_t)n_chunks * a.n_rt * (uint32_t)a.n_ct;
+  const uint32_t cus = (uint32_t)std::max(p->ctx->cus, 1);
+  const double kWideCost = 1.9;
+  const bool wide_pays = kWideCost * (double)((wblocks + cus - 1) / cus) <= (double)((blocks8 + cus - 1) / cus);
+  const int tile = ob::opt_int(ob::Opt::GramTile, 0);
+  const bool wide = tile == 2 || (tile != 1 && wide_pays);
+  p->timing.oz_wide = wide ? 1 : 0;
+  if (wide) {  // oz_gram_w_kernel: 4 waves, 256 replicates x 64 pairs per block
+    OZ_HIP(hipFuncSetAttribute((const void*)oz_gram_w_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWLds));
+    hipLaunchKernelGGL(oz_gram_w_kernel, dim3(wblocks), dim3(256), kWLds, s, a);
+    OZ_HIP(hipGetLastError());
+    return OB_OK;
+  }
+  const uint32_t blocks = blocks8;
   auto launch = [&](auto kern) -> hipError_t {
     hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kLdsBytes);
     if (e != hipSuccess) return e;

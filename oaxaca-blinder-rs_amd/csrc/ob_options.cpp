@@ -24,7 +24,7 @@ constexpr Entry kNames[] = {
     {"mm_tol1", ob::Opt::MmTol1},             {"mm_fit_stride", ob::Opt::MmFitStride},
     {"mm_kappa", ob::Opt::MmKappa},           {"mm_band0", ob::Opt::MmBand0},
     {"gram_diag", ob::Opt::GramDiag},         {"l1_diag", ob::Opt::L1Diag},
-    {"debug_count_overflow", ob::Opt::DebugCountOverflow},
+    {"gram_tile", ob::Opt::GramTile},         {"debug_count_overflow", ob::Opt::DebugCountOverflow},
 };
 static_assert(sizeof(kNames) / sizeof(kNames[0]) == (size_t)ob::Opt::Count, "one name per option");
 

@@ -328,3 +328,36 @@ def test_nonfinite_rows_touch_only_replicates_that_draw_them(ob, O):
     assert np.array_equal(fin, np.isfinite(rows))
     gap = abs(float(np.nanmedian(orows[:, 5])))
     assert np.all(np.abs(rows[fin] - orows[fin]) <= 1e-6 * np.maximum(np.abs(orows[fin]), gap))
+
+
+@pytest.mark.parametrize("n,p,weighted,heavy,reps", [
+    (400_000, 20, True, False, 300),  # configs[1]-like: every column-tile pair on six slices
+    (400_000, 20, True, True, 70),    # a heavy-tailed column: seven-slice tiles, one tile per pass
+    (20001, 5, False, False, 131),    # 28 pairs: one column tile, the pair's second tile absent
+    (9000, 14, True, False, 64),      # 136 pairs: five column tiles, the last pair lone
+    (2600, 40, False, False, 200),    # 903 pairs: 29 column tiles
+])
+def test_wide_tile_gram_bitwise(ob, O, n, p, weighted, heavy, reps):
+    """The two i8 Gram kernels (option gram_tile: 1 = 8 waves x 32 pairs, oz_gram_kernel; 2 = 4
+    waves x 64 pairs with AGPR accumulators, oz_gram_w_kernel) form the same exact integer slice
+    sums and combine them with the same two roundings, so their Grams are bitwise equal, partial
+    replicate tiles (reps % 256 != 0) and dead batches included."""
+    d = O.synthetic_panel(n, p, weighted, seed=n + p + 7)
+    xa, xb = d["xa"].copy(), d["xb"].copy()
+    if heavy:
+        rng = np.random.default_rng(9)
+        xa[:, 4] = np.exp(rng.normal(0.0, 1.5, xa.shape[0]))
+        xb[:, 4] = np.exp(rng.normal(0.0, 1.5, xb.shape[0]))
+    panel = ob.Panel(xa, d["ya"], xb, d["yb"], d["wa"], d["wb"])
+    try:
+        got = {}
+        for tile in (1, 2):
+            with ob._native.option("gram_tile", tile):
+                got[tile] = panel.debug_gram(SEED, 5, reps, path=2)
+                t = panel.timing()
+                assert t["gram_path"] == 2
+        if heavy:
+            assert 0 < t["oz_tiles6"] < t["oz_tiles"]
+        assert np.array_equal(got[1], got[2], equal_nan=True)
+    finally:
+        panel.close()

@@ -66,3 +66,22 @@ def test_checker_flags_a_register_reused_under_a_load():
 """
     found = C.check(C.parse(text))
     assert [(r, a) for r, a, _ in found] == [("vgpr-busy", 0x1008)]
+
+
+WIDE = "_ZN12_GLOBAL__N_116oz_gram_w_kernelENS_6OzArgsE"  # oz_gram_w_kernel: the wide tile (round 6)
+
+
+def test_shipped_wide_gram_kernel_waits_are_clean():
+    """The wide-tile kernel uses the same untracked LDS-DMA ring with hand-counted waits (a 4-stage
+    ring, one barrier per sub-tile, PER = 2 NB + 12) and pins its accumulators to AGPRs through
+    inline-asm MFMAs: the walk must find no DMA older than two barriers at a barrier and no
+    register (VGPR or AGPR) touched under an un-waited load."""
+    if not os.path.exists(SO) or not os.path.exists(os.path.join(C.LLVM, "llvm-objdump")):
+        pytest.skip("engine library or llvm-objdump missing (run __graft_entry__.build())")
+    isa = C.disassemble_symbol(SO, WIDE)
+    insns = C.parse(isa, WIDE)
+    dma = sum(1 for i in insns if i.mnem.startswith("global_load_lds"))
+    bars = sum(1 for i in insns if i.mnem == "s_barrier")
+    mfma = sum(1 for i in insns if i.mnem.startswith("v_mfma_i32_16x16x64_i8"))
+    assert dma >= 64 and bars >= 40 and mfma >= 1000, (len(insns), dma, bars, mfma)
+    assert C.check(insns) == []
