@@ -836,16 +836,28 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
 // rounding each, then their sum): the partials are bitwise the 8-wave kernel's. A column-tile
 // pair whose tiles do not both run six slices takes its tiles one pass each (NH = 2).
 // ---------------------------------------------------------------------------------------------
+#ifndef OB_OZ_W_SPREAD
+#define OB_OZ_W_SPREAD 0
+#endif
 constexpr int kWNbuf = 4;  // ring stages (sub-tiles)
 constexpr int kWAgprTiles = 64;  // accumulator tiles (4 registers each) pinned to AGPRs
-constexpr size_t kWLds = kWNbuf * (size_t)2 * kS * 2 * 64 * 16;  // 4 x 28 KB (seven slices, one tile: 14 KB)
+// 4 stages of B (two six-slice tiles: 24 KB; one seven-slice tile: 14 KB) + A (16 KB)
+constexpr size_t kWLds = kWNbuf * (size_t)(2 * 6 * 2 * 64 + 4 * 4 * 64) * 16;
 
+#ifndef OB_OZ_W_RASTER
+#define OB_OZ_W_RASTER 0
+#endif
+// Block -> (column-tile pair, replicate tile, chunk); a group is the n_dct blocks of one (chunk,
+// replicate tile) and shares that tile's count images. OB_OZ_W_RASTER 0: each XCD sweeps a
+// contiguous eighth of the groups, so its 32 CUs hold 32 / n_dct consecutive replicate tiles of
+// one chunk at once and read each B sub-tile of the chunk from L2 that many times per fetch;
+// 1: oz_map's chunk-major deal of groups over the XCDs (every XCD streams the chunk's B).
 __device__ __forceinline__ void oz_map_w(const OzArgs& a, uint32_t* dct, uint32_t* rt, uint32_t* chunk) {
-  // oz_map's chunk-major raster over groups of n_dct blocks
   const uint32_t nwg = gridDim.x, bid = blockIdx.x, nct = (uint32_t)a.n_dct;
+  uint32_t grp, c;
+#if OB_OZ_W_RASTER
   const uint32_t sgb = 8u * nct, sg = bid / sgb, r = bid - sg * sgb;
   const uint32_t left = nwg - sg * sgb;
-  uint32_t grp, c;
   if (left >= sgb) {
     grp = sg * 8u + (r & 7u);
     c = r >> 3;
@@ -854,6 +866,12 @@ __device__ __forceinline__ void oz_map_w(const OzArgs& a, uint32_t* dct, uint32_
     grp = sg * 8u + r % ng;
     c = r / ng;
   }
+#else
+  const uint32_t xcd = bid & 7u, slot = bid >> 3, q8 = nwg >> 3, r8 = nwg & 7u;
+  const uint32_t wi = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  grp = wi / nct;
+  c = wi - grp * nct;
+#endif
   *dct = c;
   *rt = grp % a.n_rt;
   *chunk = grp / a.n_rt;
@@ -861,13 +879,18 @@ __device__ __forceinline__ void oz_map_w(const OzArgs& a, uint32_t* dct, uint32_
 
 // NS digit slices (6 or 7), NH 16-pair blocks per pass (4: column tiles ct0, ct0 + 1; 2: ct0 only),
 // NB this wave's DMA pieces per sub-tile, LIVE its replicate batch exists.
-template <int NS, int NH, int NB, bool LIVE>
+template <int NS, int NH, int NB, bool LIVE, int DIAG>
 __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* smem, int wave, uint32_t ct0,
                                                uint32_t rt, uint32_t chunk) {
   constexpr int NC = NH / 2;                 // column tiles in this pass
-  constexpr int PIECES = NC * NS * 2;        // 1 KB DMA pieces per sub-tile
-  constexpr int STAGE = PIECES * 64;         // 16-byte units per ring stage
-  constexpr int PER = 2 * NB + (LIVE ? 12 : 0);  // vector-memory ops newer than the stage to publish
+  constexpr int PIECES = NC * NS * 2;        // 1 KB B DMA pieces per sub-tile
+  constexpr int STAGE_B = PIECES * 64;       // 16-byte units of B per ring stage
+  // The four batches' A fragments come through the ring too (4 KB per wave, DMA'd by the wave for
+  // its own batch), so no load in the loop is compiler-tracked and every wait is counted here. A
+  // ring stage is 24 + 16 KB: 160 KB for four.
+  constexpr int STAGE = STAGE_B + 4 * 4 * 64;
+  constexpr int T = NB + (LIVE ? 4 : 0);     // this wave's DMA instructions per sub-tile
+  constexpr int PER = 2 * T;                 // vector-memory ops newer than the stage to publish
   const ob_v4i* bs = reinterpret_cast<const ob_v4i*>(smem);
   const int lane = threadIdx.x & 63;
   const uint32_t g = a.chunks[3 * chunk];
@@ -876,20 +899,28 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
   const uint32_t s1 = min(a.chunks[3 * chunk + 2] * 4u, (n + 63u) >> 6);
   const ob_v4i* Bg = g ? a.B1 : a.B0;
   const uint32_t batch = rt * 4u + (uint32_t)wave;
-  auto dma = [&](int buf, uint32_t s) {
+  // DMA instructions [LO, HI) of this wave's T for sub-tile s into ring stage buf: B pieces first
+  // (piece t * 4 + wave), then this wave's batch's A (4 x 1 KB [replicate block][lane])
+  auto dma = [&](int buf, uint32_t s, auto LO, auto HI) {
+    constexpr int lo = decltype(LO)::value, hi = decltype(HI)::value;
 #pragma unroll
-    for (int t = 0; t < NB; ++t) {
-      const int piece = t * 4 + wave, c = piece / (NS * 2), q = piece - c * (NS * 2);
-      const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct0 + c) * kSubUnits + q * 64;
-      oz_dma16(src + lane, (uint32_t)(buf * STAGE + piece * 64) * 16u);
+    for (int t = lo; t < hi; ++t) {
+      if (t < NB) {
+        const int piece = t * 4 + wave, c = piece / (NS * 2), q = piece - c * (NS * 2);
+        const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct0 + c) * kSubUnits + q * 64;
+        oz_dma16(src + lane, (uint32_t)(buf * STAGE + piece * 64) * 16u);
+      } else {
+        const int m = t - NB;
+        const ob_v4i* src_a = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256;
+        oz_dma16(src_a + m * 64 + lane, (uint32_t)(buf * STAGE + STAGE_B + (wave * 4 + m) * 64) * 16u);
+      }
     }
   };
-  ob_v4i ar[3][4];
-  auto aload = [&](ob_v4i (&dst)[4], uint32_t s) {
-    const ob_v4i* src_a = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256 + lane;
+  auto aread = [&](int buf, ob_v4i (&dst)[4]) {
 #pragma unroll
-    for (int m = 0; m < 4; ++m) dst[m] = src_a[m * 64];
+    for (int m = 0; m < 4; ++m) dst[m] = bs[buf * STAGE + STAGE_B + (wave * 4 + m) * 64 + lane];
   };
+  ob_v4i ar[2][4];
   // B fragments of pair block h: column tile h >> 1, half h & 1, every slice
   auto read = [&](int buf, int h, ob_v4i (&bf)[NS]) {
     const ob_v4i* bb = bs + buf * STAGE + ((h >> 1) * NS * 2 + (h & 1)) * 64 + lane;
@@ -917,55 +948,67 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
           asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+v"(acc[m][q][h]) : "v"(af[m]), "v"(bf[q]));
       }
   };
-  // prologue (as oz_gram_body): A of s0 .. s0 + 2 and B of s0 .. s0 + 3 in flight, then publish
-  if constexpr (LIVE) {
-    aload(ar[0], s0);
-    aload(ar[1], min(s0 + 1, s1 - 1));
-    aload(ar[2], min(s0 + 2, s1 - 1));
-  }
+  // OB_OZ_W_SPREAD 1: step t DMAs sub-tile t + 3 into the stage freed at barrier t - 1, its T
+  // instructions spread between the MFMA blocks before barrier t (one wave per SIMD: a burst of
+  // DMA issue right after the barrier left the MFMA pipe idle while the memory queue drained);
+  // 0: step t DMAs sub-tile t + 4 into stage t right after barrier t. Either way the stage
+  // published at barrier t was issued before barrier t - 2, and the loads newer than it at that
+  // barrier are the two later stages' T each: PER = 2 T. Every step issues the same DMAs (past the
+  // end: the last sub-tile again), so every wait is the same.
+  constexpr int AHEAD = OB_OZ_W_SPREAD ? kWNbuf - 1 : kWNbuf;
 #pragma unroll
-  for (int j = 0; j < kWNbuf; ++j)
-    if (s0 + j < s1) dma(j, s0 + j);
+  for (int j = 0; j < AHEAD; ++j)
+    if (s0 + j < s1) dma(j, s0 + j, IC<0>{}, IC<T>{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   ob_v4i fb[2][NS];
-  if constexpr (LIVE) read(0, 0, fb[0]);
-  // Step s: MFMAs of pair blocks 0 .. NH - 2 while the next block's B is read; wait + barrier (stage
-  // s + 1 landed, every read of stage s done); refill stage s with B of s + 4; read (s + 1, 0); MFMAs
-  // of the last block; A of s + 3 into the slot s frees. At barrier s the loads newer than B(s + 1)
-  // (issued right after barrier s - 3) are A(s), B(s + 2), A(s + 1), B(s + 3), A(s + 2): PER. Every
-  // step issues the same loads (past the end: the last sub-tile again), so every wait is the same.
+  if constexpr (LIVE) {
+    read(0, 0, fb[0]);
+    aread(0, ar[0]);
+  }
+  // the spread DMA of step t: T instructions over the NH - 1 MFMA blocks before the barrier
+  constexpr int SL = NH - 1;
+  auto spread = [&](int buf, uint32_t s, auto H) {
+    constexpr int h = decltype(H)::value;
+    dma(buf, s, IC<T * h / SL>{}, IC<T * (h + 1) / SL>{});
+  };
   auto step = [&](uint32_t s, auto J) {
     constexpr int j = decltype(J)::value;
     const int buf = (int)((s - s0) & (kWNbuf - 1));
-    if constexpr (LIVE) {
-#pragma unroll
-      for (int h = 0; h + 1 < NH; ++h) {
-        read(buf, h + 1, fb[(h + 1) & 1]);
-        __builtin_amdgcn_sched_barrier(0);
-        mfmas(h, ar[j], fb[h & 1]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
+    const uint32_t snext = min(s + AHEAD, s1 - 1);
+    const int bnext = (buf + AHEAD) & (kWNbuf - 1);
+    auto hblock = [&](auto H) {
+      constexpr int h = decltype(H)::value;
+      if constexpr (LIVE) read(buf, h + 1, fb[(h + 1) & 1]);
+      if constexpr (OB_OZ_W_SPREAD && !(DIAG & 4)) spread(bnext, snext, H);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (LIVE && !(DIAG & 2)) mfmas(h, ar[j], fb[h & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    hblock(IC<0>{});
+    if constexpr (NH > 2) {
+      hblock(IC<1>{});
+      hblock(IC<2>{});
     }
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
-    oz_barrier();
-    dma(buf, min(s + kWNbuf, s1 - 1));
+    if constexpr (DIAG & 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+    if constexpr (DIAG & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // timing only: no barrier
+    else oz_barrier();
+    if constexpr (!OB_OZ_W_SPREAD && !(DIAG & 4)) dma(bnext, snext, IC<0>{}, IC<T>{});
     if constexpr (LIVE) {
       read((buf + 1) & (kWNbuf - 1), 0, fb[NH & 1]);
+      aread((buf + 1) & (kWNbuf - 1), ar[j ^ 1]);
       __builtin_amdgcn_sched_barrier(0);
-      mfmas(NH - 1, ar[j], fb[(NH - 1) & 1]);
+      if constexpr (!(DIAG & 2)) mfmas(NH - 1, ar[j], fb[(NH - 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
-      aload(ar[j], min(s + 3, s1 - 1));
     }
   };
   uint32_t s = s0;
-  for (; s + 3 <= s1; s += 3) {
+  for (; s + 2 <= s1; s += 2) {
     step(s, IC<0>{});
     step(s + 1, IC<1>{});
-    step(s + 2, IC<2>{});
   }
   if (s < s1) step(s, IC<0>{});
-  if (s + 1 < s1) step(s + 1, IC<1>{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing DMAs (past the end) have landed
   __syncthreads();  // every wave is done with the ring: the epilogue stages accumulators in it
   if constexpr (LIVE) {
@@ -1003,21 +1046,22 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
   __syncthreads();  // the staging is done before a next pass refills the ring
 }
 
-template <int NS, int NH, bool LIVE>
+template <int NS, int NH, bool LIVE, int DIAG>
 __device__ __forceinline__ void oz_gram_w_pass(const OzArgs& a, unsigned char* smem, int wave, uint32_t ct0,
                                                uint32_t rt, uint32_t chunk) {
   constexpr int P = (NH / 2) * NS * 2;  // pieces per sub-tile, dealt round-robin over the 4 waves
-  if (wave < P % 4 || P % 4 == 0) oz_gram_w_body<NS, NH, (P + 3) / 4, LIVE>(a, smem, wave, ct0, rt, chunk);
-  else oz_gram_w_body<NS, NH, P / 4, LIVE>(a, smem, wave, ct0, rt, chunk);
+  if (wave < P % 4 || P % 4 == 0) oz_gram_w_body<NS, NH, (P + 3) / 4, LIVE, DIAG>(a, smem, wave, ct0, rt, chunk);
+  else oz_gram_w_body<NS, NH, P / 4, LIVE, DIAG>(a, smem, wave, ct0, rt, chunk);
 }
 
-template <int NS, int NH>
+template <int NS, int NH, int DIAG>
 __device__ __forceinline__ void oz_gram_w_pass_live(const OzArgs& a, unsigned char* smem, int wave, uint32_t ct0,
                                                     uint32_t rt, uint32_t chunk, bool live) {
-  if (live) oz_gram_w_pass<NS, NH, true>(a, smem, wave, ct0, rt, chunk);
-  else oz_gram_w_pass<NS, NH, false>(a, smem, wave, ct0, rt, chunk);
+  if (live) oz_gram_w_pass<NS, NH, true, DIAG>(a, smem, wave, ct0, rt, chunk);
+  else oz_gram_w_pass<NS, NH, false, DIAG>(a, smem, wave, ct0, rt, chunk);
 }
 
+template <int DIAG>
 __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void oz_gram_w_kernel(const OzArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1029,15 +1073,15 @@ __global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) 
   const bool six0 = a.nsl[chunk * (uint32_t)a.n_ct + ct0] == 6;
   const bool six1 = two && a.nsl[chunk * (uint32_t)a.n_ct + ct0 + 1] == 6;
   if (two && six0 && six1) {
-    oz_gram_w_pass_live<6, 4>(a, smem, wave, ct0, rt, chunk, live);
+    oz_gram_w_pass_live<6, 4, DIAG>(a, smem, wave, ct0, rt, chunk, live);
     return;
   }
   // a seven-slice tile (or a lone last tile): one column tile per pass
-  if (six0) oz_gram_w_pass_live<6, 2>(a, smem, wave, ct0, rt, chunk, live);
-  else oz_gram_w_pass_live<7, 2>(a, smem, wave, ct0, rt, chunk, live);
+  if (six0) oz_gram_w_pass_live<6, 2, DIAG>(a, smem, wave, ct0, rt, chunk, live);
+  else oz_gram_w_pass_live<7, 2, DIAG>(a, smem, wave, ct0, rt, chunk, live);
   if (!two) return;
-  if (six1) oz_gram_w_pass_live<6, 2>(a, smem, wave, ct0 + 1, rt, chunk, live);
-  else oz_gram_w_pass_live<7, 2>(a, smem, wave, ct0 + 1, rt, chunk, live);
+  if (six1) oz_gram_w_pass_live<6, 2, DIAG>(a, smem, wave, ct0 + 1, rt, chunk, live);
+  else oz_gram_w_pass_live<7, 2, DIAG>(a, smem, wave, ct0 + 1, rt, chunk, live);
 }
 
 }  // namespace
@@ -1269,9 +1313,23 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
   const bool wide = tile == 2 || (tile != 1 && wide_pays);
   p->timing.oz_wide = wide ? 1 : 0;
   if (wide) {  // oz_gram_w_kernel: 4 waves, 256 replicates x 64 pairs per block
-    OZ_HIP(hipFuncSetAttribute((const void*)oz_gram_w_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWLds));
-    hipLaunchKernelGGL(oz_gram_w_kernel, dim3(wblocks), dim3(256), kWLds, s, a);
-    OZ_HIP(hipGetLastError());
+    auto wlaunch = [&](auto kern) -> hipError_t {
+      hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWLds);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(kern, dim3(wblocks), dim3(256), kWLds, s, a);
+      return hipGetLastError();
+    };
+#if OB_TUNING  // timing ablations (gram_diag): wrong results by design
+    switch (ob::opt_int(ob::Opt::GramDiag, 0) & 14) {
+      case 2: OZ_HIP(wlaunch(oz_gram_w_kernel<2>)); break;
+      case 4: OZ_HIP(wlaunch(oz_gram_w_kernel<4>)); break;
+      case 8: OZ_HIP(wlaunch(oz_gram_w_kernel<8>)); break;
+      case 6: OZ_HIP(wlaunch(oz_gram_w_kernel<6>)); break;
+      default: OZ_HIP(wlaunch(oz_gram_w_kernel<0>)); break;
+    }
+#else
+    OZ_HIP(wlaunch(oz_gram_w_kernel<0>));
+#endif
     return OB_OK;
   }
   const uint32_t blocks = blocks8;

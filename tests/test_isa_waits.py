@@ -68,7 +68,7 @@ def test_checker_flags_a_register_reused_under_a_load():
     assert [(r, a) for r, a, _ in found] == [("vgpr-busy", 0x1008)]
 
 
-WIDE = "_ZN12_GLOBAL__N_116oz_gram_w_kernelENS_6OzArgsE"  # oz_gram_w_kernel: the wide tile (round 6)
+WIDE = "_ZN12_GLOBAL__N_116oz_gram_w_kernelILi0EEEvNS_6OzArgsE"  # oz_gram_w_kernel: the wide tile (round 6)
 
 
 def test_shipped_wide_gram_kernel_waits_are_clean():
