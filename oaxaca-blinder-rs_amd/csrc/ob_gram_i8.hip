@@ -929,7 +929,7 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
   };
   // 4 x NS x NH accumulator tiles: the first kWAgprTiles live in AGPRs (inline-asm MFMAs with an "a"
   // constraint), the rest in VGPRs. Left to itself the compiler copies accumulators between the two
-  // files and spills (tools/mfma_acc_probe.hip); pinned, 256 AGPRs + ~230 VGPRs hold the loop.
+  // files and spills (tools/probes/mfma_acc_probe.hip); pinned, 256 AGPRs + ~230 VGPRs hold the loop.
   ob_v4i acc[4][NS][NH];
 #pragma unroll
   for (int m = 0; m < 4; ++m)

@@ -1,3 +1,11 @@
+// Register-allocation probe for the wide i8 Gram (round 6): one wave per SIMD holding 4 x NS x NH
+// v_mfma_i32_16x16x64_i8 accumulator tiles through a K loop, then the int64 slice combination.
+// Build: hipcc --offload-arch=gfx950 -O3 -c mfma_acc_probe.hip -Rpass-analysis=kernel-resource-usage
+// Measured (ROCm 7.2 hipcc): <6, 2> (192 accumulators) 256 VGPRs + 227 AGPRs, no spill; <6, 3> 162
+// VGPRs spilled; <6, 4> (384) 324 spilled; <4, 4> 116; <5, 4> 25. The compiler keeps copies of
+// accumulators in both register files around the int64 epilogue. With inline-asm MFMAs pinning 64
+// tiles to AGPRs ("+a") and the epilogue staged through LDS one pair block at a time, <6, 4> holds in
+// 174 VGPRs + 256 AGPRs (oz_gram_w_kernel, ob_gram_i8.hip: 228 VGPRs with its operand buffers).
 #include <hip/hip_runtime.h>
 typedef int v4i __attribute__((ext_vector_type(4)));
 template <int NS, int NH>
