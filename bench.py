@@ -418,13 +418,15 @@ def load_probit_pmc(rows, preds, reps, ks):
     return None
 
 
-def load_traffic(rows, preds, reps, gram_path=1):
-    """HBM bytes per Gram launch (ob_gram_kernel, or oz_gram_kernel for the i8 path) from the
-    committed rocprofv3 PMC summary."""
+def load_traffic(rows, preds, reps, gram_path=1, kernel=None):
+    """HBM bytes per Gram launch (ob_gram_kernel, or the i8 path's oz_gram_w_kernel / oz_gram_kernel)
+    from the committed rocprofv3 PMC summary of that kernel at that size, else None."""
     path = os.path.join(ROOT, "profiles", "pmc_gram.json" if gram_path == 1 else "pmc_gram_i8.json")
     try:
         with open(path) as f:
             j = json.load(f)
+        if kernel and j.get("kernel") != kernel:
+            return None
         if j.get("rows") == rows and j.get("preds") == preds and j.get("reps") == reps:
             return j.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
@@ -745,7 +747,8 @@ def main():
         bytes_rep = args.rows * (args.preds + (2 if weighted else 1)) * 8.0
         reps_per_launch = min(per_rank, 16384) if launches else 0
         achieved = flops_rep * reps_per_launch / (gram_launch_ms * 1e-3) / 1e12 if gram_launch_ms else 0.0
-        traffic = load_traffic(args.rows, args.preds, per_rank, gram_path) if not taus else None
+        traffic = load_traffic(args.rows, args.preds, per_rank, gram_path,
+                               gram_kernel if gram_path == 2 else "ob_gram_kernel") if not taus else None
         if gram_path == 2:
             # exact integer-sliced Gram (ob_gram_i8.hip): the algorithmic work is one i8 multiply-add per
             # (replicate, row, live pair, 8-bit digit slice run): 7 slices, 6 on the (chunk, column tile)
@@ -758,7 +761,7 @@ def main():
             i8_tops = ops_rep * reps_per_launch / (gram_launch_ms * 1e-3) / 1e12 if gram_launch_ms else 0.0
             roof = {"bound": "mfma", "achieved": i8_tops, "peak": I8_MFMA_PEAK_TOPS, "unit": "TOPS (i8)",
                     "frac": i8_tops / I8_MFMA_PEAK_TOPS, "traffic": traffic,
-                    "traffic_source": "profiles/pmc_gram_i8.json (PMC 2 x FETCH_SIZE + WRITE_SIZE, final round-5 tree, profiles/r05_final_pmc_gram.json)",
+                    "traffic_source": "profiles/pmc_gram_i8.json (PMC 2 x FETCH_SIZE + WRITE_SIZE of this kernel at this size, round 6)",
                     "kernel": gram_kernel,
                     "avg_launch_ms": gram_launch_ms, "i8_ops_per_replicate": ops_rep,
                     "i8_ops_issued_per_replicate": ops_issued, "digit_slices_mean": slices,

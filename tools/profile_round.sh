@@ -2,10 +2,10 @@
 # Round profile of the headline bench (run on the GPU box from the repo root):
 #   bench JSON, rocprofv3 kernel-trace stats, FETCH_SIZE and WRITE_SIZE passes (separate, per
 #   MI355X_MICROARCH.md), and a GRBM_GUI_ACTIVE + MFMA-busy pass for the effective clock.
-# usage: [SKIP_BENCH=1] [KERNEL=oz_gram_kernel] bash tools/profile_round.sh TAG   -> gpurun_out/TAG_*
+# usage: [SKIP_BENCH=1] [KERNEL=oz_gram_w_kernel] bash tools/profile_round.sh TAG   -> gpurun_out/TAG_*
 set -euo pipefail
 TAG=${1:-rXX}
-KERNEL=${KERNEL:-oz_gram_kernel}
+KERNEL=${KERNEL:-oz_gram_w_kernel}
 OUT=$PWD/gpurun_out
 mkdir -p "$OUT"
 REPO=$PWD
