@@ -839,7 +839,10 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
 #ifndef OB_OZ_W_SPREAD
 #define OB_OZ_W_SPREAD 0
 #endif
-constexpr int kWNbuf = 4;  // ring stages (sub-tiles)
+#ifndef OB_OZ_W_NBUF
+#define OB_OZ_W_NBUF 4
+#endif
+constexpr int kWNbuf = OB_OZ_W_NBUF;  // ring stages (sub-tiles): 4 x 40 KB fill the 160 KB of LDS
 constexpr int kWAgprTiles = 64;  // accumulator tiles (4 registers each) pinned to AGPRs
 // 4 stages of B (two six-slice tiles: 24 KB; one seven-slice tile: 14 KB) + A (16 KB)
 constexpr size_t kWLds = kWNbuf * (size_t)(2 * 6 * 2 * 64 + 4 * 4 * 64) * 16;
@@ -890,7 +893,7 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
   // ring stage is 24 + 16 KB: 160 KB for four.
   constexpr int STAGE = STAGE_B + 4 * 4 * 64;
   constexpr int T = NB + (LIVE ? 4 : 0);     // this wave's DMA instructions per sub-tile
-  constexpr int PER = 2 * T;                 // vector-memory ops newer than the stage to publish
+  constexpr int PER = (kWNbuf - 2) * T;      // vector-memory ops newer than the stage to publish
   const ob_v4i* bs = reinterpret_cast<const ob_v4i*>(smem);
   const int lane = threadIdx.x & 63;
   const uint32_t g = a.chunks[3 * chunk];
@@ -953,7 +956,7 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
   // DMA issue right after the barrier left the MFMA pipe idle while the memory queue drained);
   // 0: step t DMAs sub-tile t + 4 into stage t right after barrier t. Either way the stage
   // published at barrier t was issued before barrier t - 2, and the loads newer than it at that
-  // barrier are the two later stages' T each: PER = 2 T. Every step issues the same DMAs (past the
+  // barrier are the later stages' T each: PER = (N - 2) T for N ring stages. Every step issues the same DMAs (past the
   // end: the last sub-tile again), so every wait is the same.
   constexpr int AHEAD = OB_OZ_W_SPREAD ? kWNbuf - 1 : kWNbuf;
 #pragma unroll
@@ -974,9 +977,9 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
   };
   auto step = [&](uint32_t s, auto J) {
     constexpr int j = decltype(J)::value;
-    const int buf = (int)((s - s0) & (kWNbuf - 1));
+    const int buf = (int)((s - s0) % kWNbuf);
     const uint32_t snext = min(s + AHEAD, s1 - 1);
-    const int bnext = (buf + AHEAD) & (kWNbuf - 1);
+    const int bnext = (buf + AHEAD) % kWNbuf;
     auto hblock = [&](auto H) {
       constexpr int h = decltype(H)::value;
       if constexpr (LIVE) read(buf, h + 1, fb[(h + 1) & 1]);
@@ -996,8 +999,8 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
     else oz_barrier();
     if constexpr (!OB_OZ_W_SPREAD && !(DIAG & 4)) dma(bnext, snext, IC<0>{}, IC<T>{});
     if constexpr (LIVE) {
-      read((buf + 1) & (kWNbuf - 1), 0, fb[NH & 1]);
-      aread((buf + 1) & (kWNbuf - 1), ar[j ^ 1]);
+      read((buf + 1) % kWNbuf, 0, fb[NH & 1]);
+      aread((buf + 1) % kWNbuf, ar[j ^ 1]);
       __builtin_amdgcn_sched_barrier(0);
       if constexpr (!(DIAG & 2)) mfmas(NH - 1, ar[j], fb[(NH - 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
