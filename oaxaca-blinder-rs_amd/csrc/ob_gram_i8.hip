@@ -1303,14 +1303,16 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
   a.n_pairs_pad = p->oz_n_ct * kPairsPerTile;
   a.n_dct = (a.n_ct + 1) / 2;
   // Which kernel: the wide tile does a block's work (twice the 8-wave kernel's) in kWideCost of the
-  // 8-wave kernel's block time (configs[1]: 11.09 against 11.65 ms per launch, profiles/
-  // r06_ab_gram_wide.txt), but has half as many blocks, so a small launch wastes more of its last
-  // round over the CUs (configs[2]'s 1,250-replicate share: 640 blocks, 2.5 rounds, 1.81 against
-  // 1.56 ms). Rounds x cost decides; both kernels give bitwise the same partials.
+  // 8-wave kernel's block time (configs[1]: 11.09-11.25 against 11.6-11.65 ms per launch, profiles/
+  // r06_ab_gram_wide.txt, r06_ab_gram_tile_choice.txt), but has half as many blocks, so a launch
+  // whose last round over the CUs is partial wastes more of it (configs[2]'s 1,250 share: 640 wide
+  // blocks, 2.5 rounds, 1.81 against 1.56 ms; configs[3]'s 5,000 x 3 outcomes: 12.5 rounds, 7.3
+  // against 7.1 ms; 2,500 replicates: 5 rounds, 2.84 against 2.98 ms). Rounds x cost decides; both
+  // kernels give bitwise the same partials.
   const uint32_t wblocks = (uint32_t)n_chunks * a.n_rt * (uint32_t)a.n_dct;
   const uint32_t blocks8 = (uint32_t)n_chunks * a.n_rt * (uint32_t)a.n_ct;
   const uint32_t cus = (uint32_t)std::max(p->ctx->cus, 1);
-  const double kWideCost = 1.9;
+  const double kWideCost = 1.95;
   const bool wide_pays = kWideCost * (double)((wblocks + cus - 1) / cus) <= (double)((blocks8 + cus - 1) / cus);
   const int tile = ob::opt_int(ob::Opt::GramTile, 0);
   const bool wide = tile == 2 || (tile != 1 && wide_pays);
