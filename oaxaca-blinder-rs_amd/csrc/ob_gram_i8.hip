@@ -503,6 +503,16 @@ __device__ __forceinline__ void oz_dma16(const void* src, uint32_t lds) {
 }
 #pragma clang diagnostic pop
 
+// The same DMA with a wave-uniform SGPR base and a per-lane 32-bit offset (global saddr form): the
+// address arithmetic stays on the scalar unit, which issues beside the MFMAs.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void oz_dma16s(uint32_t voff, const void* sbase, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(lds)
+               : "memory", "m0");
+}
+#pragma clang diagnostic pop
+
 __device__ __forceinline__ void oz_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 #ifndef OB_OZ_RASTER
@@ -837,7 +847,7 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
 // pair whose tiles do not both run six slices takes its tiles one pass each (NH = 2).
 // ---------------------------------------------------------------------------------------------
 #ifndef OB_OZ_W_SPREAD
-#define OB_OZ_W_SPREAD 0
+#define OB_OZ_W_SPREAD 3
 #endif
 #ifndef OB_OZ_W_NBUF
 #define OB_OZ_W_NBUF 4
@@ -919,6 +929,19 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
       }
     }
   };
+  // DMA instruction t of this wave for sub-tile s (OB_OZ_W_SPREAD 2): scalar base, lane offset
+  auto dma1 = [&](int buf, uint32_t s, auto TT) {
+    constexpr int t = decltype(TT)::value;
+    if constexpr (t < NB) {
+      const int piece = t * 4 + wave, c = piece / (NS * 2), q = piece - c * (NS * 2);
+      const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct0 + c) * kSubUnits + q * 64;
+      oz_dma16s((uint32_t)lane * 16u, src, (uint32_t)(buf * STAGE + piece * 64) * 16u);
+    } else {
+      constexpr int m = t - NB;
+      const ob_v4i* src_a = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256 + m * 64;
+      oz_dma16s((uint32_t)lane * 16u, src_a, (uint32_t)(buf * STAGE + STAGE_B + (wave * 4 + m) * 64) * 16u);
+    }
+  };
   auto aread = [&](int buf, ob_v4i (&dst)[4]) {
 #pragma unroll
     for (int m = 0; m < 4; ++m) dst[m] = bs[buf * STAGE + STAGE_B + (wave * 4 + m) * 64 + lane];
@@ -940,16 +963,52 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
     for (int q = 0; q < NS; ++q)
 #pragma unroll
       for (int h = 0; h < NH; ++h) acc[m][q][h] = (ob_v4i){};
+  auto mfma1 = [&](int m, int q, int h, const ob_v4i (&af)[4], const ob_v4i (&bf)[NS]) {
+    if ((m * NS + q) * NH + h < kWAgprTiles)
+      asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+a"(acc[m][q][h]) : "v"(af[m]), "v"(bf[q]));
+    else
+      asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+v"(acc[m][q][h]) : "v"(af[m]), "v"(bf[q]));
+  };
   auto mfmas = [&](int h, const ob_v4i (&af)[4], const ob_v4i (&bf)[NS]) {
 #pragma unroll
     for (int q = 0; q < NS; ++q)
 #pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        if ((m * NS + q) * NH + h < kWAgprTiles)
-          asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+a"(acc[m][q][h]) : "v"(af[m]), "v"(bf[q]));
-        else
-          asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+v"(acc[m][q][h]) : "v"(af[m]), "v"(bf[q]));
+      for (int m = 0; m < 4; ++m) mfma1(m, q, h, af, bf);
+  };
+  // OB_OZ_W_SPREAD 2: pair block H's MFMAs with DMA instruction H * NS + q issued after slice q's four
+  // (each in the shadow of the MFMAs around it), into stage bn for sub-tile sn
+  auto mfmas_dma = [&](auto H, const ob_v4i (&af)[4], const ob_v4i (&bf)[NS], int bn, uint32_t sn) {
+    constexpr int h = decltype(H)::value;
+    auto one = [&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) mfma1(m, q, h, af, bf);
+      if constexpr (h * NS + q < T) dma1(bn, sn, IC<h * NS + q>{});
+    };
+    one(IC<0>{}); one(IC<1>{}); one(IC<2>{}); one(IC<3>{}); one(IC<4>{}); one(IC<5>{});
+    if constexpr (NS > 6) one(IC<6>{});
+  };
+  // OB_OZ_W_SPREAD 3: as 2, and the next pair block's B slices (and after the barrier the next
+  // sub-tile's A) are read one slice at a time behind the MFMAs instead of in a block before them.
+  // Pre-barrier block H: MFMAs (H, q) | B slice q of (rb, H + 1) into nb | DMA H * NS + q.
+  auto mfmas_rd = [&](auto H, const ob_v4i (&af)[4], const ob_v4i (&bf)[NS], int rb, int rh, ob_v4i (&nb)[NS],
+                      int bn, uint32_t sn, bool with_dma, ob_v4i* an) {
+    constexpr int h = decltype(H)::value;
+    const ob_v4i* bb = bs + rb * STAGE + ((rh >> 1) * NS * 2 + (rh & 1)) * 64 + lane;
+    auto one = [&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) mfma1(m, q, h, af, bf);
+      nb[q] = bb[q * 128];
+      if constexpr (q < 4) {
+        if (an) an[q] = bs[rb * STAGE + STAGE_B + (wave * 4 + q) * 64 + lane];
       }
+      if constexpr (h * NS + q < T) {
+        if (with_dma) dma1(bn, sn, IC<h * NS + q>{});
+      }
+    };
+    one(IC<0>{}); one(IC<1>{}); one(IC<2>{}); one(IC<3>{}); one(IC<4>{}); one(IC<5>{});
+    if constexpr (NS > 6) one(IC<6>{});
   };
   // OB_OZ_W_SPREAD 1: step t DMAs sub-tile t + 3 into the stage freed at barrier t - 1, its T
   // instructions spread between the MFMA blocks before barrier t (one wave per SIMD: a burst of
@@ -958,7 +1017,7 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
   // published at barrier t was issued before barrier t - 2, and the loads newer than it at that
   // barrier are the later stages' T each: PER = (N - 2) T for N ring stages. Every step issues the same DMAs (past the
   // end: the last sub-tile again), so every wait is the same.
-  constexpr int AHEAD = OB_OZ_W_SPREAD ? kWNbuf - 1 : kWNbuf;
+  constexpr int AHEAD = OB_OZ_W_SPREAD ? kWNbuf - 1 : kWNbuf;  // 2: like 1, finer (mfmas_dma)
 #pragma unroll
   for (int j = 0; j < AHEAD; ++j)
     if (s0 + j < s1) dma(j, s0 + j, IC<0>{}, IC<T>{});
@@ -980,12 +1039,41 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
     const int buf = (int)((s - s0) % kWNbuf);
     const uint32_t snext = min(s + AHEAD, s1 - 1);
     const int bnext = (buf + AHEAD) % kWNbuf;
+    if constexpr (OB_OZ_W_SPREAD == 3 && LIVE && !(DIAG & 2) && !(DIAG & 4)) {
+      auto hb3 = [&](auto H) {
+        constexpr int h = decltype(H)::value;
+        __builtin_amdgcn_sched_barrier(0);
+        mfmas_rd(H, ar[j], fb[h & 1], buf, h + 1, fb[(h + 1) & 1], bnext, snext, true, nullptr);
+        if constexpr (h == NH - 2) dma(bnext, snext, IC<(NH - 1) * NS>{}, IC<T>{});
+        __builtin_amdgcn_sched_barrier(0);
+      };
+      hb3(IC<0>{});
+      if constexpr (NH > 2) {
+        hb3(IC<1>{});
+        hb3(IC<2>{});
+      }
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+      oz_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      // the last pair block's MFMAs | the next sub-tile's first B block and its A, slice by slice
+      mfmas_rd(IC<NH - 1>{}, ar[j], fb[(NH - 1) & 1], (buf + 1) % kWNbuf, 0, fb[NH & 1], bnext, snext, false,
+               ar[j ^ 1]);
+      __builtin_amdgcn_sched_barrier(0);
+      return;
+    }
     auto hblock = [&](auto H) {
       constexpr int h = decltype(H)::value;
       if constexpr (LIVE) read(buf, h + 1, fb[(h + 1) & 1]);
-      if constexpr (OB_OZ_W_SPREAD && !(DIAG & 4)) spread(bnext, snext, H);
+      if constexpr (OB_OZ_W_SPREAD == 1 && !(DIAG & 4)) spread(bnext, snext, H);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (LIVE && !(DIAG & 2)) mfmas(h, ar[j], fb[h & 1]);
+      if constexpr (OB_OZ_W_SPREAD == 2 && LIVE && !(DIAG & 2) && !(DIAG & 4)) {
+        mfmas_dma(H, ar[j], fb[h & 1], bnext, snext);
+        if constexpr (h == NH - 2)  // what the slots did not hold (NH = 2, seven pieces or more)
+          dma(bnext, snext, IC<(NH - 1) * NS>{}, IC<T>{});
+      } else {
+        if constexpr (OB_OZ_W_SPREAD == 2 && !(DIAG & 4) && h == 0) dma(bnext, snext, IC<0>{}, IC<T>{});
+        if constexpr (LIVE && !(DIAG & 2)) mfmas(h, ar[j], fb[h & 1]);
+      }
       __builtin_amdgcn_sched_barrier(0);
     };
     hblock(IC<0>{});
