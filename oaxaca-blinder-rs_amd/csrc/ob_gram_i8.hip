@@ -847,7 +847,7 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
 // pair whose tiles do not both run six slices takes its tiles one pass each (NH = 2).
 // ---------------------------------------------------------------------------------------------
 #ifndef OB_OZ_W_SPREAD
-#define OB_OZ_W_SPREAD 3
+#define OB_OZ_W_SPREAD 1
 #endif
 #ifndef OB_OZ_W_NBUF
 #define OB_OZ_W_NBUF 4
@@ -929,7 +929,7 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
       }
     }
   };
-  // DMA instruction t of this wave for sub-tile s (OB_OZ_W_SPREAD 2): scalar base, lane offset
+  // DMA instruction t of this wave for sub-tile s (mfmas_rd): scalar base, lane offset
   auto dma1 = [&](int buf, uint32_t s, auto TT) {
     constexpr int t = decltype(TT)::value;
     if constexpr (t < NB) {
@@ -975,22 +975,10 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
 #pragma unroll
       for (int m = 0; m < 4; ++m) mfma1(m, q, h, af, bf);
   };
-  // OB_OZ_W_SPREAD 2: pair block H's MFMAs with DMA instruction H * NS + q issued after slice q's four
-  // (each in the shadow of the MFMAs around it), into stage bn for sub-tile sn
-  auto mfmas_dma = [&](auto H, const ob_v4i (&af)[4], const ob_v4i (&bf)[NS], int bn, uint32_t sn) {
-    constexpr int h = decltype(H)::value;
-    auto one = [&](auto Q) {
-      constexpr int q = decltype(Q)::value;
-#pragma unroll
-      for (int m = 0; m < 4; ++m) mfma1(m, q, h, af, bf);
-      if constexpr (h * NS + q < T) dma1(bn, sn, IC<h * NS + q>{});
-    };
-    one(IC<0>{}); one(IC<1>{}); one(IC<2>{}); one(IC<3>{}); one(IC<4>{}); one(IC<5>{});
-    if constexpr (NS > 6) one(IC<6>{});
-  };
-  // OB_OZ_W_SPREAD 3: as 2, and the next pair block's B slices (and after the barrier the next
-  // sub-tile's A) are read one slice at a time behind the MFMAs instead of in a block before them.
-  // Pre-barrier block H: MFMAs (H, q) | B slice q of (rb, H + 1) into nb | DMA H * NS + q.
+  // OB_OZ_W_SPREAD 1: pre-barrier pair block H = MFMAs (H, q) | B slice q of (rb, H + 1) into nb |
+  // DMA instruction H * NS + q, slice by slice, so the scalar address work, the DMA issue and the
+  // LDS reads sit in the shadow of the MFMAs around them; after the barrier the last block's MFMAs
+  // likewise carry the next sub-tile's first B block and its A.
   auto mfmas_rd = [&](auto H, const ob_v4i (&af)[4], const ob_v4i (&bf)[NS], int rb, int rh, ob_v4i (&nb)[NS],
                       int bn, uint32_t sn, bool with_dma, ob_v4i* an) {
     constexpr int h = decltype(H)::value;
@@ -1011,13 +999,13 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
     if constexpr (NS > 6) one(IC<6>{});
   };
   // OB_OZ_W_SPREAD 1: step t DMAs sub-tile t + 3 into the stage freed at barrier t - 1, its T
-  // instructions spread between the MFMA blocks before barrier t (one wave per SIMD: a burst of
-  // DMA issue right after the barrier left the MFMA pipe idle while the memory queue drained);
-  // 0: step t DMAs sub-tile t + 4 into stage t right after barrier t. Either way the stage
+  // instructions one per slice group between the MFMAs before barrier t (mfmas_rd: one wave per
+  // SIMD, so a burst of DMA issue and address arithmetic right after the barrier left the MFMA pipe
+  // idle); 0: step t DMAs sub-tile t + 4 into stage t right after barrier t. Either way the stage
   // published at barrier t was issued before barrier t - 2, and the loads newer than it at that
   // barrier are the later stages' T each: PER = (N - 2) T for N ring stages. Every step issues the same DMAs (past the
   // end: the last sub-tile again), so every wait is the same.
-  constexpr int AHEAD = OB_OZ_W_SPREAD ? kWNbuf - 1 : kWNbuf;  // 2: like 1, finer (mfmas_dma)
+  constexpr int AHEAD = OB_OZ_W_SPREAD ? kWNbuf - 1 : kWNbuf;
 #pragma unroll
   for (int j = 0; j < AHEAD; ++j)
     if (s0 + j < s1) dma(j, s0 + j, IC<0>{}, IC<T>{});
@@ -1028,58 +1016,41 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
     read(0, 0, fb[0]);
     aread(0, ar[0]);
   }
-  // the spread DMA of step t: T instructions over the NH - 1 MFMA blocks before the barrier
-  constexpr int SL = NH - 1;
-  auto spread = [&](int buf, uint32_t s, auto H) {
-    constexpr int h = decltype(H)::value;
-    dma(buf, s, IC<T * h / SL>{}, IC<T * (h + 1) / SL>{});
-  };
   auto step = [&](uint32_t s, auto J) {
     constexpr int j = decltype(J)::value;
     const int buf = (int)((s - s0) % kWNbuf);
     const uint32_t snext = min(s + AHEAD, s1 - 1);
     const int bnext = (buf + AHEAD) % kWNbuf;
-    if constexpr (OB_OZ_W_SPREAD == 3 && LIVE && !(DIAG & 2) && !(DIAG & 4)) {
-      auto hb3 = [&](auto H) {
+    if constexpr (OB_OZ_W_SPREAD && LIVE && !(DIAG & 2) && !(DIAG & 4)) {
+      auto hb = [&](auto H) {
         constexpr int h = decltype(H)::value;
         __builtin_amdgcn_sched_barrier(0);
         mfmas_rd(H, ar[j], fb[h & 1], buf, h + 1, fb[(h + 1) & 1], bnext, snext, true, nullptr);
-        if constexpr (h == NH - 2) dma(bnext, snext, IC<(NH - 1) * NS>{}, IC<T>{});
+        if constexpr (h == NH - 2) dma(bnext, snext, IC<(NH - 1) * NS>{}, IC<T>{});  // what the slots did not hold
         __builtin_amdgcn_sched_barrier(0);
       };
-      hb3(IC<0>{});
+      hb(IC<0>{});
       if constexpr (NH > 2) {
-        hb3(IC<1>{});
-        hb3(IC<2>{});
+        hb(IC<1>{});
+        hb(IC<2>{});
       }
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
       oz_barrier();
       __builtin_amdgcn_sched_barrier(0);
-      // the last pair block's MFMAs | the next sub-tile's first B block and its A, slice by slice
       mfmas_rd(IC<NH - 1>{}, ar[j], fb[(NH - 1) & 1], (buf + 1) % kWNbuf, 0, fb[NH & 1], bnext, snext, false,
                ar[j ^ 1]);
       __builtin_amdgcn_sched_barrier(0);
       return;
     }
-    auto hblock = [&](auto H) {
-      constexpr int h = decltype(H)::value;
+    // dead batches, timing ablations and OB_OZ_W_SPREAD 0: block-wise reads; the step's DMA in one
+    // burst (spread: before the barrier, into the stage freed at the previous one; 0: after it)
+    if constexpr (OB_OZ_W_SPREAD && !(DIAG & 4)) dma(bnext, snext, IC<0>{}, IC<T>{});
+#pragma unroll
+    for (int h = 0; h + 1 < NH; ++h) {
       if constexpr (LIVE) read(buf, h + 1, fb[(h + 1) & 1]);
-      if constexpr (OB_OZ_W_SPREAD == 1 && !(DIAG & 4)) spread(bnext, snext, H);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (OB_OZ_W_SPREAD == 2 && LIVE && !(DIAG & 2) && !(DIAG & 4)) {
-        mfmas_dma(H, ar[j], fb[h & 1], bnext, snext);
-        if constexpr (h == NH - 2)  // what the slots did not hold (NH = 2, seven pieces or more)
-          dma(bnext, snext, IC<(NH - 1) * NS>{}, IC<T>{});
-      } else {
-        if constexpr (OB_OZ_W_SPREAD == 2 && !(DIAG & 4) && h == 0) dma(bnext, snext, IC<0>{}, IC<T>{});
-        if constexpr (LIVE && !(DIAG & 2)) mfmas(h, ar[j], fb[h & 1]);
-      }
+      if constexpr (LIVE && !(DIAG & 2)) mfmas(h, ar[j], fb[h & 1]);
       __builtin_amdgcn_sched_barrier(0);
-    };
-    hblock(IC<0>{});
-    if constexpr (NH > 2) {
-      hblock(IC<1>{});
-      hblock(IC<2>{});
     }
     if constexpr (DIAG & 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
