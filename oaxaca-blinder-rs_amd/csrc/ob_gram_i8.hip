@@ -846,9 +846,6 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
 // rounding each, then their sum): the partials are bitwise the 8-wave kernel's. A column-tile
 // pair whose tiles do not both run six slices takes its tiles one pass each (NH = 2).
 // ---------------------------------------------------------------------------------------------
-#ifndef OB_OZ_HALF_COST
-#define OB_OZ_HALF_COST 2.0  // above 1: never chosen until measured (tools: -DOB_OZ_HALF_COST=..., option gram_tile 3)
-#endif
 #ifndef OB_OZ_W_SPREAD
 #define OB_OZ_W_SPREAD 1
 #endif
@@ -895,21 +892,17 @@ __device__ __forceinline__ void oz_map_w(const OzArgs& a, uint32_t* dct, uint32_
 
 // NS digit slices (6 or 7), NH 16-pair blocks per pass (4: column tiles ct0, ct0 + 1; 2: ct0 only),
 // NB this wave's DMA pieces per sub-tile, LIVE its replicate batch exists.
-template <int NS, int NH, int NB, bool LIVE, int DIAG, bool HALF>
+template <int NS, int NH, int NB, bool LIVE, int DIAG>
 __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* smem, int wave, uint32_t ct0,
                                                uint32_t rt, uint32_t chunk) {
-  // HALF: the block is 128 replicates x 64 pairs; wave w takes batch w >> 1 and column tile w & 1
-  // (NH = 2 pair blocks), the two waves of a batch each DMA half of its A
-  constexpr int NC = HALF ? 2 : NH / 2;      // column tiles in this pass
-  constexpr int NBAT = HALF ? 2 : 4;         // replicate batches per block
-  constexpr int AP = HALF ? 2 : 4;           // A DMA pieces per wave
+  constexpr int NC = NH / 2;                 // column tiles in this pass
   constexpr int PIECES = NC * NS * 2;        // 1 KB B DMA pieces per sub-tile
   constexpr int STAGE_B = PIECES * 64;       // 16-byte units of B per ring stage
   // The four batches' A fragments come through the ring too (4 KB per wave, DMA'd by the wave for
   // its own batch), so no load in the loop is compiler-tracked and every wait is counted here. A
   // ring stage is 24 + 16 KB: 160 KB for four.
-  constexpr int STAGE = STAGE_B + NBAT * 4 * 64;
-  constexpr int T = NB + (LIVE ? AP : 0);    // this wave's DMA instructions per sub-tile
+  constexpr int STAGE = STAGE_B + 4 * 4 * 64;
+  constexpr int T = NB + (LIVE ? 4 : 0);     // this wave's DMA instructions per sub-tile
   constexpr int PER = (kWNbuf - 2) * T;      // vector-memory ops newer than the stage to publish
   const ob_v4i* bs = reinterpret_cast<const ob_v4i*>(smem);
   const int lane = threadIdx.x & 63;
@@ -918,8 +911,7 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
   const uint32_t s0 = a.chunks[3 * chunk + 1] * 4u;
   const uint32_t s1 = min(a.chunks[3 * chunk + 2] * 4u, (n + 63u) >> 6);
   const ob_v4i* Bg = g ? a.B1 : a.B0;
-  const int bl = HALF ? wave >> 1 : wave, cw = HALF ? wave & 1 : 0;  // batch slot, column tile (HALF)
-  const uint32_t batch = rt * (uint32_t)NBAT + (uint32_t)bl;
+  const uint32_t batch = rt * 4u + (uint32_t)wave;
   // DMA instructions [LO, HI) of this wave's T for sub-tile s into ring stage buf: B pieces first
   // (piece t * 4 + wave), then this wave's batch's A (4 x 1 KB [replicate block][lane])
   auto dma = [&](int buf, uint32_t s, auto LO, auto HI) {
@@ -931,9 +923,9 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
         const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct0 + c) * kSubUnits + q * 64;
         oz_dma16(src + lane, (uint32_t)(buf * STAGE + piece * 64) * 16u);
       } else {
-        const int m = HALF ? cw * 2 + (t - NB) : t - NB;
+        const int m = t - NB;
         const ob_v4i* src_a = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256;
-        oz_dma16(src_a + m * 64 + lane, (uint32_t)(buf * STAGE + STAGE_B + (bl * 4 + m) * 64) * 16u);
+        oz_dma16(src_a + m * 64 + lane, (uint32_t)(buf * STAGE + STAGE_B + (wave * 4 + m) * 64) * 16u);
       }
     }
   };
@@ -945,19 +937,19 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
       const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct0 + c) * kSubUnits + q * 64;
       oz_dma16s((uint32_t)lane * 16u, src, (uint32_t)(buf * STAGE + piece * 64) * 16u);
     } else {
-      const int m = HALF ? cw * 2 + (t - NB) : t - NB;
+      constexpr int m = t - NB;
       const ob_v4i* src_a = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256 + m * 64;
-      oz_dma16s((uint32_t)lane * 16u, src_a, (uint32_t)(buf * STAGE + STAGE_B + (bl * 4 + m) * 64) * 16u);
+      oz_dma16s((uint32_t)lane * 16u, src_a, (uint32_t)(buf * STAGE + STAGE_B + (wave * 4 + m) * 64) * 16u);
     }
   };
   auto aread = [&](int buf, ob_v4i (&dst)[4]) {
 #pragma unroll
-    for (int m = 0; m < 4; ++m) dst[m] = bs[buf * STAGE + STAGE_B + (bl * 4 + m) * 64 + lane];
+    for (int m = 0; m < 4; ++m) dst[m] = bs[buf * STAGE + STAGE_B + (wave * 4 + m) * 64 + lane];
   };
   ob_v4i ar[2][4];
-  // B fragments of pair block h: column tile h >> 1 (HALF: the wave's), half h & 1, every slice
+  // B fragments of pair block h: column tile h >> 1, half h & 1, every slice
   auto read = [&](int buf, int h, ob_v4i (&bf)[NS]) {
-    const ob_v4i* bb = bs + buf * STAGE + ((HALF ? cw : h >> 1) * NS * 2 + (h & 1)) * 64 + lane;
+    const ob_v4i* bb = bs + buf * STAGE + ((h >> 1) * NS * 2 + (h & 1)) * 64 + lane;
 #pragma unroll
     for (int q = 0; q < NS; ++q) bf[q] = bb[q * 128];
   };
@@ -990,14 +982,14 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
   auto mfmas_rd = [&](auto H, const ob_v4i (&af)[4], const ob_v4i (&bf)[NS], int rb, int rh, ob_v4i (&nb)[NS],
                       int bn, uint32_t sn, bool with_dma, ob_v4i* an) {
     constexpr int h = decltype(H)::value;
-    const ob_v4i* bb = bs + rb * STAGE + ((HALF ? cw : rh >> 1) * NS * 2 + (rh & 1)) * 64 + lane;
+    const ob_v4i* bb = bs + rb * STAGE + ((rh >> 1) * NS * 2 + (rh & 1)) * 64 + lane;
     auto one = [&](auto Q) {
       constexpr int q = decltype(Q)::value;
 #pragma unroll
       for (int m = 0; m < 4; ++m) mfma1(m, q, h, af, bf);
       nb[q] = bb[q * 128];
       if constexpr (q < 4) {
-        if (an) an[q] = bs[rb * STAGE + STAGE_B + (bl * 4 + q) * 64 + lane];
+        if (an) an[q] = bs[rb * STAGE + STAGE_B + (wave * 4 + q) * 64 + lane];
       }
       if constexpr (h * NS + q < T) {
         if (with_dma) dma1(bn, sn, IC<h * NS + q>{});
@@ -1095,7 +1087,7 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
 #pragma unroll
         for (int q = 0; q < NS; ++q) st[(m * NS + q) * 64 + lane] = acc[m][q][h];
       __builtin_amdgcn_sched_barrier(0);
-      const int pair = (int)(ct0 + (HALF ? cw : h >> 1)) * kPairsPerTile + 16 * (h & 1) + (lane & 15);
+      const int pair = (int)(ct0 + (h >> 1)) * kPairsPerTile + 16 * (h & 1) + (lane & 15);
       const int E = a.pexp[chunk * a.n_pairs_pad + min(pair, a.n_pairs_pad - 1)];
       const int sh0 = E - kFracBits + 8 * (kS - 0 - kSlo), sh1 = E - kFracBits + 8 * (kS - kSlo - (NS - kSlo));
 #pragma unroll
@@ -1120,8 +1112,8 @@ template <int NS, int NH, bool LIVE, int DIAG>
 __device__ __forceinline__ void oz_gram_w_pass(const OzArgs& a, unsigned char* smem, int wave, uint32_t ct0,
                                                uint32_t rt, uint32_t chunk) {
   constexpr int P = (NH / 2) * NS * 2;  // pieces per sub-tile, dealt round-robin over the 4 waves
-  if (wave < P % 4 || P % 4 == 0) oz_gram_w_body<NS, NH, (P + 3) / 4, LIVE, DIAG, false>(a, smem, wave, ct0, rt, chunk);
-  else oz_gram_w_body<NS, NH, P / 4, LIVE, DIAG, false>(a, smem, wave, ct0, rt, chunk);
+  if (wave < P % 4 || P % 4 == 0) oz_gram_w_body<NS, NH, (P + 3) / 4, LIVE, DIAG>(a, smem, wave, ct0, rt, chunk);
+  else oz_gram_w_body<NS, NH, P / 4, LIVE, DIAG>(a, smem, wave, ct0, rt, chunk);
 }
 
 template <int NS, int NH, int DIAG>
@@ -1129,31 +1121,6 @@ __device__ __forceinline__ void oz_gram_w_pass_live(const OzArgs& a, unsigned ch
                                                     uint32_t rt, uint32_t chunk, bool live) {
   if (live) oz_gram_w_pass<NS, NH, true, DIAG>(a, smem, wave, ct0, rt, chunk);
   else oz_gram_w_pass<NS, NH, false, DIAG>(a, smem, wave, ct0, rt, chunk);
-}
-
-// HALF blocks (128 replicates x 64 pairs, both column tiles present): NS digit slices for both tiles.
-template <int NS, int DIAG>
-__device__ __forceinline__ void oz_gram_h_live(const OzArgs& a, unsigned char* smem, int wave, uint32_t ct0,
-                                               uint32_t rt, uint32_t chunk, bool live) {
-  if (live) oz_gram_w_body<NS, 2, NS, true, DIAG, true>(a, smem, wave, ct0, rt, chunk);
-  else oz_gram_w_body<NS, 2, NS, false, DIAG, true>(a, smem, wave, ct0, rt, chunk);
-}
-
-// The half-wide tile for launches whose wide blocks would leave a partial last round: the wide
-// kernel's schedule on (chunk, 128 replicates, 64 pairs), so twice the blocks of the same size as
-// the 8-wave kernel's. Even column-tile counts only (every block has both tiles); a block with a
-// seven-slice tile runs seven slices on both (the six-slice tile's seventh digits are zero).
-template <int DIAG>
-__global__ __launch_bounds__(256, 1) __attribute__((amdgpu_waves_per_eu(1, 1))) void oz_gram_h_kernel(const OzArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint32_t dct, rt, chunk;
-  oz_map_w(a, &dct, &rt, &chunk);
-  const bool live = rt * 2u + (uint32_t)(wave >> 1) < a.nb_rep;
-  const uint32_t ct0 = 2u * dct;
-  const bool six = a.nsl[chunk * (uint32_t)a.n_ct + ct0] == 6 && a.nsl[chunk * (uint32_t)a.n_ct + ct0 + 1] == 6;
-  if (six) oz_gram_h_live<6, DIAG>(a, smem, wave, ct0, rt, chunk, live);
-  else oz_gram_h_live<7, DIAG>(a, smem, wave, ct0, rt, chunk, live);
 }
 
 template <int DIAG>
@@ -1394,58 +1361,41 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
   a.e_pad = p->e_pad;
   a.n_pairs_pad = p->oz_n_ct * kPairsPerTile;
   a.n_dct = (a.n_ct + 1) / 2;
-  // Which kernel (bitwise the same partials from all three): per launch the cheapest by rounds of
-  // blocks over the CUs x block cost, in units of the 8-wave kernel's block. The wide block does
-  // twice that work in kWideCost of its time but there are half as many, so a partial last round
-  // costs it more; the half-wide block (HALF: 128 replicates x 64 pairs, the wide schedule) does
-  // the same work as an 8-wave block in kHalfCost of its time, as many blocks. Measured (profiles/
-  // r06_ab_gram_tile_choice.txt, r06_ab_gram_half.txt): configs[1] wide 10.68-10.74 against
-  // 11.57 ms; configs[3] (5,000 x 3 outcomes) 7.03 against 7.16; 2,500 replicates 2.73-2.75
-  // against 3.00; configs[2]'s 1,250 share (640 wide blocks, 2.5 rounds) 1.58 against 1.56.
+  // Which kernel: the wide tile does a block's work (twice the 8-wave kernel's) in kWideCost of the
+  // 8-wave kernel's block time, but has half as many blocks, so a launch whose last round over the
+  // CUs is partial wastes more of it. Rounds x cost decides; both kernels give bitwise the same
+  // partials. Measured with the interleaved schedule (profiles/r06_ab_gram_tile_choice2.txt,
+  // r06_ab_gram_half.txt): configs[1] 10.68-10.90 against 11.57 ms; configs[3] (5,000 x 3 outcomes,
+  // 12.5 rounds) 7.03 against 7.16; 2,500 replicates (5 rounds) 2.65-2.75 against 2.93-3.00;
+  // configs[2]'s 1,250 share (640 wide blocks, 2.5 rounds) 1.53-1.60 against 1.54-1.56. (A half-wide
+  // tile, the same schedule on 128 replicates x 64 pairs for twice the blocks, measured 12.97 ms at
+  // configs[1] and 1.57-1.66 at 1,250, slower than both: half the MFMAs per sub-tile for the same
+  // barrier and DMA work, with one wave per SIMD.)
   const uint32_t wblocks = (uint32_t)n_chunks * a.n_rt * (uint32_t)a.n_dct;
   const uint32_t blocks8 = (uint32_t)n_chunks * a.n_rt * (uint32_t)a.n_ct;
-  const uint32_t n_rt2 = (nb_rep + 1) / 2;
-  const uint32_t hblocks = (uint32_t)n_chunks * n_rt2 * (uint32_t)a.n_dct;
   const uint32_t cus = (uint32_t)std::max(p->ctx->cus, 1);
-  const double kWideCost = 1.85, kHalfCost = OB_OZ_HALF_COST;
-  auto rounds = [&](uint32_t b) { return (double)((b + cus - 1) / cus); };
-  const double c8 = rounds(blocks8), cw = kWideCost * rounds(wblocks);
-  const double ch = (a.n_ct % 2 == 0) ? kHalfCost * rounds(hblocks) : 1e300;
+  const double kWideCost = 1.85;
+  const bool wide_pays = kWideCost * (double)((wblocks + cus - 1) / cus) <= (double)((blocks8 + cus - 1) / cus);
   const int tile = ob::opt_int(ob::Opt::GramTile, 0);
-  int kind = cw <= c8 && cw <= ch ? 2 : (ch < c8 ? 3 : 1);
-  if (tile == 1 || tile == 2) kind = tile;
-  if (tile == 3 && a.n_ct % 2 == 0) kind = 3;
-  p->timing.oz_wide = kind == 1 ? 0 : kind - 1;
-  auto wlaunch = [&](auto kern, uint32_t nblk) -> hipError_t {
-    hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWLds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(kern, dim3(nblk), dim3(256), kWLds, s, a);
-    return hipGetLastError();
-  };
-  if (kind == 3) {  // oz_gram_h_kernel: 4 waves, 128 replicates x 64 pairs per block
-    a.n_rt = n_rt2;
-#if OB_TUNING
-    switch (ob::opt_int(ob::Opt::GramDiag, 0) & 14) {
-      case 2: OZ_HIP(wlaunch(oz_gram_h_kernel<2>, hblocks)); break;
-      case 4: OZ_HIP(wlaunch(oz_gram_h_kernel<4>, hblocks)); break;
-      default: OZ_HIP(wlaunch(oz_gram_h_kernel<0>, hblocks)); break;
-    }
-#else
-    OZ_HIP(wlaunch(oz_gram_h_kernel<0>, hblocks));
-#endif
-    return OB_OK;
-  }
-  if (kind == 2) {  // oz_gram_w_kernel: 4 waves, 256 replicates x 64 pairs per block
+  const bool wide = tile == 2 || (tile != 1 && wide_pays);
+  p->timing.oz_wide = wide ? 1 : 0;
+  if (wide) {  // oz_gram_w_kernel: 4 waves, 256 replicates x 64 pairs per block
+    auto wlaunch = [&](auto kern) -> hipError_t {
+      hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWLds);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(kern, dim3(wblocks), dim3(256), kWLds, s, a);
+      return hipGetLastError();
+    };
 #if OB_TUNING  // timing ablations (gram_diag): wrong results by design
     switch (ob::opt_int(ob::Opt::GramDiag, 0) & 14) {
-      case 2: OZ_HIP(wlaunch(oz_gram_w_kernel<2>, wblocks)); break;
-      case 4: OZ_HIP(wlaunch(oz_gram_w_kernel<4>, wblocks)); break;
-      case 8: OZ_HIP(wlaunch(oz_gram_w_kernel<8>, wblocks)); break;
-      case 6: OZ_HIP(wlaunch(oz_gram_w_kernel<6>, wblocks)); break;
-      default: OZ_HIP(wlaunch(oz_gram_w_kernel<0>, wblocks)); break;
+      case 2: OZ_HIP(wlaunch(oz_gram_w_kernel<2>)); break;
+      case 4: OZ_HIP(wlaunch(oz_gram_w_kernel<4>)); break;
+      case 8: OZ_HIP(wlaunch(oz_gram_w_kernel<8>)); break;
+      case 6: OZ_HIP(wlaunch(oz_gram_w_kernel<6>)); break;
+      default: OZ_HIP(wlaunch(oz_gram_w_kernel<0>)); break;
     }
 #else
-    OZ_HIP(wlaunch(oz_gram_w_kernel<0>, wblocks));
+    OZ_HIP(wlaunch(oz_gram_w_kernel<0>));
 #endif
     return OB_OK;
   }

@@ -85,14 +85,3 @@ def test_shipped_wide_gram_kernel_waits_are_clean():
     mfma = sum(1 for i in insns if i.mnem.startswith("v_mfma_i32_16x16x64_i8"))
     assert dma >= 64 and bars >= 40 and mfma >= 1000, (len(insns), dma, bars, mfma)
     assert C.check(insns) == []
-
-
-def test_shipped_half_wide_gram_kernel_waits_are_clean():
-    """The half-wide variant (oz_gram_h_kernel: the wide schedule on 128 replicates x 64 pairs)."""
-    if not os.path.exists(SO) or not os.path.exists(os.path.join(C.LLVM, "llvm-objdump")):
-        pytest.skip("engine library or llvm-objdump missing (run __graft_entry__.build())")
-    sym = "_ZN12_GLOBAL__N_116oz_gram_h_kernelILi0EEEvNS_6OzArgsE"
-    insns = C.parse(C.disassemble_symbol(SO, sym), sym)
-    assert sum(1 for i in insns if i.mnem.startswith("v_mfma_i32_16x16x64_i8")) >= 200
-    assert C.check(insns) == []
-
