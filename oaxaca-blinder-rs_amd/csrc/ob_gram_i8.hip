@@ -987,8 +987,8 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
       constexpr int q = decltype(Q)::value;
 #pragma unroll
       for (int m = 0; m < 4; ++m) mfma1(m, q, h, af, bf);
-      nb[q] = bb[q * 128];
-      if constexpr (q < 4) {
+      if constexpr (!(DIAG & 128)) nb[q] = bb[q * 128];  // DIAG 128 (timing only): no B reads in the loop
+      if constexpr (q < 4 && !(DIAG & 256)) {               // DIAG 256 (timing only): no A reads
         if (an) an[q] = bs[rb * STAGE + STAGE_B + (wave * 4 + q) * 64 + lane];
       }
       if constexpr (h * NS + q < T) {
@@ -1387,8 +1387,11 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
       return hipGetLastError();
     };
 #if OB_TUNING  // timing ablations (gram_diag): wrong results by design
-    switch (ob::opt_int(ob::Opt::GramDiag, 0) & 14) {
+    switch (ob::opt_int(ob::Opt::GramDiag, 0) & 398) {
       case 2: OZ_HIP(wlaunch(oz_gram_w_kernel<2>)); break;
+      case 128: OZ_HIP(wlaunch(oz_gram_w_kernel<128>)); break;
+      case 256: OZ_HIP(wlaunch(oz_gram_w_kernel<256>)); break;
+      case 384: OZ_HIP(wlaunch(oz_gram_w_kernel<384>)); break;
       case 4: OZ_HIP(wlaunch(oz_gram_w_kernel<4>)); break;
       case 8: OZ_HIP(wlaunch(oz_gram_w_kernel<8>)); break;
       case 6: OZ_HIP(wlaunch(oz_gram_w_kernel<6>)); break;
