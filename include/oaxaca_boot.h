@@ -268,6 +268,9 @@ int ob_debug_mm_betas(ob_panel* panel, uint64_t seed, int32_t simulations, uint6
                    block count favours; their Grams are bitwise equal)
      "debug_count_overflow" nonzero: the resample's count-overflow word is raised after every
                    count kernel of a Machado-Mata run or ob_debug_counts (tests the OB_E_OVERFLOW path)
+     "rs_double"   1: two level-1 / count-image buffers per panel, so each boot segment's resample
+                   runs under the previous segment's Gram (rows bitwise unchanged; twice the image HBM),
+                   0: one buffer (default: the engine's rule)
    Unknown names are OB_E_INVALID. ob_get_option reads back what ob_set_option stored (NaN: unset). ob_tuning_build() is 1 in a -DOB_TUNING=1 build (`make tuning`),
    which also reads OB_<NAME> from the environment for options nobody set. */
 int ob_set_option(const char* name, double value);

@@ -1834,6 +1834,7 @@ int engine_mark(ob_panel* p, hipStream_t s, bool scratch) {
   if (scratch) {
     if (!p->scratch_ev) HIP_OK(hipEventCreateWithFlags(&p->scratch_ev, hipEventDisableTiming));
     HIP_OK(hipEventRecord(p->scratch_ev, s));
+    if (p->scratch_ev2) HIP_OK(hipEventRecord(p->scratch_ev2, s));
     p->scratch_recorded = true;
   }
   return OB_OK;
@@ -1934,6 +1935,17 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     }
   }
   const hipStream_t sr = overlap ? p->rs_stream : s;
+  // two m1 / count-image buffers (ob_engine.hpp): a segment's resample then waits only for the Gram
+  // two segments back and runs under the previous one's
+  const bool dbl = overlap && ob::opt_int(ob::Opt::RsDouble, 0) == 1;
+  if (dbl) {
+    OB_TRY(ensure_buf(&p->d_m1b, p->cap_m1b, (size_t)tiles * pl.rep_pad));
+    OB_TRY(ensure_buf(&p->d_countsb, p->cap_countsb, (size_t)tiles * pl.nb_rep * 4 * kCimgWords));
+    if (!p->scratch_ev2) {
+      HIP_OK(hipEventCreateWithFlags(&p->scratch_ev2, hipEventDisableTiming));
+      HIP_OK(hipEventRecord(p->scratch_ev2, s));
+    }
+  }
   for (uint64_t s0 = 0; s0 < n_reps; s0 += seg) {
     const uint32_t ns = (uint32_t)std::min<uint64_t>(seg, n_reps - s0);
     const Plan& plx = (ns == seg) ? pl : pl_tail;
@@ -1941,21 +1953,26 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     const uint32_t frep = (uint32_t)(first_rep + s0);
     hipEvent_t* ev = p->seg_events.data() + kSegEvents * (size_t)p->pending_segments;
     const bool timed = true;
-    if (overlap) HIP_OK(hipStreamWaitEvent(sr, p->scratch_ev, 0));
+    const int buf = dbl ? p->rs_parity : 0;
+    uint32_t* const m1 = buf ? p->d_m1b : p->d_m1;
+    uint32_t* const counts = buf ? p->d_countsb : p->d_counts;
+    const hipEvent_t sev = buf ? p->scratch_ev2 : p->scratch_ev;  // the last read of this buffer
+    if (dbl) p->rs_parity ^= 1;
+    if (overlap) HIP_OK(hipStreamWaitEvent(sr, sev, 0));
     if (timed) HIP_OK(hipEventRecord(ev[0], sr));
     hipLaunchKernelGGL(l1k, dim3(ns, 2), dim3(kBlock), lds_l1, sr, p->n[0], p->n[1], p->ntiles[0], frep,
-                       tiles, key0, key1, p->d_m1, ky);
+                       tiles, key0, key1, m1, ky);
     HIP_OK(hipGetLastError());
     if (timed) HIP_OK(hipEventRecord(ev[1], sr));
     GramArgs ga = gram_args(p, plx);
     ga.chunks = p->d_chunks;
-    ga.m1 = p->d_m1;
+    ga.m1 = m1;
     ga.n_reps = ns;
     ga.first_rep = frep;
     ga.key0 = key0;
     ga.key1 = key1;
     ga.partial = p->d_partial;
-    ga.counts = p->d_counts;
+    ga.counts = counts;
     ga.tiles_total = tiles;
     ga.diag = diag_mode();
     const dim3 cgrid((tiles + kCntTilesPerBlock - 1) / kCntTilesPerBlock, plx.nb_rep);
@@ -1969,27 +1986,27 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     }
     if (timed) HIP_OK(hipEventRecord(ev[3], s));
     if (use_i8) {
-      OB_TRY(ob::oz_gram(p, p->d_chunks, nchx, p->d_counts, plx.nb_rep, plx.rep_pad, ns, p->d_partial, s));
+      OB_TRY(ob::oz_gram(p, p->d_chunks, nchx, counts, plx.nb_rep, plx.rep_pad, ns, p->d_partial, s));
     } else {
       const uint32_t blocks = plx.nb_rep * plx.n_cg * (uint32_t)nchx;
       HIP_OK(launch_gram(p, plx.cb, false, ga, blocks, s));
     }
     if (timed) HIP_OK(hipEventRecord(ev[4], s));
     const bool exc = use_i8 && ob::oz_exceptions_pending(p);
-    if (overlap && !exc) HIP_OK(hipEventRecord(p->scratch_ev, s));  // the count images are free again
+    if (overlap && !exc) HIP_OK(hipEventRecord(sev, s));  // the count images are free again
     const size_t nred = (size_t)ns * p->e_pad;
     hipLaunchKernelGGL(ob_reduce_kernel, dim3((unsigned)((nred + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
                        (const double*)p->d_partial, (const uint32_t*)p->d_chunks, nchx, plx.rep_pad, p->e_pad, ns,
                        p->d_gram);
     HIP_OK(hipGetLastError());
     if (exc) {
-      OB_TRY(ob::oz_exceptions(p, p->d_counts, plx.nb_rep, ns, p->d_gram, s));
-      if (overlap) HIP_OK(hipEventRecord(p->scratch_ev, s));
+      OB_TRY(ob::oz_exceptions(p, counts, plx.nb_rep, ns, p->d_gram, s));
+      if (overlap) HIP_OK(hipEventRecord(sev, s));
     }
     if (timed) HIP_OK(hipEventRecord(ev[5], s));
     if (p->heckman) {  // probit iterations + IMR sums + two-step solve (synchronizes the stream)
       ob_heck_seg hs = heck_seg(p, plx, p->d_chunks, p->d_gram, ref_mode);
-      hs.counts = p->d_counts;
+      hs.counts = counts;
       hs.counts_i8 = use_i8 ? 1 : 0;
       hs.n_reps = ns;
       hs.rows = d_rows + s0 * p->row_len;
@@ -2271,6 +2288,8 @@ void ob_panel_destroy(ob_panel* p) {
   (void)hipFree(p->d_norm);
   (void)hipFree(p->d_m1);
   (void)hipFree(p->d_counts);
+  (void)hipFree(p->d_m1b);
+  (void)hipFree(p->d_countsb);
   (void)hipFree(p->d_partial);
   (void)hipFree(p->d_gram);
   (void)hipFree(p->d_chunks);
@@ -2286,6 +2305,7 @@ void ob_panel_destroy(ob_panel* p) {
   if (p->rs_stream) (void)hipStreamSynchronize(p->rs_stream);
   if (p->rs_ev) (void)hipEventDestroy(p->rs_ev);
   if (p->scratch_ev) (void)hipEventDestroy(p->scratch_ev);
+  if (p->scratch_ev2) (void)hipEventDestroy(p->scratch_ev2);
   if (p->rs_stream) (void)hipStreamDestroy(p->rs_stream);
   ob::shard_free(p);
   ob::oz_free(p);

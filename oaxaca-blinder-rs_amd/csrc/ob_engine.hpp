@@ -142,6 +142,15 @@ struct ob_panel {
   hipStream_t rs_stream = nullptr;
   hipEvent_t rs_ev = nullptr, scratch_ev = nullptr;
   bool scratch_recorded = false;
+  // Double-buffered resample (option rs_double): a second m1 / count-image pair, so segment k + 1's
+  // level 1 and counts (buffer (k + 1) & 1) wait only for the Gram of segment k - 1 (scratch_ev2
+  // marks the second buffer's last read) and run under the Gram of segment k. rs_parity is the
+  // buffer of the next boot segment.
+  uint32_t* d_m1b = nullptr;
+  uint32_t* d_countsb = nullptr;
+  size_t cap_m1b = 0, cap_countsb = 0;
+  hipEvent_t scratch_ev2 = nullptr;
+  int rs_parity = 0;
 };
 
 namespace ob {

@@ -471,3 +471,38 @@ def test_level1_tree_shapes_match_oracle(ob, O, na, nb):
     orows, ook = O.boot_ref(cfg, O.with_intercept(xa), ya, None, O.with_intercept(xb), yb, None, SEED, 5, 4,
                             threads=8, full=False)
     assert ok.all() and ook.all() and close(rows, orows, abs(orows[0, 5]))[0]
+
+
+def test_double_buffered_resample_bitwise(ob, O):
+    """Option rs_double: two m1 / count-image buffers, so each boot segment's level 1 and counts run
+    under the previous segment's Gram (ob_engine.hpp). The kernels and their inputs are unchanged,
+    so the rows equal the one-buffer run bitwise: single calls, calls enqueued back to back on the
+    device API with one sync, a two-segment call, and a point estimate and a debug-counts call (both
+    on the first buffer) between boots."""
+    import torch
+
+    panel, _, _ = make(O, ob, 5000, 6, True)
+    want = [panel.boot(SEED, r0, 300, 2) for r0 in (0, 300, 600)]
+    pe = panel.point_estimate(2)
+    cnt = panel.debug_counts(SEED, 7, 64, 1)
+    small, _, _ = make(O, ob, 600, 2, False)
+    long_rows, long_ok = small.boot(SEED, 0, 16500, 0)
+    with ob._native.option("rs_double", 1):
+        got = [panel.boot(SEED, r0, 300, 2) for r0 in (0, 300, 600)]
+        for (a, oa), (b, obb) in zip(want, got):
+            assert np.array_equal(a, b) and np.array_equal(oa, obb)
+        dev = torch.device("cuda", 0)
+        rows = torch.empty((900, panel.row_len), dtype=torch.float64, device=dev)
+        ok = torch.empty(900, dtype=torch.uint8, device=dev)
+        for i, r0 in enumerate((0, 300, 600)):
+            panel.boot_device(SEED, r0, 300, rows[300 * i:].data_ptr(), ok[300 * i:].data_ptr(), 2)
+        panel.sync()
+        assert np.array_equal(rows.cpu().numpy(), np.vstack([w[0] for w in want]))
+        assert np.array_equal(ok.cpu().numpy(), np.concatenate([w[1] for w in want]))
+        b0 = panel.boot(SEED, 0, 300, 2)
+        assert np.array_equal(panel.point_estimate(2), pe)
+        assert all(np.array_equal(x, y) for x, y in zip(panel.debug_counts(SEED, 7, 64, 1), cnt))
+        b1 = panel.boot(SEED, 300, 300, 2)
+        assert np.array_equal(b0[0], want[0][0]) and np.array_equal(b1[0], want[1][0])
+        r2, o2 = small.boot(SEED, 0, 16500, 0)
+        assert np.array_equal(r2, long_rows) and np.array_equal(o2, long_ok)
