@@ -1936,8 +1936,13 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   }
   const hipStream_t sr = overlap ? p->rs_stream : s;
   // two m1 / count-image buffers (ob_engine.hpp): a segment's resample then waits only for the Gram
-  // two segments back and runs under the previous one's
-  const bool dbl = overlap && ob::opt_int(ob::Opt::RsDouble, 0) == 1;
+  // two segments back and runs under the previous one's. By default only under the 8-wave i8 Gram:
+  // its partial last rounds leave CUs to the resample (configs[2]'s 1,250 share: 536-545k -> 561-562k
+  // replicates/s), while a wide-tile block needs a whole CU's LDS, so resample blocks there delay
+  // the Gram more than they hide (5,000 / 2,500 / 10k replicates: -9 / -11 / -4.5 %;
+  // profiles/r06_ab_rs_double.txt)
+  const int rs_opt = ob::opt_int(ob::Opt::RsDouble, -1);
+  const bool dbl = overlap && (rs_opt == 1 || (rs_opt < 0 && use_i8 && !ob::oz_wide(p, nch, pl.nb_rep)));
   if (dbl) {
     OB_TRY(ensure_buf(&p->d_m1b, p->cap_m1b, (size_t)tiles * pl.rep_pad));
     OB_TRY(ensure_buf(&p->d_countsb, p->cap_countsb, (size_t)tiles * pl.nb_rep * 4 * kCimgWords));

@@ -171,6 +171,8 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
             uint32_t rep_pad, uint32_t n_reps, double* partial, hipStream_t s);
 // adds the exception rows' f64 terms to the reduced Grams [rep][2][e_pad] of a segment
 bool oz_exceptions_pending(const ob_panel* p);
+// whether oz_gram runs the wide-tile kernel for a launch of nb_rep 64-replicate batches
+bool oz_wide(const ob_panel* p, int n_chunks, uint32_t nb_rep);
 int oz_exceptions(ob_panel* p, const uint32_t* counts, uint32_t nb_rep, uint32_t n_reps, double* gram, hipStream_t s);
 // after the stream is synchronized: exception count / bits into p->timing, overflow -> error
 int oz_collect(ob_panel* p);

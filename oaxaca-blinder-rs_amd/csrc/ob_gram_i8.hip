@@ -1108,6 +1108,219 @@ __device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* s
   __syncthreads();  // the staging is done before a next pass refills the ring
 }
 
+// OB_OZ_W_GRID 1: the same block tile and ring, the waves as a 2 x 2 grid. Wave w = (wr = w & 1,
+// wc = w >> 1) owns replicate batches 2 wr, 2 wr + 1 (8 replicate blocks) and pair blocks
+// wc NHW .. wc NHW + NHW - 1 (NHW = NH / 2: column tile ct0 + wc when NH = 4, one half of ct0 when
+// NH = 2): per sub-tile 8 A and NHW NS B fragment reads for the same 8 x NS x NHW MFMAs, against 4 A
+// and NH NS B in the 1 x 4 layout above (20 reads per 96 MFMAs instead of 28: the B reads are what
+// the gram_diag 128 ablation found costly). The DMA is unchanged (wave w loads B pieces t * 4 + w and
+// its own batch w's A, DLIVE: batch w exists), so every wait is the 1 x 4 body's. A step is 2 NHW
+// units (pair block h, replicate half mh) of 4 NS MFMAs, h-major; the last unit (the last two when
+// NHW = 2) runs after the barrier and reads the next sub-tile's first B block and A. MLIVE: batch
+// 2 wr exists (the wave computes; a dead second batch computes on stale LDS and is never stored).
+template <int NS, int NH, int NB, bool DLIVE, bool MLIVE, int DIAG>
+__device__ __forceinline__ void oz_gram_w2_body(const OzArgs& a, unsigned char* smem, int wave, uint32_t ct0,
+                                                uint32_t rt, uint32_t chunk) {
+  constexpr int NHW = NH / 2;                // pair blocks per wave
+  constexpr int U = 2 * NHW;                 // units per step
+  constexpr int POST = NHW > 1 ? 2 : 1;      // units after the barrier
+  constexpr int NC = NH / 2;
+  constexpr int PIECES = NC * NS * 2;
+  constexpr int STAGE_B = PIECES * 64;
+  constexpr int STAGE = STAGE_B + 4 * 4 * 64;
+  constexpr int T = NB + (DLIVE ? 4 : 0);
+  constexpr int PER = (kWNbuf - 2) * T;
+  constexpr int PRE_SLOTS = (U - POST) * NS;  // DMA slots before the barrier
+  static_assert(PRE_SLOTS >= 1, "at least one unit before the barrier");
+  const ob_v4i* bs = reinterpret_cast<const ob_v4i*>(smem);
+  const int lane = threadIdx.x & 63;
+  const int wr = wave & 1, wc = wave >> 1;
+  const uint32_t g = a.chunks[3 * chunk];
+  const uint32_t n = g ? a.n1 : a.n0, tg0 = g ? a.tiles0 : 0u;
+  const uint32_t s0 = a.chunks[3 * chunk + 1] * 4u;
+  const uint32_t s1 = min(a.chunks[3 * chunk + 2] * 4u, (n + 63u) >> 6);
+  const ob_v4i* Bg = g ? a.B1 : a.B0;
+  const uint32_t dbatch = rt * 4u + (uint32_t)wave;  // the batch whose A this wave DMAs
+  auto dma = [&](int buf, uint32_t s, auto LO, auto HI) {
+    constexpr int lo = decltype(LO)::value, hi = decltype(HI)::value;
+#pragma unroll
+    for (int t = lo; t < hi; ++t) {
+      if (t < NB) {
+        const int piece = t * 4 + wave, c = piece / (NS * 2), q = piece - c * (NS * 2);
+        const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct0 + c) * kSubUnits + q * 64;
+        oz_dma16(src + lane, (uint32_t)(buf * STAGE + piece * 64) * 16u);
+      } else {
+        const int m = t - NB;
+        const ob_v4i* src_a = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + dbatch) * 4 + (s & 3)) * 256;
+        oz_dma16(src_a + m * 64 + lane, (uint32_t)(buf * STAGE + STAGE_B + (wave * 4 + m) * 64) * 16u);
+      }
+    }
+  };
+  auto dma1 = [&](int buf, uint32_t s, auto TT) {
+    constexpr int t = decltype(TT)::value;
+    if constexpr (t < NB) {
+      const int piece = t * 4 + wave, c = piece / (NS * 2), q = piece - c * (NS * 2);
+      const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct0 + c) * kSubUnits + q * 64;
+      oz_dma16s((uint32_t)lane * 16u, src, (uint32_t)(buf * STAGE + piece * 64) * 16u);
+    } else {
+      constexpr int m = t - NB;
+      const ob_v4i* src_a = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + dbatch) * 4 + (s & 3)) * 256 + m * 64;
+      oz_dma16s((uint32_t)lane * 16u, src_a, (uint32_t)(buf * STAGE + STAGE_B + (wave * 4 + m) * 64) * 16u);
+    }
+  };
+  // this wave's 8 A fragments: batches 2 wr, 2 wr + 1, blocks 0..3 each
+  auto aread1 = [&](int buf, int m) { return bs[buf * STAGE + STAGE_B + (8 * wr + m) * 64 + lane]; };
+  // B fragment q of this wave's pair block h
+  auto bread1 = [&](int buf, int h, int q) {
+    const int hg = wc * NHW + h;
+    return bs[buf * STAGE + ((hg >> 1) * NS * 2 + (hg & 1)) * 64 + q * 128 + lane];
+  };
+  ob_v4i ar[2][8];
+  ob_v4i fb[2][NS];
+  ob_v4i acc[8][NS][NHW];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int q = 0; q < NS; ++q)
+#pragma unroll
+      for (int h = 0; h < NHW; ++h) acc[m][q][h] = (ob_v4i){};
+  auto mfma1 = [&](int m, int q, int h, const ob_v4i& af, const ob_v4i& bf) {
+    if ((m * NS + q) * NHW + h < kWAgprTiles)
+      asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+a"(acc[m][q][h]) : "v"(af), "v"(bf));
+    else
+      asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+v"(acc[m][q][h]) : "v"(af), "v"(bf));
+  };
+  constexpr int AHEAD = kWNbuf - 1;
+#pragma unroll
+  for (int j = 0; j < AHEAD; ++j)
+    if (s0 + j < s1) dma(j, s0 + j, IC<0>{}, IC<T>{});
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if constexpr (MLIVE) {
+#pragma unroll
+    for (int q = 0; q < NS; ++q) fb[0][q] = bread1(0, 0, q);
+#pragma unroll
+    for (int m = 0; m < 8; ++m) ar[0][m] = aread1(0, m);
+  }
+  // unit u = (h = u >> 1, mh = u & 1) of a step with parity j: 4 NS MFMAs on ar[j][4 mh ..] and
+  // fb[(h + j NHW) & 1]; slot q (after the 4 MFMAs of slice q) issues this unit's reads and DMAs
+  auto unit = [&](auto J, auto UU, int buf, int bnext, uint32_t snext) {
+    constexpr int j = decltype(J)::value, u = decltype(UU)::value;
+    constexpr int h = u >> 1, mh = u & 1;
+    constexpr int fcur = (h + j * NHW) & 1, fnext = (h + 1 + j * NHW) & 1;
+    constexpr bool pre = u < U - POST;
+    auto slot = [&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) mfma1(4 * mh + m, q, h, ar[j][4 * mh + m], fb[fcur][q]);
+      if constexpr (pre) {
+        // the next pair block of this sub-tile, during its first unit; the step's DMAs one or two per slot
+        if constexpr (mh == 0 && h + 1 < NHW && !(DIAG & 128)) fb[fnext][q] = bread1(buf, h + 1, q);
+        constexpr int k = u * NS + q;  // slot index before the barrier
+        if constexpr (k < T && !(DIAG & 4)) dma1(bnext, snext, IC<k>{});
+        if constexpr (k + PRE_SLOTS < T && !(DIAG & 4)) dma1(bnext, snext, IC<k + PRE_SLOTS>{});
+      } else {
+        // after the barrier: the next sub-tile's first B block, then its A
+        constexpr int pu = u - (U - POST);  // 0 .. POST - 1
+        const int nbuf = (buf + 1) % kWNbuf;
+        constexpr bool rb = !(DIAG & 128), ra = !(DIAG & 256);  // timing ablations: no B / A reads
+        if constexpr (POST == 2) {
+          if constexpr (pu == 0) {
+            if constexpr (rb) fb[fnext][q] = bread1(nbuf, 0, q);
+          } else if constexpr (ra) {
+            ar[j ^ 1][q] = aread1(nbuf, q);
+            if constexpr (q + NS < 8) ar[j ^ 1][q + NS] = aread1(nbuf, q + NS);
+          }
+        } else {
+          if constexpr (rb) fb[fnext][q] = bread1(nbuf, 0, q);
+          if constexpr (ra) {
+            ar[j ^ 1][q] = aread1(nbuf, q);
+            if constexpr (q + NS < 8) ar[j ^ 1][q + NS] = aread1(nbuf, q + NS);
+          }
+        }
+      }
+    };
+    __builtin_amdgcn_sched_barrier(0);
+    slot(IC<0>{}); slot(IC<1>{}); slot(IC<2>{}); slot(IC<3>{}); slot(IC<4>{}); slot(IC<5>{});
+    if constexpr (NS > 6) slot(IC<6>{});
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  static_assert(2 * PRE_SLOTS >= T, "the pre-barrier slots hold every DMA of a step");
+  auto step = [&](uint32_t s, auto J) {
+    const int buf = (int)((s - s0) % kWNbuf);
+    const uint32_t snext = min(s + AHEAD, s1 - 1);
+    const int bnext = (buf + AHEAD) % kWNbuf;
+    if constexpr (MLIVE && !(DIAG & 2)) {
+      unit(J, IC<0>{}, buf, bnext, snext);
+      if constexpr (U - POST > 1) unit(J, IC<1>{}, buf, bnext, snext);
+      if constexpr (DIAG & 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+      if constexpr (DIAG & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // timing only: no barrier
+      else oz_barrier();
+      if constexpr (POST == 2) {
+        unit(J, IC<U - 2>{}, buf, bnext, snext);
+        unit(J, IC<U - 1>{}, buf, bnext, snext);
+      } else {
+        unit(J, IC<U - 1>{}, buf, bnext, snext);
+      }
+      return;
+    }
+    // dead waves (and gram_diag 2): no MFMAs, the step's DMA in one burst before the barrier
+    if constexpr (!(DIAG & 4)) dma(bnext, snext, IC<0>{}, IC<T>{});
+    if constexpr (DIAG & 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+    if constexpr (DIAG & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // as the live waves
+    else oz_barrier();
+  };
+  uint32_t s = s0;
+  for (; s + 2 <= s1; s += 2) {
+    step(s, IC<0>{});
+    step(s + 1, IC<1>{});
+  }
+  if (s < s1) step(s, IC<0>{});
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if constexpr (MLIVE) {
+    // as oz_gram_w_body's epilogue, four replicate blocks at a time through this wave's quarter of the ring
+    ob_v4i* st = reinterpret_cast<ob_v4i*>(smem) + (size_t)wave * (4 * NS * 64);
+#pragma unroll
+    for (int h = 0; h < NHW; ++h) {
+      const int hg = wc * NHW + h;
+      const int pair = (int)(ct0 + (hg >> 1)) * kPairsPerTile + 16 * (hg & 1) + (lane & 15);
+      const int E = a.pexp[chunk * a.n_pairs_pad + min(pair, a.n_pairs_pad - 1)];
+      const int sh0 = E - kFracBits + 8 * (kS - 0 - kSlo), sh1 = E - kFracBits + 8 * (kS - kSlo - (NS - kSlo));
+#pragma unroll
+      for (int mh = 0; mh < 2; ++mh) {
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int q = 0; q < NS; ++q) st[(m * NS + q) * 64 + lane] = acc[4 * mh + m][q][h];
+        __builtin_amdgcn_sched_barrier(0);
+        const uint32_t batch = rt * 4u + 2u * (uint32_t)wr + (uint32_t)mh;
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            long long p0 = 0, p1 = 0;
+#pragma unroll
+            for (int q = 0; q < kSlo; ++q) p0 = p0 * 256 + st[(m * NS + q) * 64 + lane][i];
+#pragma unroll
+            for (int q = kSlo; q < NS; ++q) p1 = p1 * 256 + st[(m * NS + q) * 64 + lane][i];
+            const double val = ldexp((double)p0, sh0) + ldexp((double)p1, sh1);
+            const uint32_t rep = batch * 64u + (uint32_t)(16 * m + 4 * (lane >> 4) + i);
+            if (pair < a.e_pad && rep < a.n_reps) a.partial[((size_t)chunk * a.rep_pad + rep) * a.e_pad + pair] = val;
+          }
+      }
+    }
+  }
+  __syncthreads();
+}
+
+#ifndef OB_OZ_W_GRID
+#define OB_OZ_W_GRID 1  // 1: oz_gram_w2_body (2 x 2 wave grid); 0: oz_gram_w_body (1 x 4)
+#endif
+
 template <int NS, int NH, bool LIVE, int DIAG>
 __device__ __forceinline__ void oz_gram_w_pass(const OzArgs& a, unsigned char* smem, int wave, uint32_t ct0,
                                                uint32_t rt, uint32_t chunk) {
@@ -1116,11 +1329,27 @@ __device__ __forceinline__ void oz_gram_w_pass(const OzArgs& a, unsigned char* s
   else oz_gram_w_body<NS, NH, P / 4, LIVE, DIAG>(a, smem, wave, ct0, rt, chunk);
 }
 
+template <int NS, int NH, bool DLIVE, bool MLIVE, int DIAG>
+__device__ __forceinline__ void oz_gram_w2_pass(const OzArgs& a, unsigned char* smem, int wave, uint32_t ct0,
+                                                uint32_t rt, uint32_t chunk) {
+  constexpr int P = (NH / 2) * NS * 2;
+  if (wave < P % 4 || P % 4 == 0) oz_gram_w2_body<NS, NH, (P + 3) / 4, DLIVE, MLIVE, DIAG>(a, smem, wave, ct0, rt, chunk);
+  else oz_gram_w2_body<NS, NH, P / 4, DLIVE, MLIVE, DIAG>(a, smem, wave, ct0, rt, chunk);
+}
+
 template <int NS, int NH, int DIAG>
 __device__ __forceinline__ void oz_gram_w_pass_live(const OzArgs& a, unsigned char* smem, int wave, uint32_t ct0,
                                                     uint32_t rt, uint32_t chunk, bool live) {
-  if (live) oz_gram_w_pass<NS, NH, true, DIAG>(a, smem, wave, ct0, rt, chunk);
-  else oz_gram_w_pass<NS, NH, false, DIAG>(a, smem, wave, ct0, rt, chunk);
+  if constexpr (OB_OZ_W_GRID) {
+    const bool mlive = rt * 4u + 2u * (uint32_t)(wave & 1) < a.nb_rep;
+    if (live && mlive) oz_gram_w2_pass<NS, NH, true, true, DIAG>(a, smem, wave, ct0, rt, chunk);
+    else if (live) oz_gram_w2_pass<NS, NH, true, false, DIAG>(a, smem, wave, ct0, rt, chunk);
+    else if (mlive) oz_gram_w2_pass<NS, NH, false, true, DIAG>(a, smem, wave, ct0, rt, chunk);
+    else oz_gram_w2_pass<NS, NH, false, false, DIAG>(a, smem, wave, ct0, rt, chunk);
+  } else {
+    if (live) oz_gram_w_pass<NS, NH, true, DIAG>(a, smem, wave, ct0, rt, chunk);
+    else oz_gram_w_pass<NS, NH, false, DIAG>(a, smem, wave, ct0, rt, chunk);
+  }
 }
 
 template <int DIAG>
@@ -1340,6 +1569,16 @@ void oz_free(ob_panel* p) {
 
 // One segment's Gram partials: d_chunks holds the panel's chunk table, counts the I8 images of
 // the segment's nb_rep replicate batches.
+bool oz_wide(const ob_panel* p, int n_chunks, uint32_t nb_rep) {
+  const uint32_t n_rt = (nb_rep + 3) / 4, n_ct = (uint32_t)p->oz_n_ct, n_dct = (n_ct + 1) / 2;
+  const uint32_t wblocks = (uint32_t)n_chunks * n_rt * n_dct, blocks8 = (uint32_t)n_chunks * n_rt * n_ct;
+  const uint32_t cus = (uint32_t)std::max(p->ctx->cus, 1);
+  const double kWideCost = 1.85;
+  const bool wide_pays = kWideCost * (double)((wblocks + cus - 1) / cus) <= (double)((blocks8 + cus - 1) / cus);
+  const int tile = ob::opt_int(ob::Opt::GramTile, 0);
+  return tile == 2 || (tile != 1 && wide_pays);
+}
+
 int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t* counts, uint32_t nb_rep,
             uint32_t rep_pad, uint32_t n_reps, double* partial, hipStream_t s) {
   OzArgs a{};
@@ -1373,11 +1612,7 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
   // barrier and DMA work, with one wave per SIMD.)
   const uint32_t wblocks = (uint32_t)n_chunks * a.n_rt * (uint32_t)a.n_dct;
   const uint32_t blocks8 = (uint32_t)n_chunks * a.n_rt * (uint32_t)a.n_ct;
-  const uint32_t cus = (uint32_t)std::max(p->ctx->cus, 1);
-  const double kWideCost = 1.85;
-  const bool wide_pays = kWideCost * (double)((wblocks + cus - 1) / cus) <= (double)((blocks8 + cus - 1) / cus);
-  const int tile = ob::opt_int(ob::Opt::GramTile, 0);
-  const bool wide = tile == 2 || (tile != 1 && wide_pays);
+  const bool wide = oz_wide(p, n_chunks, nb_rep);
   p->timing.oz_wide = wide ? 1 : 0;
   if (wide) {  // oz_gram_w_kernel: 4 waves, 256 replicates x 64 pairs per block
     auto wlaunch = [&](auto kern) -> hipError_t {

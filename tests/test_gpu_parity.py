@@ -482,11 +482,12 @@ def test_double_buffered_resample_bitwise(ob, O):
     import torch
 
     panel, _, _ = make(O, ob, 5000, 6, True)
-    want = [panel.boot(SEED, r0, 300, 2) for r0 in (0, 300, 600)]
-    pe = panel.point_estimate(2)
-    cnt = panel.debug_counts(SEED, 7, 64, 1)
     small, _, _ = make(O, ob, 600, 2, False)
-    long_rows, long_ok = small.boot(SEED, 0, 16500, 0)
+    with ob._native.option("rs_double", 0):
+        want = [panel.boot(SEED, r0, 300, 2) for r0 in (0, 300, 600)]
+        pe = panel.point_estimate(2)
+        cnt = panel.debug_counts(SEED, 7, 64, 1)
+        long_rows, long_ok = small.boot(SEED, 0, 16500, 0)
     with ob._native.option("rs_double", 1):
         got = [panel.boot(SEED, r0, 300, 2) for r0 in (0, 300, 600)]
         for (a, oa), (b, obb) in zip(want, got):

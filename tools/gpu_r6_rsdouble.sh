@@ -10,9 +10,9 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --ti
   || { tail -40 gpurun_out/${T}_tests.log; exit 1; }
 tail -1 gpurun_out/${T}_tests.log
 source "$(dirname "${BASH_SOURCE[0]}")/tuning_env.sh"
-for r in 1 2 3; do
+for r in $(seq ${PASSES:-3}); do
   for v in 0 1; do
-    for R in 10000 1250; do
+    for R in ${SIZES:-10000 1250}; do
       out=gpurun_out/${T}_d${v}_${R}_$r.json
       OB_RS_DOUBLE=$v timeout -k 10 300 python bench.py --reps $R --cpu-seconds 0 --no-e2e --steps 20 --warmup 5 \
         > $out 2> ${out%.json}.err || { tail -20 ${out%.json}.err; exit 1; }
