@@ -668,8 +668,8 @@ __device__ __forceinline__ void check_store_counts(const GramArgs& a, uint32_t* 
     sum = __builtin_amdgcn_sad_u8(v[i], 0u, sum);
     hib |= v[i] & 0x80808080u;
   }
-  if (I8 && hib && !(a.diag & 96)) atomicOr(a.flags, 2u);  // the i8 Gram reads counts as signed bytes: at most 127
-  if ((uint32_t)part < ns) {
+  if (I8 && hib && !(a.diag & 1632)) atomicOr(a.flags, 2u);  // the i8 Gram reads counts as signed bytes: at most 127
+  if ((uint32_t)part < ns && !(a.diag & 512)) {  // timing ablation (gram_diag 512): no image stores
     if constexpr (I8) {
       uint4* out = reinterpret_cast<uint4*>(const_cast<uint32_t*>(a.counts)) + ((size_t)tt * a.nb_rep + rb) * 1024 +
                    part * 256 + (r >> 4) * 64 + (r & 15);
@@ -699,7 +699,7 @@ __device__ __forceinline__ void check_store_counts(const GramArgs& a, uint32_t* 
 // Wave 0, after the barrier that follows a tile's check_store_counts: the tile's byte sums against
 // its level-1 counts, then the sums cleared for the tile after next.
 __device__ __forceinline__ void check_sums(const GramArgs& a, uint32_t* lsum, const uint32_t* mc, int lane) {
-  if (lsum[lane] != mc[lane] && !(a.diag & 96)) atomicOr(a.flags, 1u);
+  if (lsum[lane] != mc[lane] && !(a.diag & 1632)) atomicOr(a.flags, 1u);
   lsum[lane] = 0u;
 }
 
@@ -816,7 +816,8 @@ __global__ __launch_bounds__(kBlock) void ob_count_kernel(const GramArgs a) {
     if (wave == 0 && tt > tt0) check_sums(a, lsumb[(tt - 1) & 1], mcb[(tt - 1) & 1], lane);
     const uint32_t C = cum[64];
     const uint32_t cmin = cminb[tt & 1];
-    if (OB_CNT_MAP && full_tile(w, tile) && C - cmin * 64u <= kCallMapCap)
+    if (a.diag & 1024) {  // timing ablation (gram_diag 1024): no level-2 draws at all
+    } else if (OB_CNT_MAP && full_tile(w, tile) && C - cmin * 64u <= kCallMapCap)
       level2_map_draws(a, w, tile, img, mc, cmap, C, cmin, wave, lane);
     else
       level2_draws(a, w, tile, img, mc, cum, 0, 1, wave, 4, lane);
