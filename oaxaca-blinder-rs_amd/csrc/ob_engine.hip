@@ -84,6 +84,7 @@ struct GramArgs {
   int diag;  // OB_GRAM_DIAG bits: 2 no MFMAs, 4 no sub-tile DMA (tools/gram_ablate.py), 8 raw Heckman
              // statuses; count kernel timing ablations (wrong counts): 32 no LDS atomics, 64 no Philox
   int dbl;   // ob_gram_kernel: 1 = two staged sub-tile buffers (prefetch), 0 = one (k1 > kGramDblMaxK1)
+  uint32_t rb0;  // ob_count_kernel: the launch's first 64-replicate batch (a piece of the segment)
 };
 
 // ---------------------------------------------------------------------------------------------
@@ -790,7 +791,7 @@ __global__ __launch_bounds__(kBlock) void ob_count_kernel(const GramArgs a) {
   __shared__ uint32_t cmap[OB_CNT_MAP ? kCallMapCap : 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   Work w{};
-  w.rb = blockIdx.y;
+  w.rb = a.rb0 + blockIdx.y;
   w.rep0 = w.rb * 64;
   const uint32_t tt0 = blockIdx.x * kCntTilesPerBlock;
   const uint32_t tt1 = min(a.tiles_total, tt0 + kCntTilesPerBlock);
@@ -1942,6 +1943,12 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   // replicates/s), while a wide-tile block needs a whole CU's LDS, so resample blocks there delay
   // the Gram more than they hide (5,000 / 2,500 / 10k replicates: -9 / -11 / -4.5 %;
   // profiles/r06_ab_rs_double.txt)
+  const int rs_pieces = ob::opt_int(ob::Opt::RsPieces, 1);
+  if (overlap && rs_pieces > 1) {
+    if (!p->cnt_stream) HIP_OK(hipStreamCreateWithFlags(&p->cnt_stream, hipStreamNonBlocking));
+    for (hipEvent_t& e : p->cnt_ev)
+      if (!e) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
   const int rs_opt = ob::opt_int(ob::Opt::RsDouble, -1);
   const bool dbl = overlap && (rs_opt == 1 || (rs_opt < 0 && use_i8 && !ob::oz_wide(p, nch, pl.nb_rep)));
   if (dbl) {
@@ -1966,9 +1973,18 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     if (dbl) p->rs_parity ^= 1;
     if (overlap) HIP_OK(hipStreamWaitEvent(sr, sev, 0));
     if (timed) HIP_OK(hipEventRecord(ev[0], sr));
-    hipLaunchKernelGGL(l1k, dim3(ns, 2), dim3(kBlock), lds_l1, sr, p->n[0], p->n[1], p->ntiles[0], frep,
-                       tiles, key0, key1, m1, ky);
-    HIP_OK(hipGetLastError());
+    // pieces (option rs_pieces): level 1 over replicate batches [b0, b1) of piece k, then (below) the
+    // count kernel of each piece on cnt_stream once its level 1 is done, beside the next piece's
+    const int npc = overlap ? std::max(1, std::min({rs_pieces, 8, (int)plx.nb_rep})) : 1;
+    for (int k = 0; k < npc; ++k) {
+      const uint32_t r0 = std::min<uint32_t>(64u * (plx.nb_rep * k / npc), ns);
+      const uint32_t r1 = std::min<uint32_t>(64u * (plx.nb_rep * (k + 1) / npc), ns);
+      if (r1 > r0)
+        hipLaunchKernelGGL(l1k, dim3(r1 - r0, 2), dim3(kBlock), lds_l1, sr, p->n[0], p->n[1], p->ntiles[0],
+                           frep + r0, tiles, key0, key1, m1 + (size_t)r0 * tiles, ky);
+      HIP_OK(hipGetLastError());
+      if (npc > 1) HIP_OK(hipEventRecord(p->cnt_ev[k], sr));
+    }
     if (timed) HIP_OK(hipEventRecord(ev[1], sr));
     GramArgs ga = gram_args(p, plx);
     ga.chunks = p->d_chunks;
@@ -1981,13 +1997,21 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     ga.counts = counts;
     ga.tiles_total = tiles;
     ga.diag = diag_mode();
-    const dim3 cgrid((tiles + kCntTilesPerBlock - 1) / kCntTilesPerBlock, plx.nb_rep);
-    if (use_i8) hipLaunchKernelGGL(ob_count_kernel<true>, cgrid, dim3(kBlock), 0, sr, ga);
-    else hipLaunchKernelGGL(ob_count_kernel<false>, cgrid, dim3(kBlock), 0, sr, ga);
-    HIP_OK(hipGetLastError());
-    if (timed) HIP_OK(hipEventRecord(ev[2], sr));
+    const hipStream_t sc = npc > 1 ? p->cnt_stream : sr;
+    for (int k = 0; k < npc; ++k) {
+      const uint32_t b0 = plx.nb_rep * k / npc, b1 = plx.nb_rep * (k + 1) / npc;
+      if (npc > 1) HIP_OK(hipStreamWaitEvent(sc, p->cnt_ev[k], 0));
+      if (b1 == b0) continue;
+      ga.rb0 = b0;
+      const dim3 cgrid((tiles + kCntTilesPerBlock - 1) / kCntTilesPerBlock, b1 - b0);
+      if (use_i8) hipLaunchKernelGGL(ob_count_kernel<true>, cgrid, dim3(kBlock), 0, sc, ga);
+      else hipLaunchKernelGGL(ob_count_kernel<false>, cgrid, dim3(kBlock), 0, sc, ga);
+      HIP_OK(hipGetLastError());
+    }
+    ga.rb0 = 0;
+    if (timed) HIP_OK(hipEventRecord(ev[2], sc));
     if (overlap) {
-      HIP_OK(hipEventRecord(p->rs_ev, sr));
+      HIP_OK(hipEventRecord(p->rs_ev, sc));
       HIP_OK(hipStreamWaitEvent(s, p->rs_ev, 0));
     }
     if (timed) HIP_OK(hipEventRecord(ev[3], s));
@@ -2312,6 +2336,10 @@ void ob_panel_destroy(ob_panel* p) {
   if (p->rs_ev) (void)hipEventDestroy(p->rs_ev);
   if (p->scratch_ev) (void)hipEventDestroy(p->scratch_ev);
   if (p->scratch_ev2) (void)hipEventDestroy(p->scratch_ev2);
+  if (p->cnt_stream) (void)hipStreamSynchronize(p->cnt_stream);
+  for (hipEvent_t e : p->cnt_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (p->cnt_stream) (void)hipStreamDestroy(p->cnt_stream);
   if (p->rs_stream) (void)hipStreamDestroy(p->rs_stream);
   ob::shard_free(p);
   ob::oz_free(p);

@@ -151,6 +151,10 @@ struct ob_panel {
   size_t cap_m1b = 0, cap_countsb = 0;
   hipEvent_t scratch_ev2 = nullptr;
   int rs_parity = 0;
+  // Pieced resample (option rs_pieces): level 1 of replicate piece k + 1 on rs_stream beside the
+  // count kernel of piece k on cnt_stream (cnt_ev[k]: piece k's level 1 is done)
+  hipStream_t cnt_stream = nullptr;
+  hipEvent_t cnt_ev[8] = {};
 };
 
 namespace ob {

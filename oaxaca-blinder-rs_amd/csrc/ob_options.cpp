@@ -25,7 +25,7 @@ constexpr Entry kNames[] = {
     {"mm_kappa", ob::Opt::MmKappa},           {"mm_band0", ob::Opt::MmBand0},
     {"gram_diag", ob::Opt::GramDiag},         {"l1_diag", ob::Opt::L1Diag},
     {"gram_tile", ob::Opt::GramTile},         {"debug_count_overflow", ob::Opt::DebugCountOverflow},
-    {"rs_double", ob::Opt::RsDouble},
+    {"rs_double", ob::Opt::RsDouble},         {"rs_pieces", ob::Opt::RsPieces},
 };
 static_assert(sizeof(kNames) / sizeof(kNames[0]) == (size_t)ob::Opt::Count, "one name per option");
 

@@ -36,6 +36,8 @@ enum class Opt : int {
                        // error path that a real count above 255 would take, p < 1e-500 per row)
   RsDouble,     // 1: two count-image / m1 buffers, so a boot's resample runs under the previous Gram;
                 // 0: one; unset: the engine's rule (engine_boot)
+  RsPieces,     // level 1 and counts of a segment in this many replicate pieces, counts of piece k
+                // beside level 1 of piece k + 1 (1: one launch each); unset: the engine's rule
   Count
 };
 

@@ -507,3 +507,27 @@ def test_double_buffered_resample_bitwise(ob, O):
         assert np.array_equal(b0[0], want[0][0]) and np.array_equal(b1[0], want[1][0])
         r2, o2 = small.boot(SEED, 0, 16500, 0)
         assert np.array_equal(r2, long_rows) and np.array_equal(o2, long_ok)
+
+
+def test_pieced_resample_bitwise(ob, O):
+    """Option rs_pieces: level 1 and the count kernel of a segment in replicate pieces, each piece's
+    counts beside the next piece's level 1 (ob_engine.hip engine_boot). Same kernels on the same
+    (replicate, tile) units, so the rows equal the one-launch run bitwise, with and without the
+    double-buffered resample, across a two-segment call and a partial last batch."""
+    panel, _, _ = make(O, ob, 7000, 5, True)
+    small, _, _ = make(O, ob, 600, 2, False)
+    with ob._native.option("rs_pieces", 1), ob._native.option("rs_double", 0):
+        want = panel.boot(SEED, 11, 777, 3)
+        want_long = small.boot(SEED, 0, 16500, 0)
+        cnt = panel.debug_counts(SEED, 11, 128, 0)
+    for pieces in (2, 3, 5, 8):
+        for dbl in (0, 1):
+            with ob._native.option("rs_pieces", pieces), ob._native.option("rs_double", dbl):
+                got = panel.boot(SEED, 11, 777, 3)
+                assert np.array_equal(got[0], want[0]) and np.array_equal(got[1], want[1]), (pieces, dbl)
+                got2 = panel.boot(SEED, 11, 777, 3)  # back to back on the same buffers
+                assert np.array_equal(got2[0], want[0]), (pieces, dbl)
+    with ob._native.option("rs_pieces", 4):
+        r, o = small.boot(SEED, 0, 16500, 0)
+        assert np.array_equal(r, want_long[0]) and np.array_equal(o, want_long[1])
+        assert all(np.array_equal(x, y) for x, y in zip(panel.debug_counts(SEED, 11, 128, 0), cnt))
