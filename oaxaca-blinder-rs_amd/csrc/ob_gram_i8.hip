@@ -834,21 +834,19 @@ __global__ __launch_bounds__(kWaves * 64, 1) void oz_gram_kernel(const OzArgs a)
 }
 
 // ---------------------------------------------------------------------------------------------
-// Wide tile (round 6): one wave per SIMD, a block = 4 waves = (chunk, 256 replicates, 64 pairs).
-// Wave w owns replicate batch w and every digit slice of both 32-pair column tiles: per 64-row
-// sub-tile 4 replicate blocks x 6 slices x 4 pair blocks = 96 v_mfma_i32_16x16x64_i8 against one
-// 4 KB A load (its batch's count fragments, no longer loaded twice, once per slice group) and
-// 24 KB of B (both column tiles' six slices, LDS-DMA into a 4-stage ring, one barrier per sub-tile).
-// 384 accumulator registers (AGPRs) per wave: the block tile is twice the 8-wave kernel's, so each
-// A byte meets twice the MFMAs, and the four waves' A loads (16 KB per sub-tile, half of the
-// 8-wave kernel's 32 KB) plus B (24 KB per 64 pairs) are 40 KB per 384 MFMAs against 44 KB per
-// 192. The slice sums meet exactly as in oz_gram_body (slices 0-3 and 4-5 / 4-6 in int64, one
-// rounding each, then their sum): the partials are bitwise the 8-wave kernel's. A column-tile
-// pair whose tiles do not both run six slices takes its tiles one pass each (NH = 2).
+// Wide tile (round 6): one wave per SIMD, a block = 4 waves = (chunk, 256 replicates, 64 pairs),
+// per 64-row sub-tile 4 replicate batches x 6 slices x 4 pair blocks = 384 v_mfma_i32_16x16x64_i8
+// against 16 KB of A (the four batches' count fragments) and 24 KB of B (both column tiles' six
+// slices), all by LDS-DMA into a 4-stage ring, one barrier per sub-tile. The block tile is twice the
+// 8-wave kernel's, so each operand byte meets twice the MFMAs: 40 KB per 384 MFMAs against 44 KB per
+// 192. 384 accumulator registers per wave (256 in AGPRs). The waves split the tile as a 2 x 2 grid
+// (oz_gram_w2_body). The slice sums meet exactly as in oz_gram_body (slices 0-3 and 4-5 / 4-6 in
+// int64, one rounding each, then their sum): the partials are bitwise the 8-wave kernel's. A
+// column-tile pair whose tiles do not both run six slices takes its tiles one pass each (NH = 2).
+// (Round 6 first ran the tile as 1 x 4 -- wave w = replicate batch w x all 64 pairs -- with the
+// same ring and interleaved schedule: 4 A + 24 B fragment reads per 96 MFMAs against the grid's
+// 8 + 12, 5 % slower; removed after the grid)
 // ---------------------------------------------------------------------------------------------
-#ifndef OB_OZ_W_SPREAD
-#define OB_OZ_W_SPREAD 1
-#endif
 #ifndef OB_OZ_W_NBUF
 #define OB_OZ_W_NBUF 4
 #endif
@@ -891,230 +889,16 @@ __device__ __forceinline__ void oz_map_w(const OzArgs& a, uint32_t* dct, uint32_
 }
 
 // NS digit slices (6 or 7), NH 16-pair blocks per pass (4: column tiles ct0, ct0 + 1; 2: ct0 only),
-// NB this wave's DMA pieces per sub-tile, LIVE its replicate batch exists.
-template <int NS, int NH, int NB, bool LIVE, int DIAG>
-__device__ __forceinline__ void oz_gram_w_body(const OzArgs& a, unsigned char* smem, int wave, uint32_t ct0,
-                                               uint32_t rt, uint32_t chunk) {
-  constexpr int NC = NH / 2;                 // column tiles in this pass
-  constexpr int PIECES = NC * NS * 2;        // 1 KB B DMA pieces per sub-tile
-  constexpr int STAGE_B = PIECES * 64;       // 16-byte units of B per ring stage
-  // The four batches' A fragments come through the ring too (4 KB per wave, DMA'd by the wave for
-  // its own batch), so no load in the loop is compiler-tracked and every wait is counted here. A
-  // ring stage is 24 + 16 KB: 160 KB for four.
-  constexpr int STAGE = STAGE_B + 4 * 4 * 64;
-  constexpr int T = NB + (LIVE ? 4 : 0);     // this wave's DMA instructions per sub-tile
-  constexpr int PER = (kWNbuf - 2) * T;      // vector-memory ops newer than the stage to publish
-  const ob_v4i* bs = reinterpret_cast<const ob_v4i*>(smem);
-  const int lane = threadIdx.x & 63;
-  const uint32_t g = a.chunks[3 * chunk];
-  const uint32_t n = g ? a.n1 : a.n0, tg0 = g ? a.tiles0 : 0u;
-  const uint32_t s0 = a.chunks[3 * chunk + 1] * 4u;
-  const uint32_t s1 = min(a.chunks[3 * chunk + 2] * 4u, (n + 63u) >> 6);
-  const ob_v4i* Bg = g ? a.B1 : a.B0;
-  const uint32_t batch = rt * 4u + (uint32_t)wave;
-  // DMA instructions [LO, HI) of this wave's T for sub-tile s into ring stage buf: B pieces first
-  // (piece t * 4 + wave), then this wave's batch's A (4 x 1 KB [replicate block][lane])
-  auto dma = [&](int buf, uint32_t s, auto LO, auto HI) {
-    constexpr int lo = decltype(LO)::value, hi = decltype(HI)::value;
-#pragma unroll
-    for (int t = lo; t < hi; ++t) {
-      if (t < NB) {
-        const int piece = t * 4 + wave, c = piece / (NS * 2), q = piece - c * (NS * 2);
-        const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct0 + c) * kSubUnits + q * 64;
-        oz_dma16(src + lane, (uint32_t)(buf * STAGE + piece * 64) * 16u);
-      } else {
-        const int m = t - NB;
-        const ob_v4i* src_a = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256;
-        oz_dma16(src_a + m * 64 + lane, (uint32_t)(buf * STAGE + STAGE_B + (wave * 4 + m) * 64) * 16u);
-      }
-    }
-  };
-  // DMA instruction t of this wave for sub-tile s (mfmas_rd): scalar base, lane offset
-  auto dma1 = [&](int buf, uint32_t s, auto TT) {
-    constexpr int t = decltype(TT)::value;
-    if constexpr (t < NB) {
-      const int piece = t * 4 + wave, c = piece / (NS * 2), q = piece - c * (NS * 2);
-      const ob_v4i* src = Bg + ((size_t)s * a.n_ct + ct0 + c) * kSubUnits + q * 64;
-      oz_dma16s((uint32_t)lane * 16u, src, (uint32_t)(buf * STAGE + piece * 64) * 16u);
-    } else {
-      constexpr int m = t - NB;
-      const ob_v4i* src_a = a.counts + (((size_t)(tg0 + (s >> 2)) * a.nb_rep + batch) * 4 + (s & 3)) * 256 + m * 64;
-      oz_dma16s((uint32_t)lane * 16u, src_a, (uint32_t)(buf * STAGE + STAGE_B + (wave * 4 + m) * 64) * 16u);
-    }
-  };
-  auto aread = [&](int buf, ob_v4i (&dst)[4]) {
-#pragma unroll
-    for (int m = 0; m < 4; ++m) dst[m] = bs[buf * STAGE + STAGE_B + (wave * 4 + m) * 64 + lane];
-  };
-  ob_v4i ar[2][4];
-  // B fragments of pair block h: column tile h >> 1, half h & 1, every slice
-  auto read = [&](int buf, int h, ob_v4i (&bf)[NS]) {
-    const ob_v4i* bb = bs + buf * STAGE + ((h >> 1) * NS * 2 + (h & 1)) * 64 + lane;
-#pragma unroll
-    for (int q = 0; q < NS; ++q) bf[q] = bb[q * 128];
-  };
-  // 4 x NS x NH accumulator tiles: the first kWAgprTiles live in AGPRs (inline-asm MFMAs with an "a"
-  // constraint), the rest in VGPRs. Left to itself the compiler copies accumulators between the two
-  // files and spills (tools/probes/mfma_acc_probe.hip); pinned, 256 AGPRs + ~230 VGPRs hold the loop.
-  ob_v4i acc[4][NS][NH];
-#pragma unroll
-  for (int m = 0; m < 4; ++m)
-#pragma unroll
-    for (int q = 0; q < NS; ++q)
-#pragma unroll
-      for (int h = 0; h < NH; ++h) acc[m][q][h] = (ob_v4i){};
-  auto mfma1 = [&](int m, int q, int h, const ob_v4i (&af)[4], const ob_v4i (&bf)[NS]) {
-    if ((m * NS + q) * NH + h < kWAgprTiles)
-      asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+a"(acc[m][q][h]) : "v"(af[m]), "v"(bf[q]));
-    else
-      asm volatile("v_mfma_i32_16x16x64_i8 %0, %1, %2, %0" : "+v"(acc[m][q][h]) : "v"(af[m]), "v"(bf[q]));
-  };
-  auto mfmas = [&](int h, const ob_v4i (&af)[4], const ob_v4i (&bf)[NS]) {
-#pragma unroll
-    for (int q = 0; q < NS; ++q)
-#pragma unroll
-      for (int m = 0; m < 4; ++m) mfma1(m, q, h, af, bf);
-  };
-  // OB_OZ_W_SPREAD 1: pre-barrier pair block H = MFMAs (H, q) | B slice q of (rb, H + 1) into nb |
-  // DMA instruction H * NS + q, slice by slice, so the scalar address work, the DMA issue and the
-  // LDS reads sit in the shadow of the MFMAs around them; after the barrier the last block's MFMAs
-  // likewise carry the next sub-tile's first B block and its A.
-  auto mfmas_rd = [&](auto H, const ob_v4i (&af)[4], const ob_v4i (&bf)[NS], int rb, int rh, ob_v4i (&nb)[NS],
-                      int bn, uint32_t sn, bool with_dma, ob_v4i* an) {
-    constexpr int h = decltype(H)::value;
-    const ob_v4i* bb = bs + rb * STAGE + ((rh >> 1) * NS * 2 + (rh & 1)) * 64 + lane;
-    auto one = [&](auto Q) {
-      constexpr int q = decltype(Q)::value;
-#pragma unroll
-      for (int m = 0; m < 4; ++m) mfma1(m, q, h, af, bf);
-      if constexpr (!(DIAG & 128)) nb[q] = bb[q * 128];  // DIAG 128 (timing only): no B reads in the loop
-      if constexpr (q < 4 && !(DIAG & 256)) {               // DIAG 256 (timing only): no A reads
-        if (an) an[q] = bs[rb * STAGE + STAGE_B + (wave * 4 + q) * 64 + lane];
-      }
-      if constexpr (h * NS + q < T) {
-        if (with_dma) dma1(bn, sn, IC<h * NS + q>{});
-      }
-    };
-    one(IC<0>{}); one(IC<1>{}); one(IC<2>{}); one(IC<3>{}); one(IC<4>{}); one(IC<5>{});
-    if constexpr (NS > 6) one(IC<6>{});
-  };
-  // OB_OZ_W_SPREAD 1: step t DMAs sub-tile t + 3 into the stage freed at barrier t - 1, its T
-  // instructions one per slice group between the MFMAs before barrier t (mfmas_rd: one wave per
-  // SIMD, so a burst of DMA issue and address arithmetic right after the barrier left the MFMA pipe
-  // idle); 0: step t DMAs sub-tile t + 4 into stage t right after barrier t. Either way the stage
-  // published at barrier t was issued before barrier t - 2, and the loads newer than it at that
-  // barrier are the later stages' T each: PER = (N - 2) T for N ring stages. Every step issues the same DMAs (past the
-  // end: the last sub-tile again), so every wait is the same.
-  constexpr int AHEAD = OB_OZ_W_SPREAD ? kWNbuf - 1 : kWNbuf;
-#pragma unroll
-  for (int j = 0; j < AHEAD; ++j)
-    if (s0 + j < s1) dma(j, s0 + j, IC<0>{}, IC<T>{});
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  ob_v4i fb[2][NS];
-  if constexpr (LIVE) {
-    read(0, 0, fb[0]);
-    aread(0, ar[0]);
-  }
-  auto step = [&](uint32_t s, auto J) {
-    constexpr int j = decltype(J)::value;
-    const int buf = (int)((s - s0) % kWNbuf);
-    const uint32_t snext = min(s + AHEAD, s1 - 1);
-    const int bnext = (buf + AHEAD) % kWNbuf;
-    if constexpr (OB_OZ_W_SPREAD && LIVE && !(DIAG & 2) && !(DIAG & 4)) {
-      auto hb = [&](auto H) {
-        constexpr int h = decltype(H)::value;
-        __builtin_amdgcn_sched_barrier(0);
-        mfmas_rd(H, ar[j], fb[h & 1], buf, h + 1, fb[(h + 1) & 1], bnext, snext, true, nullptr);
-        if constexpr (h == NH - 2) dma(bnext, snext, IC<(NH - 1) * NS>{}, IC<T>{});  // what the slots did not hold
-        __builtin_amdgcn_sched_barrier(0);
-      };
-      hb(IC<0>{});
-      if constexpr (NH > 2) {
-        hb(IC<1>{});
-        hb(IC<2>{});
-      }
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
-      oz_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      mfmas_rd(IC<NH - 1>{}, ar[j], fb[(NH - 1) & 1], (buf + 1) % kWNbuf, 0, fb[NH & 1], bnext, snext, false,
-               ar[j ^ 1]);
-      __builtin_amdgcn_sched_barrier(0);
-      return;
-    }
-    // dead batches, timing ablations and OB_OZ_W_SPREAD 0: block-wise reads; the step's DMA in one
-    // burst (spread: before the barrier, into the stage freed at the previous one; 0: after it)
-    if constexpr (OB_OZ_W_SPREAD && !(DIAG & 4)) dma(bnext, snext, IC<0>{}, IC<T>{});
-#pragma unroll
-    for (int h = 0; h + 1 < NH; ++h) {
-      if constexpr (LIVE) read(buf, h + 1, fb[(h + 1) & 1]);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (LIVE && !(DIAG & 2)) mfmas(h, ar[j], fb[h & 1]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if constexpr (DIAG & 4) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
-    if constexpr (DIAG & 8) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // timing only: no barrier
-    else oz_barrier();
-    if constexpr (!OB_OZ_W_SPREAD && !(DIAG & 4)) dma(bnext, snext, IC<0>{}, IC<T>{});
-    if constexpr (LIVE) {
-      read((buf + 1) % kWNbuf, 0, fb[NH & 1]);
-      aread((buf + 1) % kWNbuf, ar[j ^ 1]);
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (!(DIAG & 2)) mfmas(NH - 1, ar[j], fb[(NH - 1) & 1]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  uint32_t s = s0;
-  for (; s + 2 <= s1; s += 2) {
-    step(s, IC<0>{});
-    step(s + 1, IC<1>{});
-  }
-  if (s < s1) step(s, IC<0>{});
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing DMAs (past the end) have landed
-  __syncthreads();  // every wave is done with the ring: the epilogue stages accumulators in it
-  if constexpr (LIVE) {
-    // slices -> f64 exactly as oz_gram_body: slices 0-3 and 4 .. NS - 1 each in int64, one ldexp
-    // each, then their sum (the 8-wave kernel's group-0 value plus its group-1 value). One pair
-    // block at a time through this wave's quarter of the ring (a lane reads back only its own
-    // words), so the int64 arithmetic never holds every accumulator in VGPRs at once.
-    ob_v4i* st = reinterpret_cast<ob_v4i*>(smem) + (size_t)wave * (4 * NS * 64);
-#pragma unroll
-    for (int h = 0; h < NH; ++h) {
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int q = 0; q < NS; ++q) st[(m * NS + q) * 64 + lane] = acc[m][q][h];
-      __builtin_amdgcn_sched_barrier(0);
-      const int pair = (int)(ct0 + (h >> 1)) * kPairsPerTile + 16 * (h & 1) + (lane & 15);
-      const int E = a.pexp[chunk * a.n_pairs_pad + min(pair, a.n_pairs_pad - 1)];
-      const int sh0 = E - kFracBits + 8 * (kS - 0 - kSlo), sh1 = E - kFracBits + 8 * (kS - kSlo - (NS - kSlo));
-#pragma unroll
-      for (int m = 0; m < 4; ++m)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          long long p0 = 0, p1 = 0;
-#pragma unroll
-          for (int q = 0; q < kSlo; ++q) p0 = p0 * 256 + st[(m * NS + q) * 64 + lane][i];
-#pragma unroll
-          for (int q = kSlo; q < NS; ++q) p1 = p1 * 256 + st[(m * NS + q) * 64 + lane][i];
-          const double val = ldexp((double)p0, sh0) + ldexp((double)p1, sh1);
-          const uint32_t rep = batch * 64u + (uint32_t)(16 * m + 4 * (lane >> 4) + i);
-          if (pair < a.e_pad && rep < a.n_reps) a.partial[((size_t)chunk * a.rep_pad + rep) * a.e_pad + pair] = val;
-        }
-    }
-  }
-  __syncthreads();  // the staging is done before a next pass refills the ring
-}
-
-// OB_OZ_W_GRID 1: the same block tile and ring, the waves as a 2 x 2 grid. Wave w = (wr = w & 1,
+// NB this wave's B DMA pieces per sub-tile. The waves as a 2 x 2 grid: wave w = (wr = w & 1,
 // wc = w >> 1) owns replicate batches 2 wr, 2 wr + 1 (8 replicate blocks) and pair blocks
 // wc NHW .. wc NHW + NHW - 1 (NHW = NH / 2: column tile ct0 + wc when NH = 4, one half of ct0 when
-// NH = 2): per sub-tile 8 A and NHW NS B fragment reads for the same 8 x NS x NHW MFMAs, against 4 A
-// and NH NS B in the 1 x 4 layout above (20 reads per 96 MFMAs instead of 28: the B reads are what
-// the gram_diag 128 ablation found costly). The DMA is unchanged (wave w loads B pieces t * 4 + w and
-// its own batch w's A, DLIVE: batch w exists), so every wait is the 1 x 4 body's. A step is 2 NHW
+// NH = 2): per sub-tile 8 A and NHW NS B fragment reads for its 8 x NS x NHW MFMAs (20 reads per 96
+// MFMAs; a 1 x 4 split needs 28, and the B reads are what the gram_diag 128 ablation found costly).
+// Wave w DMAs B pieces t * 4 + w and its own batch w's A (DLIVE: batch w exists); the step DMAs
+// sub-tile t + 3 into the stage freed at barrier t - 1, one or two instructions after each slice's
+// MFMAs before the barrier (address arithmetic on the scalar unit, in the MFMAs' shadow), and the
+// stage published at barrier t was issued before barrier t - 2, so the wait is vmcnt((N - 2) T) for
+// N stages, the same at every step (past the end the last sub-tile is fetched again). A step is 2 NHW
 // units (pair block h, replicate half mh) of 4 NS MFMAs, h-major; the last unit (the last two when
 // NHW = 2) runs after the barrier and reads the next sub-tile's first B block and A. MLIVE: batch
 // 2 wr exists (the wave computes; a dead second batch computes on stale LDS and is never stored).
@@ -1281,7 +1065,9 @@ __device__ __forceinline__ void oz_gram_w2_body(const OzArgs& a, unsigned char* 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if constexpr (MLIVE) {
-    // as oz_gram_w_body's epilogue, four replicate blocks at a time through this wave's quarter of the ring
+    // slices -> f64 exactly as oz_gram_body: slices 0-3 and 4 .. NS - 1 each in int64, one ldexp each, then
+    // their sum; four replicate blocks at a time through this wave's quarter of the ring (a lane reads
+    // back only its own words), so the int64 arithmetic never holds every accumulator in VGPRs at once
     ob_v4i* st = reinterpret_cast<ob_v4i*>(smem) + (size_t)wave * (4 * NS * 64);
 #pragma unroll
     for (int h = 0; h < NHW; ++h) {
@@ -1317,18 +1103,6 @@ __device__ __forceinline__ void oz_gram_w2_body(const OzArgs& a, unsigned char* 
   __syncthreads();
 }
 
-#ifndef OB_OZ_W_GRID
-#define OB_OZ_W_GRID 1  // 1: oz_gram_w2_body (2 x 2 wave grid); 0: oz_gram_w_body (1 x 4)
-#endif
-
-template <int NS, int NH, bool LIVE, int DIAG>
-__device__ __forceinline__ void oz_gram_w_pass(const OzArgs& a, unsigned char* smem, int wave, uint32_t ct0,
-                                               uint32_t rt, uint32_t chunk) {
-  constexpr int P = (NH / 2) * NS * 2;  // pieces per sub-tile, dealt round-robin over the 4 waves
-  if (wave < P % 4 || P % 4 == 0) oz_gram_w_body<NS, NH, (P + 3) / 4, LIVE, DIAG>(a, smem, wave, ct0, rt, chunk);
-  else oz_gram_w_body<NS, NH, P / 4, LIVE, DIAG>(a, smem, wave, ct0, rt, chunk);
-}
-
 template <int NS, int NH, bool DLIVE, bool MLIVE, int DIAG>
 __device__ __forceinline__ void oz_gram_w2_pass(const OzArgs& a, unsigned char* smem, int wave, uint32_t ct0,
                                                 uint32_t rt, uint32_t chunk) {
@@ -1340,16 +1114,11 @@ __device__ __forceinline__ void oz_gram_w2_pass(const OzArgs& a, unsigned char* 
 template <int NS, int NH, int DIAG>
 __device__ __forceinline__ void oz_gram_w_pass_live(const OzArgs& a, unsigned char* smem, int wave, uint32_t ct0,
                                                     uint32_t rt, uint32_t chunk, bool live) {
-  if constexpr (OB_OZ_W_GRID) {
-    const bool mlive = rt * 4u + 2u * (uint32_t)(wave & 1) < a.nb_rep;
-    if (live && mlive) oz_gram_w2_pass<NS, NH, true, true, DIAG>(a, smem, wave, ct0, rt, chunk);
-    else if (live) oz_gram_w2_pass<NS, NH, true, false, DIAG>(a, smem, wave, ct0, rt, chunk);
-    else if (mlive) oz_gram_w2_pass<NS, NH, false, true, DIAG>(a, smem, wave, ct0, rt, chunk);
-    else oz_gram_w2_pass<NS, NH, false, false, DIAG>(a, smem, wave, ct0, rt, chunk);
-  } else {
-    if (live) oz_gram_w_pass<NS, NH, true, DIAG>(a, smem, wave, ct0, rt, chunk);
-    else oz_gram_w_pass<NS, NH, false, DIAG>(a, smem, wave, ct0, rt, chunk);
-  }
+  const bool mlive = rt * 4u + 2u * (uint32_t)(wave & 1) < a.nb_rep;
+  if (live && mlive) oz_gram_w2_pass<NS, NH, true, true, DIAG>(a, smem, wave, ct0, rt, chunk);
+  else if (live) oz_gram_w2_pass<NS, NH, true, false, DIAG>(a, smem, wave, ct0, rt, chunk);
+  else if (mlive) oz_gram_w2_pass<NS, NH, false, true, DIAG>(a, smem, wave, ct0, rt, chunk);
+  else oz_gram_w2_pass<NS, NH, false, false, DIAG>(a, smem, wave, ct0, rt, chunk);
 }
 
 template <int DIAG>
