@@ -1865,7 +1865,9 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
   OB_TRY(ensure_buf(&p->d_counts, p->cap_counts, (size_t)tiles * pl.nb_rep * 4 * kCimgWords));
   OB_TRY(ensure_buf(&p->d_partial, p->cap_partial, need_partial * p->e_pad));
   OB_TRY(ensure_buf(&p->d_gram, p->cap_gram, (size_t)2 * pl.rep_pad * p->e_pad));
+  bool s_work = false;  // this call put work on s that its Gram reads (tail_stream: g_stream waits for it)
   if (!p->chunks_ready) {  // the chunk table depends on the panel only: uploaded once, never rewritten
+    s_work = true;
     p->chunks = pl.chunks;
     OB_TRY(ensure_buf(&p->d_chunks, p->cap_chunks, p->chunks.size()));
     HIP_OK(hipMemcpyAsync(p->d_chunks, p->chunks.data(), sizeof(uint32_t) * p->chunks.size(), hipMemcpyHostToDevice, s));
@@ -1886,6 +1888,7 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     p->pending_gathers = 0;
   }
   if (use_i8) {
+    if (p->oz_state == 0) s_work = true;
     OB_TRY(ob::oz_prepare(p, s));
     use_i8 = p->oz_state == 1;
     if (!use_i8 && force == 2) return ob::fail(OB_E_UNSUPPORTED, "the i8 Gram's digit images do not fit in HBM");
@@ -1959,6 +1962,26 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
       HIP_OK(hipEventRecord(p->scratch_ev2, s));
     }
   }
+  const bool tov = overlap && ob::opt_int(ob::Opt::TailStream, 0) == 1;
+  if (tov) {
+    if (!p->g_stream) HIP_OK(hipStreamCreateWithFlags(&p->g_stream, hipStreamNonBlocking));
+    if (!p->t_stream) HIP_OK(hipStreamCreateWithFlags(&p->t_stream, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&p->g_ev, &p->t_ev, &p->user_ev, &p->prep_ev})
+      if (!*e) HIP_OK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    for (hipEvent_t& e : p->red_ev)
+      if (!e) {
+        HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIP_OK(hipEventRecord(e, s));
+      }
+    OB_TRY(ensure_buf(&p->d_partialb, p->cap_partialb, need_partial * p->e_pad));
+    HIP_OK(hipEventRecord(p->user_ev, s));
+    if (s_work) {
+      HIP_OK(hipEventRecord(p->prep_ev, s));
+      HIP_OK(hipStreamWaitEvent(p->g_stream, p->prep_ev, 0));
+    }
+  }
+  const hipStream_t sg = tov ? p->g_stream : s;  // the Gram
+  const hipStream_t st = tov ? p->t_stream : s;  // reduce, exceptions, solve
   for (uint64_t s0 = 0; s0 < n_reps; s0 += seg) {
     const uint32_t ns = (uint32_t)std::min<uint64_t>(seg, n_reps - s0);
     const Plan& plx = (ns == seg) ? pl : pl_tail;
@@ -1971,6 +1994,9 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     uint32_t* const counts = buf ? p->d_countsb : p->d_counts;
     const hipEvent_t sev = buf ? p->scratch_ev2 : p->scratch_ev;  // the last read of this buffer
     if (dbl) p->rs_parity ^= 1;
+    const int pb = tov ? p->part_parity : 0;
+    if (tov) p->part_parity ^= 1;
+    double* const partial = pb ? p->d_partialb : p->d_partial;
     if (overlap) HIP_OK(hipStreamWaitEvent(sr, sev, 0));
     if (timed) HIP_OK(hipEventRecord(ev[0], sr));
     // pieces (option rs_pieces): level 1 over replicate batches [b0, b1) of piece k, then (below) the
@@ -1993,7 +2019,7 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     ga.first_rep = frep;
     ga.key0 = key0;
     ga.key1 = key1;
-    ga.partial = p->d_partial;
+    ga.partial = partial;
     ga.counts = counts;
     ga.tiles_total = tiles;
     ga.diag = diag_mode();
@@ -2012,28 +2038,35 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
     if (timed) HIP_OK(hipEventRecord(ev[2], sc));
     if (overlap) {
       HIP_OK(hipEventRecord(p->rs_ev, sc));
-      HIP_OK(hipStreamWaitEvent(s, p->rs_ev, 0));
+      HIP_OK(hipStreamWaitEvent(sg, p->rs_ev, 0));
     }
-    if (timed) HIP_OK(hipEventRecord(ev[3], s));
+    if (tov) HIP_OK(hipStreamWaitEvent(sg, p->red_ev[pb], 0));  // the reduce two segments back read it
+    if (timed) HIP_OK(hipEventRecord(ev[3], sg));
     if (use_i8) {
-      OB_TRY(ob::oz_gram(p, p->d_chunks, nchx, counts, plx.nb_rep, plx.rep_pad, ns, p->d_partial, s));
+      OB_TRY(ob::oz_gram(p, p->d_chunks, nchx, counts, plx.nb_rep, plx.rep_pad, ns, partial, sg));
     } else {
       const uint32_t blocks = plx.nb_rep * plx.n_cg * (uint32_t)nchx;
-      HIP_OK(launch_gram(p, plx.cb, false, ga, blocks, s));
+      HIP_OK(launch_gram(p, plx.cb, false, ga, blocks, sg));
     }
-    if (timed) HIP_OK(hipEventRecord(ev[4], s));
+    if (timed) HIP_OK(hipEventRecord(ev[4], sg));
     const bool exc = use_i8 && ob::oz_exceptions_pending(p);
-    if (overlap && !exc) HIP_OK(hipEventRecord(sev, s));  // the count images are free again
+    if (overlap && !exc) HIP_OK(hipEventRecord(sev, sg));  // the count images are free again
+    if (tov) {
+      HIP_OK(hipEventRecord(p->g_ev, sg));
+      HIP_OK(hipStreamWaitEvent(st, p->g_ev, 0));
+      HIP_OK(hipStreamWaitEvent(st, p->user_ev, 0));  // the caller's use of the rows buffers so far
+    }
     const size_t nred = (size_t)ns * p->e_pad;
-    hipLaunchKernelGGL(ob_reduce_kernel, dim3((unsigned)((nred + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                       (const double*)p->d_partial, (const uint32_t*)p->d_chunks, nchx, plx.rep_pad, p->e_pad, ns,
+    hipLaunchKernelGGL(ob_reduce_kernel, dim3((unsigned)((nred + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+                       (const double*)partial, (const uint32_t*)p->d_chunks, nchx, plx.rep_pad, p->e_pad, ns,
                        p->d_gram);
     HIP_OK(hipGetLastError());
+    if (tov) HIP_OK(hipEventRecord(p->red_ev[pb], st));
     if (exc) {
-      OB_TRY(ob::oz_exceptions(p, counts, plx.nb_rep, ns, p->d_gram, s));
-      if (overlap) HIP_OK(hipEventRecord(sev, s));
+      OB_TRY(ob::oz_exceptions(p, counts, plx.nb_rep, ns, p->d_gram, st));
+      if (overlap) HIP_OK(hipEventRecord(sev, st));
     }
-    if (timed) HIP_OK(hipEventRecord(ev[5], s));
+    if (timed) HIP_OK(hipEventRecord(ev[5], st));
     if (p->heckman) {  // probit iterations + IMR sums + two-step solve (synchronizes the stream)
       ob_heck_seg hs = heck_seg(p, plx, p->d_chunks, p->d_gram, ref_mode);
       hs.counts = counts;
@@ -2060,11 +2093,15 @@ int engine_boot(ob_panel* p, uint64_t seed, uint64_t first_rep, uint64_t n_reps,
       sa.gram_out = nullptr;
       sa.raw_beta_b = nullptr;
       sa.raw_status = 0;
-      HIP_OK(launch_solve(p, sa, ns, s));
+      HIP_OK(launch_solve(p, sa, ns, st));
     }
-    if (timed) HIP_OK(hipEventRecord(ev[6], s));
+    if (timed) HIP_OK(hipEventRecord(ev[6], st));
     p->timing.gram_launches += 1;
     p->pending_segments += 1;
+  }
+  if (tov) {  // the caller's stream sees the rows complete, as without the tail stream
+    HIP_OK(hipEventRecord(p->t_ev, st));
+    HIP_OK(hipStreamWaitEvent(s, p->t_ev, 0));
   }
   p->timing_pending = true;
   p->last_stream = s;
@@ -2336,6 +2373,13 @@ void ob_panel_destroy(ob_panel* p) {
   if (p->rs_ev) (void)hipEventDestroy(p->rs_ev);
   if (p->scratch_ev) (void)hipEventDestroy(p->scratch_ev);
   if (p->scratch_ev2) (void)hipEventDestroy(p->scratch_ev2);
+  for (hipStream_t x : {p->g_stream, p->t_stream})
+    if (x) (void)hipStreamSynchronize(x);
+  for (hipEvent_t e : {p->g_ev, p->t_ev, p->user_ev, p->prep_ev, p->red_ev[0], p->red_ev[1]})
+    if (e) (void)hipEventDestroy(e);
+  for (hipStream_t x : {p->g_stream, p->t_stream})
+    if (x) (void)hipStreamDestroy(x);
+  (void)hipFree(p->d_partialb);
   if (p->cnt_stream) (void)hipStreamSynchronize(p->cnt_stream);
   for (hipEvent_t e : p->cnt_ev)
     if (e) (void)hipEventDestroy(e);

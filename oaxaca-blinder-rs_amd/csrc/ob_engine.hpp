@@ -155,6 +155,16 @@ struct ob_panel {
   // count kernel of piece k on cnt_stream (cnt_ev[k]: piece k's level 1 is done)
   hipStream_t cnt_stream = nullptr;
   hipEvent_t cnt_ev[8] = {};
+  // Tail stream (option tail_stream): the Gram on g_stream, the reduce / exceptions / solve on
+  // t_stream, the caller's stream waiting only for t_ev at the end of the call, so segment k + 1's
+  // Gram (partial buffer part_parity) runs under segment k's tail. red_ev[b]: the last reduce that
+  // read partial buffer b; user_ev: the caller's stream at the call (the rows buffers); prep_ev: work
+  // this call put on the caller's stream before its first Gram (chunk table, digit images).
+  hipStream_t g_stream = nullptr, t_stream = nullptr;
+  hipEvent_t g_ev = nullptr, t_ev = nullptr, user_ev = nullptr, prep_ev = nullptr, red_ev[2] = {};
+  double* d_partialb = nullptr;
+  size_t cap_partialb = 0;
+  int part_parity = 0;
 };
 
 namespace ob {

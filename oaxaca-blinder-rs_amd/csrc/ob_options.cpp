@@ -26,6 +26,7 @@ constexpr Entry kNames[] = {
     {"gram_diag", ob::Opt::GramDiag},         {"l1_diag", ob::Opt::L1Diag},
     {"gram_tile", ob::Opt::GramTile},         {"debug_count_overflow", ob::Opt::DebugCountOverflow},
     {"rs_double", ob::Opt::RsDouble},         {"rs_pieces", ob::Opt::RsPieces},
+    {"tail_stream", ob::Opt::TailStream},
 };
 static_assert(sizeof(kNames) / sizeof(kNames[0]) == (size_t)ob::Opt::Count, "one name per option");
 

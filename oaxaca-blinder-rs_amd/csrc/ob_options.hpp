@@ -38,6 +38,8 @@ enum class Opt : int {
                 // 0: one; unset: the engine's rule (engine_boot)
   RsPieces,     // level 1 and counts of a segment in this many replicate pieces, counts of piece k
                 // beside level 1 of piece k + 1 (1: one launch each); unset: the engine's rule
+  TailStream,   // 1: a boot's reduce / solve on a stream of their own, so the next segment's Gram
+                // need not wait for them (two partial buffers); 0: on the caller's stream; unset: rule
   Count
 };
 

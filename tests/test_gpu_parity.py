@@ -531,3 +531,41 @@ def test_pieced_resample_bitwise(ob, O):
         r, o = small.boot(SEED, 0, 16500, 0)
         assert np.array_equal(r, want_long[0]) and np.array_equal(o, want_long[1])
         assert all(np.array_equal(x, y) for x, y in zip(panel.debug_counts(SEED, 11, 128, 0), cnt))
+
+
+def test_tail_stream_bitwise_and_ordered(ob, O):
+    """Option tail_stream: the Gram on an engine stream, reduce / exceptions / solve on another, the
+    caller's stream waiting for them at the end of the call, so the next segment's Gram runs under
+    this one's tail (two partial buffers). Rows bitwise as on one stream; a copy the caller enqueues
+    between two calls that reuse one rows buffer still sees the first call's rows (the tail waits
+    for the caller's stream); calls alternate between two torch streams; with and without rs_double."""
+    import torch
+
+    panel, _, _ = make(O, ob, 6000, 5, True)
+    small, _, _ = make(O, ob, 600, 2, False)
+    with ob._native.option("tail_stream", 0), ob._native.option("rs_double", 0):
+        want = [panel.boot(SEED, r0, 256, 2) for r0 in (0, 256, 512)]
+        want_long = small.boot(SEED, 0, 16500, 0)
+    dev = torch.device("cuda", 0)
+    for dbl in (0, 1):
+        with ob._native.option("tail_stream", 1), ob._native.option("rs_double", dbl):
+            got = [panel.boot(SEED, r0, 256, 2) for r0 in (0, 256, 512)]
+            for (a, oa), (b, obb) in zip(want, got):
+                assert np.array_equal(a, b) and np.array_equal(oa, obb), dbl
+            rows = torch.empty((256, panel.row_len), dtype=torch.float64, device=dev)
+            ok = torch.empty(256, dtype=torch.uint8, device=dev)
+            copies = []
+            streams = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
+            for i, r0 in enumerate((0, 256, 512)):
+                st = streams[i % 2]
+                if i:
+                    st.wait_stream(streams[(i - 1) % 2])  # the caller orders its own streams
+                with torch.cuda.stream(st):
+                    panel.boot_device(SEED, r0, 256, rows.data_ptr(), ok.data_ptr(), 2, stream=st.cuda_stream)
+                    copies.append((rows.clone(), ok.clone()))  # enqueued on st after the call
+            panel.sync()
+            torch.cuda.synchronize()
+            for (c, co), (w, wo) in zip(copies, want):
+                assert np.array_equal(c.cpu().numpy(), w) and np.array_equal(co.cpu().numpy(), wo), dbl
+            r, o = small.boot(SEED, 0, 16500, 0)
+            assert np.array_equal(r, want_long[0]) and np.array_equal(o, want_long[1]), dbl
