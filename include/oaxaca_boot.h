@@ -271,6 +271,10 @@ int ob_debug_mm_betas(ob_panel* panel, uint64_t seed, int32_t simulations, uint6
      "rs_double"   1: two level-1 / count-image buffers per panel, so each boot segment's resample
                    runs under the previous segment's Gram (rows bitwise unchanged; twice the image HBM),
                    0: one buffer (default: the engine's rule)
+     "rs_pieces"   n > 1: level 1 and counts of a segment in n replicate pieces, each piece's counts beside
+                   the next piece's level 1 (default 1; rows bitwise unchanged)
+     "tail_stream" 1: the Gram and the reduce / solve on engine streams, the caller's stream waiting for
+                   them at the end of the call (default 0; rows bitwise unchanged)
    Unknown names are OB_E_INVALID. ob_get_option reads back what ob_set_option stored (NaN: unset). ob_tuning_build() is 1 in a -DOB_TUNING=1 build (`make tuning`),
    which also reads OB_<NAME> from the environment for options nobody set. */
 int ob_set_option(const char* name, double value);
