@@ -176,7 +176,8 @@ typedef struct {
                                 slices (pairs of narrow magnitude range) */
   int32_t oz_tiles;          /* i8 Gram: all (chunk, column tile) blocks */
   int32_t oz_wide;           /* i8 Gram, last launch: 1 = the wide-tile kernel (4 waves, 256 replicates x 64
-                                pairs per block), 0 = the 8-wave kernel (32 pairs); option gram_tile */
+                                pairs per block), 2 = the wide tile with each chunk split over two blocks,
+                                0 = the 8-wave kernel (32 pairs); option gram_tile */
 } ob_timing;
 int ob_panel_last_timing(const ob_panel* panel, ob_timing* out);
 /* Synchronize the stream used by the last *_device call and collect its timings. */
@@ -264,7 +265,7 @@ int ob_debug_mm_betas(ob_panel* panel, uint64_t seed, int32_t simulations, uint6
      "mm_state_gb", "mm_delta1", "mm_delta2", "mm_tol1", "mm_fit_stride", "mm_kappa", "mm_band0":
                    Machado-Mata tuning (the verification keeps results exact)
      "gram_diag", "l1_diag": timing ablations, tuning builds only (OB_E_UNSUPPORTED otherwise)
-     "gram_tile"   1: the 8-wave i8 Gram kernel, 2: the wide-tile one (default: whichever the launch's
+     "gram_tile"   1: the 8-wave i8 Gram kernel, 2: the wide-tile one, 3: the wide tile split (default: whichever the launch's
                    block count favours; their Grams are bitwise equal)
      "debug_count_overflow" nonzero: the resample's count-overflow word is raised after every
                    count kernel of a Machado-Mata run or ob_debug_counts (tests the OB_E_OVERFLOW path)

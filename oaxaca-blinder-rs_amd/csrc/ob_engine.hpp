@@ -103,6 +103,8 @@ struct ob_panel {
   int32_t* d_oz_pexp = nullptr;
   int64_t* d_oz_psum = nullptr;  // [chunk][pair][2]: exponent sum and count of the nonzero |P| (digit choice)
   uint8_t* d_oz_nsl = nullptr;   // [chunk][column tile]: digit slices the Gram runs (6 or 7)
+  long long* d_oz_pint = nullptr;  // split wide launches: the halves' int64 slice-group sums
+  size_t cap_oz_pint = 0;
   uint8_t* d_oz_pnsl = nullptr;  // [chunk][pair]: 6 = the pair's seventh digit is written as zero
   int oz_tiles6 = 0, oz_tiles = 0;  // (chunk, column tile) blocks on 6 slices / all (read with the meta)
   // exception rows (ob_gram_i8.hip): rows whose magnitude dwarfs their chunk's

@@ -475,6 +475,9 @@ struct OzArgs {
   uint32_t n0, n1, tiles0, nb_rep, n_reps, rep_pad, n_rt;
   int n_ct, e_pad, n_pairs_pad;
   int n_dct;  // oz_gram_w_kernel: column-tile pairs (64 pairs)
+  int ksplit;  // oz_gram_w_kernel: 2 = each (chunk, tiles) block pair splits the chunk's sub-tiles
+  long long* pint;  // ksplit 2: [half][chunk][rep_pad][e_pad][2] int64 slice-group sums
+  int n_chunks;
 };
 
 constexpr int kWaves = 8;                         // 2 per SIMD: (replicate batch, slice group)
@@ -855,6 +858,9 @@ constexpr int kWAgprTiles = 64;  // accumulator tiles (4 registers each) pinned 
 // 4 stages of B (two six-slice tiles: 24 KB; one seven-slice tile: 14 KB) + A (16 KB)
 constexpr size_t kWLds = kWNbuf * (size_t)(2 * 6 * 2 * 64 + 4 * 4 * 64) * 16;
 
+#ifndef OB_OZ_W_SPLIT
+#define OB_OZ_W_SPLIT 1  // the engine may split a wide launch's chunks over two blocks (oz_gram_mode)
+#endif
 #ifndef OB_OZ_W_RASTER
 #define OB_OZ_W_RASTER 0
 #endif
@@ -864,7 +870,8 @@ constexpr size_t kWLds = kWNbuf * (size_t)(2 * 6 * 2 * 64 + 4 * 4 * 64) * 16;
 // one chunk at once and read each B sub-tile of the chunk from L2 that many times per fetch;
 // 1: oz_map's chunk-major deal of groups over the XCDs (every XCD streams the chunk's B).
 __device__ __forceinline__ void oz_map_w(const OzArgs& a, uint32_t* dct, uint32_t* rt, uint32_t* chunk) {
-  const uint32_t nwg = gridDim.x, bid = blockIdx.x, nct = (uint32_t)a.n_dct;
+  // ksplit 2: blocks 2i and 2i + 1 are the two halves of work item i (different XCDs)
+  const uint32_t nwg = gridDim.x / (uint32_t)a.ksplit, bid = blockIdx.x / (uint32_t)a.ksplit, nct = (uint32_t)a.n_dct;
   uint32_t grp, c;
 #if OB_OZ_W_RASTER
   const uint32_t sgb = 8u * nct, sg = bid / sgb, r = bid - sg * sgb;
@@ -921,8 +928,12 @@ __device__ __forceinline__ void oz_gram_w2_body(const OzArgs& a, unsigned char* 
   const int wr = wave & 1, wc = wave >> 1;
   const uint32_t g = a.chunks[3 * chunk];
   const uint32_t n = g ? a.n1 : a.n0, tg0 = g ? a.tiles0 : 0u;
-  const uint32_t s0 = a.chunks[3 * chunk + 1] * 4u;
-  const uint32_t s1 = min(a.chunks[3 * chunk + 2] * 4u, (n + 63u) >> 6);
+  const uint32_t c0 = a.chunks[3 * chunk + 1] * 4u;
+  const uint32_t c1 = min(a.chunks[3 * chunk + 2] * 4u, (n + 63u) >> 6);
+  // ksplit 2: this block takes half `half` of the chunk's sub-tiles (integer slice sums add exactly)
+  const uint32_t half = blockIdx.x % (uint32_t)a.ksplit, cmid = c0 + (c1 - c0) / 2u;
+  const uint32_t s0 = a.ksplit == 1 ? c0 : (half ? cmid : c0);
+  const uint32_t s1 = a.ksplit == 1 ? c1 : (half ? c1 : cmid);
   const ob_v4i* Bg = g ? a.B1 : a.B0;
   const uint32_t dbatch = rt * 4u + (uint32_t)wave;  // the batch whose A this wave DMAs
   auto dma = [&](int buf, uint32_t s, auto LO, auto HI) {
@@ -980,7 +991,7 @@ __device__ __forceinline__ void oz_gram_w2_body(const OzArgs& a, unsigned char* 
     if (s0 + j < s1) dma(j, s0 + j, IC<0>{}, IC<T>{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if constexpr (MLIVE) {
+  if (MLIVE && s0 < s1) {
 #pragma unroll
     for (int q = 0; q < NS; ++q) fb[0][q] = bread1(0, 0, q);
 #pragma unroll
@@ -1093,9 +1104,16 @@ __device__ __forceinline__ void oz_gram_w2_body(const OzArgs& a, unsigned char* 
             for (int q = 0; q < kSlo; ++q) p0 = p0 * 256 + st[(m * NS + q) * 64 + lane][i];
 #pragma unroll
             for (int q = kSlo; q < NS; ++q) p1 = p1 * 256 + st[(m * NS + q) * 64 + lane][i];
-            const double val = ldexp((double)p0, sh0) + ldexp((double)p1, sh1);
             const uint32_t rep = batch * 64u + (uint32_t)(16 * m + 4 * (lane >> 4) + i);
-            if (pair < a.e_pad && rep < a.n_reps) a.partial[((size_t)chunk * a.rep_pad + rep) * a.e_pad + pair] = val;
+            if (pair < a.e_pad && rep < a.n_reps) {
+              if (a.ksplit == 1) {
+                a.partial[((size_t)chunk * a.rep_pad + rep) * a.e_pad + pair] = ldexp((double)p0, sh0) + ldexp((double)p1, sh1);
+              } else {  // the two halves meet in oz_split_combine_kernel, in int64, before the roundings
+                long long* d = a.pint + ((((size_t)half * a.n_chunks + chunk) * a.rep_pad + rep) * a.e_pad + pair) * 2;
+                d[0] = p0;
+                d[1] = p1;
+              }
+            }
           }
       }
     }
@@ -1328,6 +1346,7 @@ void oz_free(ob_panel* p) {
   (void)hipFree(p->d_oz_psum);
   (void)hipFree(p->d_oz_nsl);
   (void)hipFree(p->d_oz_pnsl);
+  (void)hipFree(p->d_oz_pint);
   (void)hipFree(p->d_oz_acc);
   (void)hipFree(p->d_oz_meta);
   (void)hipFree(p->d_oz_exc);
@@ -1338,15 +1357,41 @@ void oz_free(ob_panel* p) {
 
 // One segment's Gram partials: d_chunks holds the panel's chunk table, counts the I8 images of
 // the segment's nb_rep replicate batches.
-bool oz_wide(const ob_panel* p, int n_chunks, uint32_t nb_rep) {
+// ksplit 2: each chunk partial from its two halves' int64 slice-group sums, exactly as one block
+// would have rounded them (oz_gram_w2_body's epilogue): bitwise the unsplit partial.
+__global__ __launch_bounds__(256) void oz_split_combine_kernel(const OzArgs a) {
+  const size_t per = (size_t)a.rep_pad * a.e_pad;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)a.n_chunks * per) return;
+  const uint32_t chunk = (uint32_t)(i / per);
+  const uint32_t rem = (uint32_t)(i - (size_t)chunk * per), rep = rem / (uint32_t)a.e_pad, pair = rem % (uint32_t)a.e_pad;
+  if (rep >= a.n_reps) return;
+  const long long* h0 = a.pint + i * 2;
+  const long long* h1 = a.pint + ((size_t)a.n_chunks * per + i) * 2;
+  const long long p0 = h0[0] + h1[0], p1 = h0[1] + h1[1];
+  const int E = a.pexp[chunk * a.n_pairs_pad + min((int)pair, a.n_pairs_pad - 1)];
+  const int NS = a.nsl[chunk * (uint32_t)a.n_ct + pair / kPairsPerTile];
+  const int sh0 = E - kFracBits + 8 * (kS - 0 - kSlo), sh1 = E - kFracBits + 8 * (kS - kSlo - (NS - kSlo));
+  a.partial[i] = ldexp((double)p0, sh0) + ldexp((double)p1, sh1);
+}
+
+// 0: the 8-wave kernel, 1: the wide tile, 2: the wide tile with each block's chunk split over two
+// blocks (ksplit 2). Option gram_tile forces one (1, 2, 3); unset, split when the wide launch is a
+// few rounds over the CUs with a last round at least a quarter empty (configs[2]'s 1,250 share: 640
+// blocks = 2.5 rounds -> 1,280 half blocks = 5), else rounds x cost between the other two.
+int oz_gram_mode(const ob_panel* p, int n_chunks, uint32_t nb_rep) {
   const uint32_t n_rt = (nb_rep + 3) / 4, n_ct = (uint32_t)p->oz_n_ct, n_dct = (n_ct + 1) / 2;
   const uint32_t wblocks = (uint32_t)n_chunks * n_rt * n_dct, blocks8 = (uint32_t)n_chunks * n_rt * n_ct;
   const uint32_t cus = (uint32_t)std::max(p->ctx->cus, 1);
-  const double kWideCost = 1.85;
-  const bool wide_pays = kWideCost * (double)((wblocks + cus - 1) / cus) <= (double)((blocks8 + cus - 1) / cus);
   const int tile = ob::opt_int(ob::Opt::GramTile, 0);
-  return tile == 2 || (tile != 1 && wide_pays);
+  if (tile >= 1 && tile <= 3) return tile - 1;
+  const uint32_t wrounds = (wblocks + cus - 1) / cus;
+  if (OB_OZ_W_SPLIT && wrounds <= 4 && wrounds * cus - wblocks >= cus / 4) return 2;
+  const double kWideCost = 1.85;
+  return kWideCost * (double)wrounds <= (double)((blocks8 + cus - 1) / cus) ? 1 : 0;
 }
+
+bool oz_wide(const ob_panel* p, int n_chunks, uint32_t nb_rep) { return oz_gram_mode(p, n_chunks, nb_rep) != 0; }
 
 int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t* counts, uint32_t nb_rep,
             uint32_t rep_pad, uint32_t n_reps, double* partial, hipStream_t s) {
@@ -1381,13 +1426,31 @@ int oz_gram(ob_panel* p, const uint32_t* d_chunks, int n_chunks, const uint32_t*
   // barrier and DMA work, with one wave per SIMD.)
   const uint32_t wblocks = (uint32_t)n_chunks * a.n_rt * (uint32_t)a.n_dct;
   const uint32_t blocks8 = (uint32_t)n_chunks * a.n_rt * (uint32_t)a.n_ct;
-  const bool wide = oz_wide(p, n_chunks, nb_rep);
-  p->timing.oz_wide = wide ? 1 : 0;
+  const int mode = oz_gram_mode(p, n_chunks, nb_rep);
+  const bool wide = mode != 0;
+  p->timing.oz_wide = mode;
   if (wide) {  // oz_gram_w_kernel: 4 waves, 256 replicates x 64 pairs per block
+    a.ksplit = mode == 2 ? 2 : 1;
+    a.n_chunks = n_chunks;
+    if (mode == 2) {
+      const size_t need = (size_t)2 * n_chunks * rep_pad * (size_t)p->e_pad * 2;
+      if (need > p->cap_oz_pint) {
+        (void)hipFree(p->d_oz_pint);
+        p->d_oz_pint = nullptr;
+        p->cap_oz_pint = 0;
+        OZ_HIP(hipMalloc(&p->d_oz_pint, need * sizeof(long long)));
+        p->cap_oz_pint = need;
+      }
+      a.pint = p->d_oz_pint;
+    }
     auto wlaunch = [&](auto kern) -> hipError_t {
       hipError_t e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kWLds);
       if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(kern, dim3(wblocks), dim3(256), kWLds, s, a);
+      hipLaunchKernelGGL(kern, dim3(wblocks * (uint32_t)a.ksplit), dim3(256), kWLds, s, a);
+      if (a.ksplit == 2) {
+        const size_t n = (size_t)n_chunks * rep_pad * (size_t)p->e_pad;
+        hipLaunchKernelGGL(oz_split_combine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+      }
       return hipGetLastError();
     };
 #if OB_TUNING  // timing ablations (gram_diag): wrong results by design

@@ -31,7 +31,8 @@ enum class Opt : int {
   MmBand0,
   GramDiag,     // timing ablations (OB_TUNING builds only): wrong results by design
   L1Diag,
-  GramTile,     // i8 Gram kernel: 1 = 8 waves, 32 pairs per block; 2 = 4 waves, 64 pairs (oz_gram_w_kernel)
+  GramTile,     // i8 Gram kernel: 1 = 8 waves, 32 pairs per block; 2 = 4 waves, 64 pairs (oz_gram_w_kernel);
+                // 3 = that wide tile with each chunk's sub-tiles split over two blocks
   DebugCountOverflow,  // nonzero: engine_counts raises its overflow word after the count kernel (tests the
                        // error path that a real count above 255 would take, p < 1e-500 per row)
   RsDouble,     // 1: two count-image / m1 buffers, so a boot's resample runs under the previous Gram;

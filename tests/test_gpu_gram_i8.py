@@ -339,9 +339,10 @@ def test_nonfinite_rows_touch_only_replicates_that_draw_them(ob, O):
 ])
 def test_wide_tile_gram_bitwise(ob, O, n, p, weighted, heavy, reps):
     """The two i8 Gram kernels (option gram_tile: 1 = 8 waves x 32 pairs, oz_gram_kernel; 2 = 4
-    waves x 64 pairs with AGPR accumulators, oz_gram_w_kernel) form the same exact integer slice
-    sums and combine them with the same two roundings, so their Grams are bitwise equal, partial
-    replicate tiles (reps % 256 != 0) and dead batches included."""
+    waves x 64 pairs with AGPR accumulators, oz_gram_w_kernel; 3 = that wide tile with each chunk's
+    sub-tiles split over two blocks whose int64 slice-group sums meet in oz_split_combine_kernel)
+    form the same exact integer slice sums and combine them with the same two roundings, so their
+    Grams are bitwise equal, partial replicate tiles (reps % 256 != 0) and dead batches included."""
     d = O.synthetic_panel(n, p, weighted, seed=n + p + 7)
     xa, xb = d["xa"].copy(), d["xb"].copy()
     if heavy:
@@ -351,13 +352,14 @@ def test_wide_tile_gram_bitwise(ob, O, n, p, weighted, heavy, reps):
     panel = ob.Panel(xa, d["ya"], xb, d["yb"], d["wa"], d["wb"])
     try:
         got = {}
-        for tile in (1, 2):
+        for tile in (1, 2, 3):
             with ob._native.option("gram_tile", tile):
                 got[tile] = panel.debug_gram(SEED, 5, reps, path=2)
                 t = panel.timing()
-                assert t["gram_path"] == 2
+                assert t["gram_path"] == 2 and t["oz_wide"] == tile - 1
         if heavy:
             assert 0 < t["oz_tiles6"] < t["oz_tiles"]
         assert np.array_equal(got[1], got[2], equal_nan=True)
+        assert np.array_equal(got[1], got[3], equal_nan=True)
     finally:
         panel.close()
