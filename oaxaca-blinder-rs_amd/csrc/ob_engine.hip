@@ -598,7 +598,10 @@ __device__ __forceinline__ void level2_draws(const GramArgs& a, const Work& w, u
 // image (kImgRow) their atomics fall on distinct banks. The part calls (m % 16 draws, one per
 // replicate) form one extra window, one lane per replicate. Same (call, replicate) -> draws as
 // level2_draws, so the same counts.
-constexpr uint32_t kCallMapCap = 2048;  // calls past the dense prefix a (tile, batch) map holds
+#ifndef OB_CNT_MAPCAP
+#define OB_CNT_MAPCAP 2048
+#endif
+constexpr uint32_t kCallMapCap = OB_CNT_MAPCAP;  // calls past the dense prefix a (tile, batch) map holds
 
 __device__ __forceinline__ void level2_map_draws(const GramArgs& a, const Work& w, uint32_t tile, uint32_t* cnt,
                                                  const uint32_t* mc, const uint32_t* cmap, uint32_t C,
