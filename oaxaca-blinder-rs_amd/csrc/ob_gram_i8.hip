@@ -858,6 +858,9 @@ constexpr int kWAgprTiles = 64;  // accumulator tiles (4 registers each) pinned 
 // 4 stages of B (two six-slice tiles: 24 KB; one seven-slice tile: 14 KB) + A (16 KB)
 constexpr size_t kWLds = kWNbuf * (size_t)(2 * 6 * 2 * 64 + 4 * 4 * 64) * 16;
 
+#ifndef OB_OZ_W_AFIRST
+#define OB_OZ_W_AFIRST 0  // 1: after the barrier, read the next step's A 0..3 with its first B block
+#endif
 #ifndef OB_OZ_W_SPLIT
 #define OB_OZ_W_SPLIT 1  // the engine may split a wide launch's chunks over two blocks (oz_gram_mode)
 #endif
@@ -1019,7 +1022,16 @@ __device__ __forceinline__ void oz_gram_w2_body(const OzArgs& a, unsigned char* 
         constexpr int pu = u - (U - POST);  // 0 .. POST - 1
         const int nbuf = (buf + 1) % kWNbuf;
         constexpr bool rb = !(DIAG & 128), ra = !(DIAG & 256);  // timing ablations: no B / A reads
-        if constexpr (POST == 2) {
+        if constexpr (POST == 2 && OB_OZ_W_AFIRST) {
+          // in the order the next step needs them: A 0..3 and its first B block in the first unit,
+          // A 4..7 (its second replicate half) in the second
+          if constexpr (pu == 0) {
+            if constexpr (ra && q < 4) ar[j ^ 1][q] = aread1(nbuf, q);
+            if constexpr (rb) fb[fnext][q] = bread1(nbuf, 0, q);
+          } else if constexpr (ra && q < 4) {
+            ar[j ^ 1][q + 4] = aread1(nbuf, q + 4);
+          }
+        } else if constexpr (POST == 2) {
           if constexpr (pu == 0) {
             if constexpr (rb) fb[fnext][q] = bread1(nbuf, 0, q);
           } else if constexpr (ra) {
